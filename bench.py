@@ -1,0 +1,403 @@
+#!/usr/bin/env python3
+"""bench.py — TULIPS checksum path on MI355X: device-resident GiB/s.
+
+Metric (BASELINE.json): "GiB/s checksummed (device-resident), batched 1500 B
+and 9000 B segments". Algorithmic bytes = sum of segment lengths.
+
+Workload (one "step" = one pass of the hot path over one batch):
+  configs[1] of BASELINE.json — a 65,536-segment batch of fixed 1500 B
+  segments, device-resident, checksummed by the gfx950 kernel through the
+  C ABI (tulips_csum_batch_fixed). Each rank holds 16 such batches
+  (1,048,576 segments = 1.57 GB, i.e. shard <rank> of the M8x1500 config,
+  configs[4]) and steps rotate through them, so every step streams from HBM
+  rather than from the 256 MB Infinity Cache. Per-rank work is fixed as N
+  grows (weak scaling); no data-path collective: segments are independent.
+
+Also reported (N=1, rank 0): F9000 (configs[2]) and ZIPF (configs[3]) rates,
+the plain streaming-read ceiling on the same buffer, the end-to-end host path
+(pinned H2D + kernel + D2H), and the reference CPU checksum timed on this
+box's cores (cpu_baseline).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1 under `python -m torch.distributed.run --nproc-per-node N ...`)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s checksummed (device-resident), batched 1500 B and 9000 B segments"
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E nameplate, GB/s (MI355X_MICROARCH.md)
+SEG, NSEG = 1500, 65536        # configs[1]
+NBATCH = 16                    # batches per rank = one M8x1500 shard
+DATA_SEED = 0x54554C495053
+ZIPF_SEED, ZIPF_RMAX = 0x5A495046, 8937
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=320)
+    p.add_argument("--warmup", type=int, default=32)
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip F9000/ZIPF/e2e/ceiling side measurements")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=1.5,
+                   help="wall seconds per CPU-baseline leg")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the timed launches from a captured HIP graph")
+    return p.parse_args()
+
+
+def zipf_lengths(n, seed=ZIPF_SEED, rmax=ZIPF_RMAX):
+    """SURVEY.md §8c Zipf lengths (data generation for the ZIPF side run)."""
+    golden = 0x9E3779B97F4A7C15
+    mask = (1 << 64) - 1
+    c = np.cumsum(np.arange(1, rmax + 1, dtype=np.float64) ** -1.1)
+    # sequential summation as in the spec (np.cumsum is sequential)
+    s = np.uint64(seed)
+    k = np.arange(1, n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = s + k * np.uint64(golden)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    del mask
+    u = (z >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    r = np.searchsorted(c, u * c[-1], side="left") + 1
+    return (63 + r).astype(np.uint16)
+
+
+def fnv1a_u16(v: np.ndarray) -> str:
+    h = 0xCBF29CE484222325
+    b = np.ascontiguousarray(v, dtype="<u2").view(np.uint8)
+    prime = 0x100000001B3
+    mask = (1 << 64) - 1
+    for x in b.tobytes():
+        h = ((h ^ x) * prime) & mask
+    return f"{h:016x}"
+
+
+def golden_digests():
+    path = os.path.join(ROOT, "tests", "golden", "digests.json")
+    try:
+        with open(path) as f:
+            return json.load(f)["batches"]
+    except OSError:
+        return {}
+
+
+class Timer:
+    """HIP events recorded on the stream the kernels are launched on."""
+
+    def __init__(self, torch, stream):
+        self.torch, self.stream = torch, stream
+
+    def __call__(self, fn, reps):
+        t = self.torch
+        a, b = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+        t.cuda.synchronize()
+        a.record(self.stream)
+        for i in range(reps):
+            fn(i)
+        b.record(self.stream)
+        b.synchronize()
+        return a.elapsed_time(b) / 1e3 / reps  # seconds per rep
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from tulips_amd import csum
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    lib = csum.lib
+
+    # ---- data: M8x1500 shard <rank>, 16 batches of 65,536 x 1500 B -------------
+    batch_bytes = NSEG * SEG
+    arena = torch.empty(NBATCH * batch_bytes + 256, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(arena, NBATCH * batch_bytes, seed=DATA_SEED,
+                       byte_off=rank * NBATCH * batch_bytes)
+    outs = torch.empty(NBATCH * NSEG, dtype=torch.uint16, device=dev)
+    base = arena.data_ptr()
+    optr = outs.data_ptr()
+    fixed = lib.tulips_csum_batch_fixed
+
+    def step(i):
+        b = i % NBATCH
+        rc = fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
+                   optr + b * NSEG * 2, NSEG, 0, sh)
+        if rc:
+            raise csum.CsumError(rc, "tulips_csum_batch_fixed")
+
+    for i in range(max(args.warmup, NBATCH)):
+        step(i)
+    torch.cuda.synchronize()
+
+    graph = None
+    if args.graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            gs = torch.cuda.current_stream().cuda_stream
+            for b in range(NBATCH):
+                fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
+                      optr + b * NSEG * 2, NSEG, 0, gs)
+        graph.replay()
+        torch.cuda.synchronize()
+
+    # ---- timed region ------------------------------------------------------
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_wall0 = time.perf_counter()
+    ev0.record(stream)
+    if graph is not None:
+        reps = max(1, args.steps // NBATCH)
+        for _ in range(reps):
+            graph.replay()
+        steps_done = reps * NBATCH
+    else:
+        for i in range(args.steps):
+            step(i)
+        steps_done = args.steps
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    t_wall = time.perf_counter() - t_wall0
+    if world > 1:
+        dist.barrier()
+    t_gpu = ev0.elapsed_time(ev1) / 1e3
+    t_local = max(t_gpu, 0.0)
+    if world > 1:
+        tt = torch.tensor([t_local], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+    else:
+        t_max = t_local
+
+    total_bytes = float(world) * steps_done * batch_bytes
+    value = total_bytes / t_max / GIB
+    per_launch_s = t_local / steps_done
+
+    # ---- parity of what was measured: shard digest vs the reference's -------
+    gold = golden_digests().get("M8x1500", {})
+    out_np = outs.cpu().numpy().view(np.uint16)
+    parity = None
+    if rank < 8 and gold.get("shards"):
+        parity = "ok" if fnv1a_u16(out_np) == gold["shards"][rank]["fnv1a64"] else "MISMATCH"
+    if world > 1:
+        ok = torch.tensor([1 if parity in ("ok", None) else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity = "ok" if int(ok.item()) == 1 else "MISMATCH"
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": steps_done,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_max / steps_done * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (SplitMix64 bytes, SURVEY.md §8c spec), device-resident",
+        "config": {
+            "workload": "F1500: 65,536 x 1500 B fixed-stride segments per step "
+                        "(BASELINE configs[1]); each rank rotates 16 batches = "
+                        "M8x1500 shard <rank> (1,048,576 segments, 1.57 GB)",
+            "global_batch": world * NSEG,
+            "segment_bytes": SEG,
+            "parallelism": f"shard{world}",
+            "launch": "graph" if graph is not None else "eager",
+        },
+        "parity": parity,
+        "wall_s_timed": round(t_wall, 4),
+    }
+
+    tun = csum.default_tuning(SEG)
+    achieved = batch_bytes / per_launch_s / 1e9
+    result["roofline"] = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": read_traffic("F1500"),
+        "kernel": f"csum_kernel<G={tun.group},U={tun.unroll},FixedSegs>",
+        "bytes_per_launch": batch_bytes,
+        "avg_launch_us": round(per_launch_s * 1e6, 3),
+    }
+
+    if world == 1 and rank == 0 and not args.no_extras:
+        result["extras"] = extras(torch, csum, dev, stream, arena, batch_bytes)
+
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(arena, batch_bytes, args.cpu_seconds)
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def read_traffic(workload):
+    """HBM bytes per launch from the committed PMC summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d[workload]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def extras(torch, csum, dev, stream, arena, batch_bytes):
+    timer = Timer(torch, stream)
+    sh = stream.cuda_stream
+    lib = csum.lib
+    ex = {}
+
+    # plain streaming read of the whole 1.57 GB shard: the measured ceiling
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    nbytes = NBATCH * batch_bytes
+    t = timer(lambda i: lib.tulips_csum_stream_read(arena.data_ptr(), nbytes,
+                                                    sink.data_ptr(), 0, sh), 10)
+    ex["stream_read_ceiling_GBps"] = round(nbytes / t / 1e9, 1)
+
+    # F9000 (configs[2]): 2 distinct 590 MB batches, rotated (> Infinity Cache)
+    L9 = 9000
+    b9 = NSEG * L9
+    a9 = torch.empty(2 * b9 + 256, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(a9, 2 * b9)
+    o9 = torch.empty(2 * NSEG, dtype=torch.uint16, device=dev)
+    fixed = lib.tulips_csum_batch_fixed
+
+    def f9(i):
+        b = i % 2
+        fixed(a9.data_ptr() + b * b9, L9, L9, None, None, None,
+              o9.data_ptr() + b * NSEG * 2, NSEG, 0, sh)
+    for i in range(4):
+        f9(i)
+    t = timer(f9, 40)
+    gold = golden_digests()
+    o = o9[:NSEG].cpu().numpy().view(np.uint16)
+    tun = csum.default_tuning(L9)
+    ex["F9000"] = {"GiBps": round(b9 / t / GIB, 1), "GBps": round(b9 / t / 1e9, 1),
+                   "frac_of_peak": round(b9 / t / 1e9 / HBM_PEAK_GBS, 4),
+                   "avg_launch_us": round(t * 1e6, 2),
+                   "geometry": f"G={tun.group},U={tun.unroll}",
+                   "parity": "ok" if fnv1a_u16(o) == gold.get("F9000", {}).get("fnv1a64")
+                   else "MISMATCH"}
+    del a9, o9
+
+    # ZIPF (configs[3]): 8 batches with the same lengths, different bytes
+    lens = zipf_lengths(NSEG)
+    offs = np.zeros(NSEG, dtype=np.uint64)
+    np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+    zb = int(lens.astype(np.int64).sum())
+    nz = 8
+    az = torch.empty(nz * zb + 256, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(az, nz * zb)
+    # batch 0 = the golden ZIPF arena (stream bytes [0, zb))
+    doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    dlens = torch.from_numpy(lens).to(dev)
+    oz = torch.empty(nz * NSEG, dtype=torch.uint16, device=dev)
+    batch = lib.tulips_csum_batch
+
+    def fz(i):
+        b = i % nz
+        batch(az.data_ptr() + b * zb, doffs.data_ptr(), dlens.data_ptr(), None, None,
+              None, oz.data_ptr() + b * NSEG * 2, NSEG, 0, sh)
+    for i in range(nz):
+        fz(i)
+    t = timer(fz, 80)
+    o = oz[:NSEG].cpu().numpy().view(np.uint16)
+    ex["ZIPF"] = {"GiBps": round(zb / t / GIB, 1), "Mseg_per_s": round(NSEG / t / 1e6, 1),
+                  "frac_of_peak": round(zb / t / 1e9 / HBM_PEAK_GBS, 4),
+                  "avg_launch_us": round(t * 1e6, 2), "geometry": "G=64 (one wave/segment)",
+                  "parity": "ok" if fnv1a_u16(o) == gold.get("ZIPF", {}).get("fnv1a64")
+                  else "MISMATCH"}
+    del az, oz
+
+    # end-to-end host path: F1500 batch from host memory, results back to host
+    host = arena[:batch_bytes].cpu().numpy()
+    pinned = torch.from_numpy(host.copy()).pin_memory()
+    hoffs = (np.arange(NSEG, dtype=np.uint64) * np.uint64(SEG))
+    hlens = np.full(NSEG, SEG, dtype=np.uint16)
+    e2e = {}
+    with csum.HostContext(torch.cuda.current_device()) as ctx:
+        for name, src in (("pinned", pinned.data_ptr()), ("pageable", host)):
+            ctx.batch(src, hoffs, hlens)
+            reps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < 1.0 or reps < 3:
+                out = ctx.batch(src, hoffs, hlens)
+                reps += 1
+            t = (time.perf_counter() - t0) / reps
+            e2e[name] = {"GiBps": round(batch_bytes / t / GIB, 2),
+                         "ms_per_batch": round(t * 1e3, 3),
+                         "parity": "ok" if fnv1a_u16(out) == gold.get("F1500", {}).get(
+                             "fnv1a64") else "MISMATCH"}
+    ex["e2e_host_F1500"] = e2e
+    return ex
+
+
+def cpu_baseline(arena, batch_bytes, seconds):
+    """The reference CPU checksum (oracle/_ref: the reference's own src/stack
+    compiled with -O3 -mssse3), else the C restatement, on this box's cores,
+    over the first F1500 batch of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle, Reference  # noqa: E402 (cpu_baseline leg only)
+    if Reference.available():
+        impl, kind = Reference(), "reference"
+    else:
+        impl, kind = Oracle(), "port"
+    host = arena[:batch_bytes].cpu().numpy()
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu))
+
+    def rate(nt):
+        impl.batch(host, stride=SEG, fixed_len=SEG, n=NSEG, nthreads=nt)
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            impl.batch(host, stride=SEG, fixed_len=SEG, n=NSEG, nthreads=nt)
+            reps += 1
+        return reps * batch_bytes / (time.perf_counter() - t0) / GIB, reps
+
+    r1, n1 = rate(1)
+    rN, nN = rate(threads)
+    return {"value": round(rN, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "value_1core": round(r1, 3),
+            "sample": f"F1500 batch 0 (65,536 x 1500 B = 98.3 MB) copied to host; "
+                      f"{nN} passes on {threads} pinned threads + {n1} passes on 1 "
+                      f"thread, ~{seconds:.1f} s wall each; g++ -O3 -mssse3"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+/*
+ * tulips_csum.h — C ABI of the MI355X-native TULIPS checksum path.
+ *
+ * This is the drop-in boundary for TULIPS' Internet/TCP one's-complement
+ * checksum (xenogenics/tulips @ 2024-12-20, src/stack). Every entry point
+ * takes plain pointers and sizes; no HIP or torch types appear here, so the
+ * header can be bound from C, C++, ctypes, cgo or JNI unchanged. Streams are
+ * passed as `void*` (a hipStream_t; NULL = the legacy default stream).
+ *
+ * What each entry point replaces in the reference:
+ *
+ *   tulips_csum_host          tulips::stack::utils::checksum
+ *                             (include/tulips/stack/Utils.h:10-11,
+ *                              src/stack/Utils.cpp:14-42). The library also
+ *                             exports that exact C++ symbol,
+ *                             _ZN6tulips5stack5utils8checksumEtPKht.
+ *   tulips_csum_ipv4_host     tulips::stack::ipv4::checksum
+ *                             (include/tulips/stack/IPv4.h:90-92,
+ *                              src/stack/IPv4.cpp:75-82); C++ symbol exported.
+ *   tulips_csum_icmpv4_host   tulips::stack::icmpv4::checksum
+ *                             (include/tulips/stack/ICMPv4.h:37,
+ *                              src/stack/ICMPv4.cpp:10-15); C++ symbol exported.
+ *   tulips_csum_tcp_host      tulips::stack::tcpv4::Processor::checksum
+ *                             (private static, include/tulips/stack/tcpv4/
+ *                              Processor.h:142-145, src/stack/tcpv4/
+ *                              Processor.cpp:337-357).
+ *   tulips_csum_batch         the per-frame loop of those calls
+ *   tulips_csum_batch_fixed   (src/stack/tcpv4/Processor.cpp:121 verify,
+ *                             src/stack/tcpv4/Send.cpp:448 generate,
+ *                             src/stack/ipv4/Processor.cpp:95 verify,
+ *                             src/stack/ipv4/Producer.cpp:81 generate), done
+ *                             for a whole batch of device-resident segments by
+ *                             HIP kernels on gfx950.
+ *   tulips_csum_batch_host    the same for host-resident segments (pinned
+ *                             staging, H2D, kernel, D2H), the path a transport
+ *                             poll burst would take (src/transport/ofed/
+ *                             Device.cpp:505-545).
+ *
+ * Semantics (bit-exact with the reference):
+ *   RAW   out = utils::checksum(seed, seg, len)          (uncomplemented, host order)
+ *   INET  out = r == 0 ? 0xffff : htons(r), r = RAW      (ipv4/icmpv4 wrappers)
+ *   TCP   r = utils::checksum(pseudo, seg, len) with pseudo = checksum(
+ *         checksum((len + 6) & 0xffff, src, 4), dst, 4); out as INET
+ *   | TULIPS_CSUM_COMPLEMENT stores ~out (what the generate sites write into
+ *         the header field, src/stack/tcpv4/Send.cpp:449, ipv4/Producer.cpp:81)
+ *   A received segment verifies iff its INET/TCP result is 0xffff
+ *   (src/stack/tcpv4/Processor.cpp:122, src/stack/ipv4/Processor.cpp:96).
+ *
+ * Return values are tulips::Status values (include/tulips/api/Status.h:8-44).
+ *
+ * Ownership: device pointers are borrowed until the work queued on `stream`
+ * completes; nothing is retained after that. Threading: all entry points are
+ * reentrant; a context (tulips_csum_ctx) must be used by one thread at a time.
+ */
+#ifndef TULIPS_CSUM_H
+#define TULIPS_CSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* tulips::Status (include/tulips/api/Status.h:8-44) */
+#define TULIPS_STATUS_OK 0
+#define TULIPS_STATUS_INVALID_ARGUMENT 1
+#define TULIPS_STATUS_HARDWARE_ERROR 2
+#define TULIPS_STATUS_NO_MORE_RESOURCES 3
+#define TULIPS_STATUS_UNSUPPORTED_OPERATION 18
+
+/* Modes (low byte) and flags. */
+#define TULIPS_CSUM_RAW 0u
+#define TULIPS_CSUM_INET 1u
+#define TULIPS_CSUM_TCP 2u
+#define TULIPS_CSUM_MODE_MASK 0xffu
+#define TULIPS_CSUM_COMPLEMENT 0x100u
+
+/* Largest segment: the reference's `const uint16_t len` parameter. */
+#define TULIPS_CSUM_MAX_SEGMENT 65535u
+
+/* ---- host scalar drop-ins (no GPU involved) ------------------------------ */
+
+uint16_t tulips_csum_host(uint16_t seed, const uint8_t* data, uint16_t len);
+uint16_t tulips_csum_ipv4_host(const uint8_t* header20);
+uint16_t tulips_csum_icmpv4_host(const uint8_t* header8);
+/* src/dst: ipv4::Address::m_data, i.e. the 4 wire bytes as a native uint32. */
+uint16_t tulips_csum_tcp_host(uint32_t src, uint32_t dst, uint16_t len,
+                              const uint8_t* segment);
+
+/* ---- device-resident batches --------------------------------------------- */
+
+/*
+ * Segment i is base[offsets[i] .. offsets[i] + lengths[i]).
+ * `seeds` (RAW/INET only) may be NULL = all zero. `src`/`dst` are required
+ * for TULIPS_CSUM_TCP and ignored otherwise. All arrays are device pointers.
+ * n == 0 is a no-op returning OK. Segments may overlap and start at any byte.
+ */
+int tulips_csum_batch(const uint8_t* base, const uint64_t* offsets,
+                      const uint16_t* lengths, const uint16_t* seeds,
+                      const uint32_t* src, const uint32_t* dst, uint16_t* out,
+                      uint32_t n, uint32_t mode, void* stream);
+
+/* Segment i is base[i*stride .. i*stride + length); length <= 65535. */
+int tulips_csum_batch_fixed(const uint8_t* base, uint64_t stride,
+                            uint32_t length, const uint16_t* seeds,
+                            const uint32_t* src, const uint32_t* dst,
+                            uint16_t* out, uint32_t n, uint32_t mode,
+                            void* stream);
+
+/*
+ * Number of segments in [0, n) whose result (as selected by mode, INET or
+ * TCP) is not 0xffff, i.e. that fail verification; written to *bad_count
+ * (device pointer, uint32). `out` may be NULL when only the count is wanted.
+ */
+int tulips_csum_verify(const uint8_t* base, const uint64_t* offsets,
+                       const uint16_t* lengths, const uint32_t* src,
+                       const uint32_t* dst, uint16_t* out,
+                       uint32_t* bad_count, uint32_t n, uint32_t mode,
+                       void* stream);
+
+/* ---- host-resident batches (end-to-end path) ----------------------------- */
+
+typedef struct tulips_csum_ctx tulips_csum_ctx;
+
+/* A context owns a stream, pinned staging and device buffers sized for
+ * `chunk_bytes` of segment bytes per pipeline stage (0 = 64 MiB). */
+int tulips_csum_ctx_create(int device, uint64_t chunk_bytes,
+                           tulips_csum_ctx** ctx);
+int tulips_csum_ctx_destroy(tulips_csum_ctx* ctx);
+
+/* All pointers are host pointers; blocks until `out` holds every result. */
+int tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
+                           const uint64_t* offsets, const uint16_t* lengths,
+                           const uint16_t* seeds, const uint32_t* src,
+                           const uint32_t* dst, uint16_t* out, uint32_t n,
+                           uint32_t mode);
+
+/* ---- misc ---------------------------------------------------------------- */
+
+const char* tulips_csum_status_string(int status);
+const char* tulips_csum_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TULIPS_CSUM_H */

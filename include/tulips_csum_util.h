@@ -1,0 +1,54 @@
+/*
+ * tulips_csum_util.h — tuning and measurement entry points of the checksum
+ * library (not part of the reference surface; used by bench.py and tests).
+ */
+#ifndef TULIPS_CSUM_UTIL_H
+#define TULIPS_CSUM_UTIL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Explicit kernel geometry. Zero fields pick the library default. */
+typedef struct tulips_csum_tuning
+{
+  int32_t group;       /* lanes per segment: 16, 32 or 64 */
+  int32_t unroll;      /* 16-byte chunks in flight per lane: 2, 4 or 8 */
+  int32_t nontemporal; /* 1 = nt loads, 0 = default cache policy, -1 = default */
+  uint32_t max_blocks; /* grid cap; 0 = default */
+} tulips_csum_tuning;
+
+/* The geometry tulips_csum_batch_fixed / tulips_csum_batch would pick. */
+int tulips_csum_default_tuning(uint32_t fixed_length, int variable,
+                               tulips_csum_tuning* out);
+
+int tulips_csum_batch_fixed_tuned(const uint8_t* base, uint64_t stride,
+                                  uint32_t length, const uint16_t* seeds,
+                                  const uint32_t* src, const uint32_t* dst,
+                                  uint16_t* out, uint32_t n, uint32_t mode,
+                                  const tulips_csum_tuning* tuning,
+                                  void* stream);
+
+int tulips_csum_batch_tuned(const uint8_t* base, const uint64_t* offsets,
+                            const uint16_t* lengths, const uint16_t* seeds,
+                            const uint32_t* src, const uint32_t* dst,
+                            uint16_t* out, uint32_t n, uint32_t mode,
+                            const tulips_csum_tuning* tuning, void* stream);
+
+/* Device fill with the SplitMix64 byte stream of SURVEY.md §8c: dst[i] =
+ * stream byte (byte_off + i). Used to materialise synthetic arenas in HBM. */
+int tulips_csum_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
+                              uint64_t byte_off, void* stream);
+
+/* Plain 16-byte streaming read of [p, p + nbytes): the measured read
+ * ceiling that the checksum kernel's HBM rate is compared against. */
+int tulips_csum_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
+                            uint32_t max_blocks, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TULIPS_CSUM_UTIL_H */

@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures from the REFERENCE itself.
+
+Every expected value here is produced by ``oracle/_ref/libtulips_ref.so``,
+i.e. the reference's own ``src/stack`` translation units (Utils.cpp, IPv4.cpp,
+ICMPv4.cpp, tcpv4/Processor.cpp, ...) compiled by ``oracle/Makefile`` from
+``/root/reference``. Run it in the build container (where /root/reference
+exists):
+
+    make -C oracle && python tests/golden/make_golden.py
+
+Outputs (small, committed):
+  kat.json          single-call known answers for a1/a2/a5/a6
+  adversarial.npz   a 192 KiB random arena + edge-case segments (every length
+                    class, every start alignment 0..15, odd offsets, seeds,
+                    overlapping segments) with the reference's outputs per mode
+  digests.json      FNV-1a-64 / sum digests of the SURVEY.md §8c batches
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+from oracle import (DATA_SEED, MODE_INET, MODE_RAW, MODE_TCP,  # noqa: E402
+                    FLAG_COMPLEMENT, Oracle, Reference, fixed_offsets, ip4,
+                    packed_offsets)
+
+NTHREADS = min(8, os.cpu_count() or 1)
+
+
+def kat(ref: Reference) -> list:
+    rows = []
+
+    def a1(seed, data):
+        rows.append({"fn": "checksum", "seed": seed, "data": data.hex(),
+                     "expect": ref.checksum(seed, data)})
+
+    # SURVEY.md §8a known answers (re-derived here from the reference)
+    a1(0, bytes.fromhex("0001f203f4f5f6f7"))          # RFC 1071 example
+    a1(0x1234, b"")
+    a1(0, bytes.fromhex("0001f2"))
+    a1(0, bytes.fromhex("ffff0001"))
+    a1(0, bytes.fromhex("ffff"))
+    a1(0, bytes.fromhex("ffffffff"))
+    a1(0xFFFF, bytes(4))
+    a1(0, bytes(4))
+    a1(1, bytes.fromhex("ffff"))
+    a1(0, b"")
+    a1(0xFFFF, b"")
+    a1(0, b"\x80")
+    a1(0xFFFF, b"\xff")
+    a1(0x0001, b"\xff\xfe")
+    rng = np.random.default_rng(1071)
+    for L in list(range(0, 40)) + [63, 64, 65, 127, 128, 129, 1499, 1500, 1501]:
+        for seed in (0, 1, 0x7FFF, 0xFFFE, 0xFFFF, int(rng.integers(0, 65536))):
+            a1(seed, rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+    for L in (2, 3, 8, 9, 20):
+        a1(0, b"\xff" * L)
+        a1(0xFFFF, b"\xff" * L)
+        a1(0, b"\x00" * L)
+
+    ip = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
+    rows.append({"fn": "ipv4", "data": ip.hex(), "expect": ref.ipv4_checksum(ip)})
+    v = ref.ipv4_checksum(ip)
+    stored = (~v) & 0xFFFF  # ipv4/Producer.cpp:81 writes ~checksum
+    ip2 = ip[:10] + stored.to_bytes(2, "little") + ip[12:]
+    rows.append({"fn": "ipv4", "data": ip2.hex(), "expect": ref.ipv4_checksum(ip2)})
+    for _ in range(16):
+        h = rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
+        rows.append({"fn": "ipv4", "data": h.hex(), "expect": ref.ipv4_checksum(h)})
+
+    icmp = bytes.fromhex("0800000012340001")
+    rows.append({"fn": "icmpv4", "data": icmp.hex(), "expect": ref.icmpv4_checksum(icmp)})
+    for _ in range(16):
+        h = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+        rows.append({"fn": "icmpv4", "data": h.hex(), "expect": ref.icmpv4_checksum(h)})
+
+    syn = bytes.fromhex("22b8270f000000010000000050022000" "00000000")
+    src, dst = ip4(10, 1, 0, 1), ip4(10, 1, 0, 2)
+    rows.append({"fn": "tcp", "src": src, "dst": dst, "data": syn.hex(),
+                 "expect": ref.tcp_checksum(src, dst, syn)})
+    for L in (0, 1, 20, 21, 40, 61, 1460, 1480):
+        for _ in range(3):
+            s = int(rng.integers(0, 2**32)); d = int(rng.integers(0, 2**32))
+            seg = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+            rows.append({"fn": "tcp", "src": s, "dst": d, "data": seg.hex(),
+                         "expect": ref.tcp_checksum(s, d, seg)})
+    # the uint16 `len + 6` wrap of Processor.cpp:346 (len > 65529)
+    # (segment bytes given by the SplitMix64 stream spec to keep the file small)
+    orc = Oracle()
+    for L in (65529, 65530, 65531, 65535):
+        seg = orc.splitmix_bytes(L, seed=L).tobytes()
+        s = int(rng.integers(0, 2**32)); d = int(rng.integers(0, 2**32))
+        rows.append({"fn": "tcp", "src": s, "dst": d, "data_splitmix": [L, L],
+                     "expect": ref.tcp_checksum(s, d, seg)})
+    return rows
+
+
+EDGE_LENGTHS = [0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 65,
+                127, 128, 129, 255, 256, 257, 1023, 1024, 1025, 1499, 1500,
+                1501, 4095, 4096, 4097, 8999, 9000, 9001, 16383, 16384, 16385,
+                65534, 65535]
+
+
+def adversarial(ref: Reference, orc: Oracle) -> dict:
+    rng = np.random.default_rng(8937)
+    arena_n = 192 * 1024
+    arena = orc.splitmix_bytes(arena_n, seed=0xADE5A11)
+    offs, lens = [], []
+    for L in EDGE_LENGTHS:
+        for start in range(0, 18):          # every alignment mod 16, plus 16, 17
+            base = int(rng.integers(0, arena_n - L - 64)) & ~63
+            offs.append(base + start)
+            lens.append(L)
+    for _ in range(2000):                   # random segments, random alignment
+        L = int(rng.integers(0, 20000))
+        offs.append(int(rng.integers(0, arena_n - L)))
+        lens.append(L)
+    offs = np.array(offs, dtype=np.uint64)
+    lens = np.array(lens, dtype=np.uint16)
+    n = len(offs)
+    seeds = rng.integers(0, 65536, n, dtype=np.uint16)
+    seeds[:64] = 0
+    seeds[64:128] = 0xFFFF
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    out = {}
+    kw = dict(nthreads=NTHREADS)
+    out["raw_noseed"] = ref.batch(arena, offs, lens, mode=MODE_RAW, **kw)
+    out["raw_seed"] = ref.batch(arena, offs, lens, seeds=seeds, mode=MODE_RAW, **kw)
+    out["inet_seed"] = ref.batch(arena, offs, lens, seeds=seeds, mode=MODE_INET, **kw)
+    out["tcp"] = ref.batch(arena, offs, lens, src=src, dst=dst, mode=MODE_TCP, **kw)
+    out["tcp_complement"] = ref.batch(arena, offs, lens, src=src, dst=dst,
+                                      mode=MODE_TCP | FLAG_COMPLEMENT, **kw)
+    # constant arenas: the 0x0000 / 0xffff representation paths
+    zeros = np.zeros(arena_n, dtype=np.uint8)
+    ones = np.full(arena_n, 0xFF, dtype=np.uint8)
+    out["zeros_raw_seed"] = ref.batch(zeros, offs, lens, seeds=seeds, mode=MODE_RAW, **kw)
+    out["zeros_inet_noseed"] = ref.batch(zeros, offs, lens, mode=MODE_INET, **kw)
+    out["ones_raw_seed"] = ref.batch(ones, offs, lens, seeds=seeds, mode=MODE_RAW, **kw)
+    out["ones_tcp"] = ref.batch(ones, offs, lens, src=src, dst=dst, mode=MODE_TCP, **kw)
+    return dict(arena=arena, offsets=offs, lengths=lens, seeds=seeds, src=src,
+                dst=dst, **{"expect_" + k: v for k, v in out.items()})
+
+
+def digest(orc, v):
+    return {"fnv1a64": f"{orc.fnv1a_u16(v):016x}", "sum": int(v.astype(np.int64).sum())}
+
+
+def digests(ref: Reference, orc: Oracle) -> dict:
+    N = 65536
+    d = {"spec": "SURVEY.md §8c: SplitMix64 arena seed 0x54554C495053, packed; "
+                 "FNV-1a-64 over u16 outputs (LE bytes); TCP src 10.1.0.1 dst 10.1.0.2",
+         "batches": {}}
+    src = np.full(N, ip4(10, 1, 0, 1), dtype=np.uint32)
+    dst = np.full(N, ip4(10, 1, 0, 2), dtype=np.uint32)
+    kw = dict(nthreads=NTHREADS)
+    for L, stride in ((1500, 1500), (1500, 2048), (9000, 9000), (9000, 9216), (64, 64)):
+        arena = orc.splitmix_bytes(N * stride)
+        v = ref.batch(arena, stride=stride, fixed_len=L, n=N, mode=MODE_RAW, **kw)
+        name = f"F{L}" + ("" if stride == L else f"s{stride}")
+        d["batches"][name] = dict(n=N, length=L, stride=stride, mode="raw", **digest(orc, v))
+        if stride == L and L in (1500, 9000):
+            v = ref.batch(arena, stride=stride, fixed_len=L, n=N, mode=MODE_TCP,
+                          src=src, dst=dst, **kw)
+            d["batches"][name + "-tcp"] = dict(n=N, length=L, stride=stride, mode="tcp",
+                                               **digest(orc, v))
+    lens = orc.zipf_lengths(N)
+    offs = packed_offsets(lens)
+    arena = orc.splitmix_bytes(int(lens.astype(np.int64).sum()))
+    d["zipf_lengths"] = {"fnv1a64": f"{orc.fnv1a_u16(lens):016x}",
+                         "total": int(lens.astype(np.int64).sum()),
+                         "min": int(lens.min()), "max": int(lens.max()),
+                         "odd": int((lens & 1).sum()), "first4": [int(x) for x in lens[:4]]}
+    v = ref.batch(arena, offs, lens, mode=MODE_RAW, **kw)
+    d["batches"]["ZIPF"] = dict(n=N, mode="raw", **digest(orc, v))
+    v = ref.batch(arena, offs, lens, mode=MODE_TCP, src=src, dst=dst, **kw)
+    d["batches"]["ZIPF-tcp"] = dict(n=N, mode="tcp", **digest(orc, v))
+    # M8x1500: 8 contiguous shards of 1,048,576 segments (8.4 M total)
+    shard_n, L = 1 << 20, 1500
+    shard_digests, all_out = [], []
+    for r in range(8):
+        arena = orc.splitmix_bytes(shard_n * L, byte_off=r * shard_n * L)
+        v = ref.batch(arena, stride=L, fixed_len=L, n=shard_n, mode=MODE_RAW, **kw)
+        shard_digests.append(digest(orc, v))
+        all_out.append(v)
+        del arena
+    full = np.concatenate(all_out)
+    d["batches"]["M8x1500"] = dict(n=8 * shard_n, length=L, stride=L, mode="raw",
+                                   shards=shard_digests, **digest(orc, full))
+    # one 65,536-segment batch of each shard: bench.py's rotating F1500 steps
+    return d
+
+
+def main():
+    ref = Reference()
+    orc = Oracle()
+    rows = kat(ref)
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump({"source": "oracle/_ref/libtulips_ref.so (reference src/stack compiled)",
+                   "cases": rows}, f, indent=0)
+    adv = adversarial(ref, orc)
+    np.savez_compressed(os.path.join(HERE, "adversarial.npz"), **adv)
+    dg = digests(ref, orc)
+    with open(os.path.join(HERE, "digests.json"), "w") as f:
+        json.dump(dg, f, indent=1)
+    print(f"kat: {len(rows)} cases; adversarial: {len(adv['offsets'])} segments; "
+          f"digests: {sorted(dg['batches'])}")
+
+
+if __name__ == "__main__":
+    main()

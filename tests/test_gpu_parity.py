@@ -1,0 +1,286 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the reference.
+
+Expected values come from the committed fixtures (computed by the reference's
+own compiled src/stack, tests/golden/make_golden.py) and, for fresh random
+cases, from the CPU restatement oracle/csum_oracle.c (itself pinned to the
+reference by tests/test_oracle.py). Bar: bit-exact.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from oracle import (MODE_INET, MODE_RAW, MODE_TCP, FLAG_COMPLEMENT,  # noqa: E402
+                    fixed_offsets, ip4, packed_offsets)
+
+import tulips_amd  # noqa: E402
+from tulips_amd import csum  # noqa: E402
+
+DEV = "cuda:0"
+
+GEOMETRIES = [(g, u, nt) for g in (16, 32, 64) for u in (2, 4, 8) for nt in (0, 1)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+def d(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.view(dtype)
+    return t.to(DEV)
+
+
+def h(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def u16(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint16)
+
+
+def fnv(oracle, t):
+    torch.cuda.synchronize()
+    return f"{oracle.fnv1a_u16(u16(t)):016x}"
+
+
+# -- fixtures ---------------------------------------------------------------
+def test_adversarial_all_modes_default_geometry(golden):
+    adv = golden.adversarial()
+    offs, lens = d(adv["offsets"]), d(adv["lengths"])
+    seeds, src, dst = d(adv["seeds"]), d(adv["src"]), d(adv["dst"])
+    for name, (kind, mode, use_seeds) in golden.ADV_CASES.items():
+        arena = d(golden.adv_arena(adv, kind))
+        out = tulips_amd.batch(arena, offs, lens, seeds=seeds if use_seeds else None,
+                               src=src, dst=dst, mode=mode)
+        np.testing.assert_array_equal(u16(out), adv["expect_" + name], err_msg=name)
+
+
+@pytest.mark.parametrize("geom", GEOMETRIES)
+def test_adversarial_every_geometry(golden, geom):
+    g, u, nt = geom
+    adv = golden.adversarial()
+    arena = d(adv["arena"])
+    offs, lens = d(adv["offsets"]), d(adv["lengths"])
+    src, dst, seeds = d(adv["src"]), d(adv["dst"]), d(adv["seeds"])
+    for max_blocks in (0, 7):
+        t = csum.Tuning(group=g, unroll=u, nontemporal=nt, max_blocks=max_blocks)
+        out = tulips_amd.batch(arena, offs, lens, src=src, dst=dst, mode=MODE_TCP, tuning=t)
+        np.testing.assert_array_equal(u16(out), adv["expect_tcp"])
+        out = tulips_amd.batch(arena, offs, lens, seeds=seeds, mode=MODE_RAW, tuning=t)
+        np.testing.assert_array_equal(u16(out), adv["expect_raw_seed"])
+
+
+def test_kat_through_device_batch(golden, oracle):
+    """Every single-call known answer, as one device batch per function."""
+    cases = golden.kat()
+    for fn, mode in (("checksum", MODE_RAW), ("ipv4", MODE_INET), ("icmpv4", MODE_INET),
+                     ("tcp", MODE_TCP)):
+        rows = [c for c in cases if c["fn"] == fn]
+        datas = [golden.kat_data(c, oracle) for c in rows]
+        if fn == "ipv4":
+            datas = [x[:20] for x in datas]
+        if fn == "icmpv4":
+            datas = [x[:8] for x in datas]
+        lens = np.array([len(x) for x in datas], dtype=np.uint16)
+        offs = packed_offsets(lens) + np.uint64(1)   # odd base: flips every parity
+        arena = np.frombuffer(b"\x5a" + b"".join(datas) + b"\x5a" * 16, dtype=np.uint8)
+        seeds = np.array([c.get("seed", 0) for c in rows], dtype=np.uint16)
+        src = np.array([c.get("src", 0) for c in rows], dtype=np.uint32)
+        dst = np.array([c.get("dst", 0) for c in rows], dtype=np.uint32)
+        out = tulips_amd.batch(d(arena), d(offs), d(lens), seeds=d(seeds), src=d(src),
+                               dst=d(dst), mode=mode)
+        np.testing.assert_array_equal(u16(out), np.array([c["expect"] for c in rows],
+                                                         dtype=np.uint16), err_msg=fn)
+
+
+# -- SURVEY.md §8c batches: digests at full size -------------------------------
+def _fill(nbytes, byte_off=0):
+    buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=DEV)
+    csum.fill_splitmix(buf, nbytes, byte_off=byte_off)
+    return buf
+
+
+def test_device_fill_matches_spec(oracle):
+    buf = _fill(1 << 20)
+    np.testing.assert_array_equal(h(buf)[: 1 << 20], oracle.splitmix_bytes(1 << 20))
+    for off in (1, 3, 8, 12345):
+        buf = torch.zeros(4096, dtype=torch.uint8, device=DEV)
+        csum.fill_splitmix(buf[5:], 1000, byte_off=off)
+        got = h(buf)
+        np.testing.assert_array_equal(got[5:1005], oracle.splitmix_bytes(1000, byte_off=off))
+        assert not got[:5].any() and not got[1005:].any()
+
+
+@pytest.mark.parametrize("name", ["F1500", "F9000", "F1500s2048", "F9000s9216", "F64",
+                                  "F1500-tcp", "F9000-tcp"])
+def test_fixed_digest(golden, oracle, name):
+    b = golden.digests()["batches"][name]
+    n, L, stride = b["n"], b["length"], b["stride"]
+    arena = _fill(n * stride)
+    if b["mode"] == "tcp":
+        src = d(np.full(n, ip4(10, 1, 0, 1), np.uint32))
+        dst = d(np.full(n, ip4(10, 1, 0, 2), np.uint32))
+        out = tulips_amd.batch_fixed(arena, stride, L, n, src=src, dst=dst, mode=MODE_TCP)
+    else:
+        out = tulips_amd.batch_fixed(arena, stride, L, n)
+    assert fnv(oracle, out) == b["fnv1a64"]
+    # the variable-length entry point on the same segments agrees
+    offs = d(fixed_offsets(n, stride))
+    lens = d(np.full(n, L, np.uint16))
+    if b["mode"] != "tcp":
+        out2 = tulips_amd.batch(arena, offs, lens)
+        assert fnv(oracle, out2) == b["fnv1a64"]
+
+
+@pytest.mark.parametrize("name", ["ZIPF", "ZIPF-tcp"])
+def test_zipf_digest(golden, oracle, name):
+    b = golden.digests()["batches"][name]
+    n = b["n"]
+    lens = oracle.zipf_lengths(n)
+    offs = packed_offsets(lens)
+    arena = _fill(int(lens.astype(np.int64).sum()))
+    kw = {}
+    if b["mode"] == "tcp":
+        kw = dict(src=d(np.full(n, ip4(10, 1, 0, 1), np.uint32)),
+                  dst=d(np.full(n, ip4(10, 1, 0, 2), np.uint32)), mode=MODE_TCP)
+    for g in (None, 16, 32, 64):
+        t = None if g is None else csum.Tuning(group=g, unroll=4, nontemporal=-1, max_blocks=0)
+        out = tulips_amd.batch(arena, d(offs), d(lens), tuning=t, **kw)
+        assert fnv(oracle, out) == b["fnv1a64"], g
+
+
+def test_m8_all_shards(golden, oracle):
+    """M8x1500 (8,388,608 segments, 12.6 GB): every shard's digest, each shard
+    materialised in HBM at its global byte offset, as one rank of the 8-GPU
+    run would hold it."""
+    b = golden.digests()["batches"]["M8x1500"]
+    shard_n, L = b["n"] // 8, 1500
+    arena = torch.empty(shard_n * L + 64, dtype=torch.uint8, device=DEV)
+    outs = []
+    for r in range(8):
+        csum.fill_splitmix(arena, shard_n * L, byte_off=r * shard_n * L)
+        out = tulips_amd.batch_fixed(arena, L, L, shard_n)
+        assert fnv(oracle, out) == b["shards"][r]["fnv1a64"], r
+        outs.append(u16(out))
+    assert f"{oracle.fnv1a_u16(np.concatenate(outs)):016x}" == b["fnv1a64"]
+
+
+# -- fresh random cases vs the restatement ----------------------------------
+def test_random_vs_oracle_all_alignments(oracle):
+    rng = np.random.default_rng(355)
+    arena = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    n = 30000
+    lens = rng.integers(0, 12000, n).astype(np.uint16)
+    lens[:500] = rng.integers(0, 64, 500)
+    lens[500:600] = rng.integers(60000, 65536, 100)
+    offs = np.array([rng.integers(0, len(arena) - int(L)) for L in lens], dtype=np.uint64)
+    seeds = rng.integers(0, 65536, n, dtype=np.uint16)
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    da, do, dl = d(arena), d(offs), d(lens)
+    ds_, dsrc, ddst = d(seeds), d(src), d(dst)
+    for mode in (MODE_RAW, MODE_INET, MODE_TCP, MODE_RAW | FLAG_COMPLEMENT,
+                 MODE_TCP | FLAG_COMPLEMENT):
+        exp = oracle.batch(arena, offs, lens, seeds=seeds, src=src, dst=dst, mode=mode,
+                           nthreads=8)
+        got = tulips_amd.batch(da, do, dl, seeds=ds_, src=dsrc, dst=ddst, mode=mode)
+        np.testing.assert_array_equal(u16(got), exp, err_msg=hex(mode))
+
+
+@pytest.mark.parametrize("L", [0, 1, 2, 3, 15, 16, 17, 63, 64, 65, 1499, 1500, 1501, 8999,
+                               9000, 9001, 65535])
+@pytest.mark.parametrize("base_off", [0, 1, 2, 7, 15])
+def test_fixed_lengths_and_base_alignment(oracle, L, base_off):
+    n = 257
+    stride = max(L, 1) + 3  # odd-ish stride: every segment a different alignment
+    rng = np.random.default_rng(L * 31 + base_off)
+    arena = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+    exp = oracle.batch(arena[base_off:], stride=stride, fixed_len=L, n=n, mode=MODE_RAW)
+    da = d(arena)
+    for g in (16, 32, 64):
+        for u in (2, 8):
+            t = csum.Tuning(group=g, unroll=u, nontemporal=0, max_blocks=0)
+            got = tulips_amd.batch_fixed(da, stride, L, n, tuning=t, base_offset=base_off)
+            np.testing.assert_array_equal(u16(got), exp, err_msg=f"g{g} u{u}")
+
+
+# -- verify and generate (the stack's two call patterns) ------------------------
+def test_generate_then_verify_roundtrip_and_corruption(oracle):
+    """Generate side writes ~csum into the TCP header (Send.cpp:448-449);
+    the receive side accepts iff the recomputed value is 0xffff
+    (Processor.cpp:121-131). Corrupt some segments: exactly those fail."""
+    rng = np.random.default_rng(99)
+    n, L = 4096, 1480
+    segs = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    segs[:, 16:18] = 0                                   # chksum field zeroed
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    arena = d(segs.reshape(-1))
+    offs = d(fixed_offsets(n, L))
+    lens = d(np.full(n, L, np.uint16))
+    gen = tulips_amd.batch(arena, offs, lens, src=d(src), dst=d(dst),
+                           mode=MODE_TCP | FLAG_COMPLEMENT)
+    g = u16(gen)
+    segs[:, 16] = (g & 0xFF).astype(np.uint8)            # stored as the u16 in memory
+    segs[:, 17] = (g >> 8).astype(np.uint8)
+    bad_idx = rng.choice(n, 37, replace=False)
+    for i in bad_idx:
+        segs[i, int(rng.integers(0, L))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    arena = d(segs.reshape(-1))
+    out = torch.empty(n, dtype=torch.uint16, device=DEV)
+    bad = tulips_amd.verify(arena, offs, lens, src=d(src), dst=d(dst), mode=MODE_TCP, out=out)
+    o = u16(out)
+    assert int(h(bad)[0]) == 37
+    assert set(np.nonzero(o != 0xFFFF)[0]) == set(bad_idx)
+    exp = oracle.batch(segs.reshape(-1), fixed_offsets(n, L), np.full(n, L, np.uint16),
+                       src=src, dst=dst, mode=MODE_TCP)
+    np.testing.assert_array_equal(o, exp)
+
+
+def test_ipv4_headers_batch(oracle):
+    rng = np.random.default_rng(4)
+    n = 10000
+    hdrs = rng.integers(0, 256, (n, 20), dtype=np.uint8)
+    exp = np.array([oracle.ipv4_checksum(hdrs[i].tobytes()) for i in range(n)], np.uint16)
+    out = tulips_amd.batch_fixed(d(hdrs.reshape(-1)), 20, 20, n, mode=MODE_INET)
+    np.testing.assert_array_equal(u16(out), exp)
+
+
+# -- end-to-end host path ---------------------------------------------------
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_context_path(golden, oracle, pinned):
+    b = golden.digests()["batches"]["ZIPF"]
+    n = b["n"]
+    lens = oracle.zipf_lengths(n)
+    offs = packed_offsets(lens)
+    arena_np = oracle.splitmix_bytes(int(lens.astype(np.int64).sum()))
+    if pinned:
+        pt = torch.from_numpy(arena_np).pin_memory()
+        arena_arg = pt.data_ptr()
+    else:
+        arena_arg = arena_np
+    with csum.HostContext(0, chunk_bytes=8 << 20) as ctx:   # many chunks
+        out = ctx.batch(arena_arg, offs, lens)
+    assert f"{oracle.fnv1a_u16(out):016x}" == b["fnv1a64"]
+    src = np.full(n, ip4(10, 1, 0, 1), np.uint32)
+    dst = np.full(n, ip4(10, 1, 0, 2), np.uint32)
+    with csum.HostContext(0) as ctx:
+        out = ctx.batch(arena_np, offs, lens, src=src, dst=dst, mode=MODE_TCP)
+    assert f"{oracle.fnv1a_u16(out):016x}" == golden.digests()["batches"]["ZIPF-tcp"]["fnv1a64"]
+
+
+def test_empty_batch_is_noop():
+    arena = torch.zeros(16, dtype=torch.uint8, device=DEV)
+    offs = torch.zeros(0, dtype=torch.int64, device=DEV)
+    lens = torch.empty(0, dtype=torch.uint16, device=DEV)
+    out = tulips_amd.batch(arena, offs, lens)
+    assert out.numel() == 0

@@ -1,0 +1,381 @@
+// csum_capi.hip — the C ABI of include/tulips_csum.h and
+// include/tulips_csum_util.h, plus the host scalar drop-ins that keep the
+// reference's C++ symbols (tulips::stack::utils::checksum & co.).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "../../include/tulips_csum.h"
+#include "../../include/tulips_csum_util.h"
+#include "csum_common.h"
+#include "csum_launch.h"
+
+using namespace tulips_amd;
+
+// ---------------------------------------------------------------------------
+// Host scalar path. A 20-byte IPv4 header or an 8-byte ICMP header never goes
+// to a GPU; these keep the reference's call sites compiling and linking
+// unchanged. Exact by the closed form in csum_common.h: the data's
+// little-endian dword sum (relative to `data`, i.e. an even "address"), folded,
+// byte-swapped, then the seed added with end-around carry.
+// ---------------------------------------------------------------------------
+namespace {
+
+inline uint32_t
+host_le_partial(const uint8_t* data, uint32_t len)
+{
+  uint64_t acc = 0;
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t w;
+    memcpy(&w, data + i, 8);
+    acc += (w & 0xffffffffu) + (w >> 32);
+  }
+  if (i < len) {
+    uint8_t tail[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+    memcpy(tail, data + i, len - i);
+    uint64_t w;
+    memcpy(&w, tail, 8);
+    acc += (w & 0xffffffffu) + (w >> 32);
+  }
+  return fold64(acc);
+}
+
+inline uint32_t
+host_checksum(uint32_t seed, const uint8_t* data, uint32_t len)
+{
+  // `data` plays the role of an even start address: swap after the fold.
+  const uint32_t r = bswap16(fold32(host_le_partial(data, len)));
+  return add_seed(r, seed);
+}
+
+} // namespace
+
+// The reference's C++ symbols (include/tulips/stack/Utils.h:10-11,
+// include/tulips/stack/IPv4.h:90-92, include/tulips/stack/ICMPv4.h:37).
+namespace tulips::stack::utils {
+__attribute__((visibility("default"))) uint16_t
+checksum(const uint16_t seed, const uint8_t* const data, const uint16_t len)
+{
+  return uint16_t(host_checksum(seed, data, len));
+}
+}
+namespace tulips::stack::ipv4 {
+__attribute__((visibility("default"))) uint16_t
+checksum(const uint8_t* const data)
+{
+  return uint16_t(inet_post(host_checksum(0, data, 20)));
+}
+}
+namespace tulips::stack::icmpv4 {
+__attribute__((visibility("default"))) uint16_t
+checksum(const uint8_t* const data)
+{
+  return uint16_t(inet_post(host_checksum(0, data, 8)));
+}
+}
+
+extern "C" {
+
+uint16_t
+tulips_csum_host(uint16_t seed, const uint8_t* data, uint16_t len)
+{
+  return uint16_t(host_checksum(seed, data, len));
+}
+
+uint16_t
+tulips_csum_ipv4_host(const uint8_t* header20)
+{
+  return uint16_t(inet_post(host_checksum(0, header20, 20)));
+}
+
+uint16_t
+tulips_csum_icmpv4_host(const uint8_t* header8)
+{
+  return uint16_t(inet_post(host_checksum(0, header8, 8)));
+}
+
+uint16_t
+tulips_csum_tcp_host(uint32_t src, uint32_t dst, uint16_t len,
+                     const uint8_t* segment)
+{
+  return uint16_t(
+    inet_post(host_checksum(tcp_seed(src, dst, len), segment, len)));
+}
+
+} // extern "C"
+
+// ---------------------------------------------------------------------------
+// Device batches.
+// ---------------------------------------------------------------------------
+namespace {
+
+inline int
+status_of(hipError_t e)
+{
+  switch (e) {
+    case hipSuccess:
+      return TULIPS_STATUS_OK;
+    case hipErrorOutOfMemory:
+      return TULIPS_STATUS_NO_MORE_RESOURCES;
+    case hipErrorInvalidValue:
+      return TULIPS_STATUS_INVALID_ARGUMENT;
+    default:
+      return TULIPS_STATUS_HARDWARE_ERROR;
+  }
+}
+
+inline bool
+mode_ok(uint32_t mode, const uint32_t* src, const uint32_t* dst)
+{
+  if ((mode & ~(TULIPS_CSUM_MODE_MASK | TULIPS_CSUM_COMPLEMENT)) != 0) {
+    return false;
+  }
+  const uint32_t m = mode & TULIPS_CSUM_MODE_MASK;
+  if (m > TULIPS_CSUM_TCP) {
+    return false;
+  }
+  return m != TULIPS_CSUM_TCP || (src && dst);
+}
+
+inline bool
+geometry_ok(int group, int unroll)
+{
+  return (group == 16 || group == 32 || group == 64) &&
+         (unroll == 2 || unroll == 4 || unroll == 8);
+}
+
+// Default geometry (tuned on MI355X; see profiles/).
+tulips_csum_tuning
+default_tuning(uint32_t len, bool variable)
+{
+  tulips_csum_tuning t;
+  t.nontemporal = 0;
+  t.max_blocks = 0;
+  if (variable) {
+    t.group = 64; // one wave per segment (BASELINE config 4)
+    t.unroll = 4;
+    return t;
+  }
+  const uint32_t nch = len / 16 + 2;
+  if (nch >= 256) {
+    t.group = 64;
+  } else if (nch >= 48) {
+    t.group = 32;
+  } else {
+    t.group = 16;
+  }
+  const uint32_t per_lane = (nch + uint32_t(t.group) - 1) / uint32_t(t.group);
+  t.unroll = per_lane <= 2 ? 2 : per_lane <= 4 ? 4 : 8;
+  return t;
+}
+
+inline void
+apply_tuning(LaunchArgs& a, const tulips_csum_tuning& d,
+             const tulips_csum_tuning* t)
+{
+  a.group = (t && t->group) ? t->group : d.group;
+  a.unroll = (t && t->unroll) ? t->unroll : d.unroll;
+  a.nontemporal = (t && t->nontemporal >= 0) ? (t->nontemporal != 0)
+                                             : (d.nontemporal != 0);
+  a.max_blocks = (t && t->max_blocks) ? t->max_blocks : d.max_blocks;
+}
+
+int
+batch_fixed(const uint8_t* base, uint64_t stride, uint32_t length,
+            const uint16_t* seeds, const uint32_t* src, const uint32_t* dst,
+            uint16_t* out, uint32_t* bad, uint32_t n, uint32_t mode,
+            const tulips_csum_tuning* tuning, void* stream)
+{
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || (!out && !bad) || length > TULIPS_CSUM_MAX_SEGMENT ||
+      !mode_ok(mode, src, dst)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  LaunchArgs a{};
+  a.seeds = seeds;
+  a.src = src;
+  a.dst = dst;
+  a.out = out;
+  a.bad = bad;
+  a.n = n;
+  a.mode = mode;
+  apply_tuning(a, default_tuning(length, false), tuning);
+  if (!geometry_ok(a.group, a.unroll)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return status_of(
+    launch_fixed(base, stride, length, a, static_cast<hipStream_t>(stream)));
+}
+
+int
+batch_var(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
+          const uint16_t* seeds, const uint32_t* src, const uint32_t* dst,
+          uint16_t* out, uint32_t* bad, uint32_t n, uint32_t mode,
+          const tulips_csum_tuning* tuning, void* stream)
+{
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths || (!out && !bad) ||
+      !mode_ok(mode, src, dst)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  LaunchArgs a{};
+  a.seeds = seeds;
+  a.src = src;
+  a.dst = dst;
+  a.out = out;
+  a.bad = bad;
+  a.n = n;
+  a.mode = mode;
+  apply_tuning(a, default_tuning(0, true), tuning);
+  if (!geometry_ok(a.group, a.unroll)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return status_of(
+    launch_var(base, offsets, lengths, a, static_cast<hipStream_t>(stream)));
+}
+
+} // namespace
+
+extern "C" {
+
+int
+tulips_csum_batch(const uint8_t* base, const uint64_t* offsets,
+                  const uint16_t* lengths, const uint16_t* seeds,
+                  const uint32_t* src, const uint32_t* dst, uint16_t* out,
+                  uint32_t n, uint32_t mode, void* stream)
+{
+  if (n && !out) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return batch_var(base, offsets, lengths, seeds, src, dst, out, nullptr, n,
+                   mode, nullptr, stream);
+}
+
+int
+tulips_csum_batch_fixed(const uint8_t* base, uint64_t stride, uint32_t length,
+                        const uint16_t* seeds, const uint32_t* src,
+                        const uint32_t* dst, uint16_t* out, uint32_t n,
+                        uint32_t mode, void* stream)
+{
+  if (n && !out) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return batch_fixed(base, stride, length, seeds, src, dst, out, nullptr, n,
+                     mode, nullptr, stream);
+}
+
+int
+tulips_csum_verify(const uint8_t* base, const uint64_t* offsets,
+                   const uint16_t* lengths, const uint32_t* src,
+                   const uint32_t* dst, uint16_t* out, uint32_t* bad_count,
+                   uint32_t n, uint32_t mode, void* stream)
+{
+  const uint32_t m = mode & TULIPS_CSUM_MODE_MASK;
+  if (!bad_count || (m != TULIPS_CSUM_INET && m != TULIPS_CSUM_TCP)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  const hipError_t e = hipMemsetAsync(bad_count, 0, sizeof(uint32_t),
+                                      static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  return batch_var(base, offsets, lengths, nullptr, src, dst, out, bad_count,
+                   n, mode, nullptr, stream);
+}
+
+int
+tulips_csum_default_tuning(uint32_t fixed_length, int variable,
+                           tulips_csum_tuning* out)
+{
+  if (!out || fixed_length > TULIPS_CSUM_MAX_SEGMENT) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  *out = default_tuning(fixed_length, variable != 0);
+  return TULIPS_STATUS_OK;
+}
+
+int
+tulips_csum_batch_fixed_tuned(const uint8_t* base, uint64_t stride,
+                              uint32_t length, const uint16_t* seeds,
+                              const uint32_t* src, const uint32_t* dst,
+                              uint16_t* out, uint32_t n, uint32_t mode,
+                              const tulips_csum_tuning* tuning, void* stream)
+{
+  if (n && !out) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return batch_fixed(base, stride, length, seeds, src, dst, out, nullptr, n,
+                     mode, tuning, stream);
+}
+
+int
+tulips_csum_batch_tuned(const uint8_t* base, const uint64_t* offsets,
+                        const uint16_t* lengths, const uint16_t* seeds,
+                        const uint32_t* src, const uint32_t* dst,
+                        uint16_t* out, uint32_t n, uint32_t mode,
+                        const tulips_csum_tuning* tuning, void* stream)
+{
+  if (n && !out) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return batch_var(base, offsets, lengths, seeds, src, dst, out, nullptr, n,
+                   mode, tuning, stream);
+}
+
+int
+tulips_csum_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
+                          uint64_t byte_off, void* stream)
+{
+  if (nbytes && !dst) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return status_of(launch_fill_splitmix(dst, nbytes, seed, byte_off,
+                                        static_cast<hipStream_t>(stream)));
+}
+
+int
+tulips_csum_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
+                        uint32_t max_blocks, void* stream)
+{
+  if ((nbytes && (!p || !sink)) || (reinterpret_cast<uintptr_t>(p) & 15)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return status_of(launch_stream_read(p, nbytes, sink, max_blocks,
+                                      static_cast<hipStream_t>(stream)));
+}
+
+const char*
+tulips_csum_status_string(int status)
+{
+  switch (status) {
+    case TULIPS_STATUS_OK:
+      return "Ok";
+    case TULIPS_STATUS_INVALID_ARGUMENT:
+      return "InvalidArgument";
+    case TULIPS_STATUS_HARDWARE_ERROR:
+      return "HardwareError";
+    case TULIPS_STATUS_NO_MORE_RESOURCES:
+      return "NoMoreResources";
+    case TULIPS_STATUS_UNSUPPORTED_OPERATION:
+      return "UnsupportedOperation";
+    default:
+      return "Unknown";
+  }
+}
+
+const char*
+tulips_csum_version(void)
+{
+  return "tulips_amd-csum 0.1 gfx950";
+}
+
+} // extern "C"

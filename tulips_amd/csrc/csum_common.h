@@ -1,0 +1,101 @@
+// csum_common.h — arithmetic shared by the host drop-ins and the gfx950
+// kernels. Everything here is a restatement of one closed form of the
+// reference loop (src/stack/Utils.cpp:14-42):
+//
+//   S = seed + sum_k BE16(d[2k], d[2k+1]) + (len odd ? d[len-1] << 8 : 0)
+//   checksum(seed, d, len) = S == 0 ? 0 : ((S - 1) mod 65535) + 1
+//
+// i.e. an end-around-carry adder that never turns a non-zero sum into 0.
+// Because 2^16 == 1 (mod 65535), any reduction order/width is exact once the
+// final fold is applied, and a little-endian word sum equals the big-endian
+// one byte-swapped when the segment starts at an even address.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define TCS_HD __host__ __device__ __forceinline__
+#else
+#define TCS_HD inline
+#endif
+
+namespace tulips_amd {
+
+constexpr uint32_t MODE_RAW = 0, MODE_INET = 1, MODE_TCP = 2;
+constexpr uint32_t MODE_MASK = 0xff, FLAG_COMPLEMENT = 0x100;
+
+// x mod 65535 with 0 kept distinct from 65535: result in [0, 0x3fffc],
+// zero iff x == 0.
+TCS_HD uint32_t fold64(uint64_t x)
+{
+  return uint32_t(x & 0xffff) + uint32_t((x >> 16) & 0xffff) +
+         uint32_t((x >> 32) & 0xffff) + uint32_t(x >> 48);
+}
+
+// Any 32-bit partial -> [0, 0xffff], zero iff x == 0.
+TCS_HD uint32_t fold32(uint32_t x)
+{
+  x = (x & 0xffff) + (x >> 16);
+  x = (x & 0xffff) + (x >> 16);
+  return x;
+}
+
+TCS_HD uint32_t bswap16(uint32_t v)
+{
+  return ((v & 0xff) << 8) | ((v >> 8) & 0xff);
+}
+
+// One's-complement add of a 16-bit seed to a folded 16-bit partial.
+TCS_HD uint32_t add_seed(uint32_t r, uint32_t seed)
+{
+  uint32_t t = r + seed;
+  return (t & 0xffff) + (t >> 16);
+}
+
+// Big-endian word sum of 4 wire bytes held as a native (LE) uint32, i.e. an
+// ipv4::Address::m_data word (include/tulips/stack/IPv4.h:55).
+TCS_HD uint32_t be_words_of_addr(uint32_t a)
+{
+  return bswap16(a & 0xffff) + bswap16(a >> 16);
+}
+
+// a2's pseudo-header seed (src/stack/tcpv4/Processor.cpp:346-351):
+// (len + 6) in uint16 arithmetic, then + src words + dst words.
+TCS_HD uint32_t tcp_seed(uint32_t src, uint32_t dst, uint32_t len)
+{
+  uint32_t s = ((len + 6u) & 0xffffu) + be_words_of_addr(src) +
+               be_words_of_addr(dst);
+  return fold32(s);
+}
+
+// Post-processing of a2/a5/a6: `sum == 0 ? 0xffff : htons(sum)`.
+TCS_HD uint32_t inet_post(uint32_t r)
+{
+  return r == 0 ? 0xffffu : bswap16(r);
+}
+
+// Finish one segment: `le_partial` is any partial (<= 2^32-1) congruent to the
+// little-endian dword sum of the segment's bytes taken at their absolute
+// addresses; `start_odd` says whether the first byte sits at an odd address.
+TCS_HD uint32_t finish(uint32_t le_partial, bool start_odd, uint32_t mode,
+                       uint32_t seed, uint32_t src, uint32_t dst, uint32_t len)
+{
+  uint32_t r = fold32(le_partial);
+  if (!start_odd) {
+    r = bswap16(r);
+  }
+  const uint32_t m = mode & MODE_MASK;
+  if (m == MODE_TCP) {
+    seed = tcp_seed(src, dst, len);
+  }
+  r = add_seed(r, seed);
+  if (m != MODE_RAW) {
+    r = inet_post(r);
+  }
+  if (mode & FLAG_COMPLEMENT) {
+    r = ~r & 0xffffu;
+  }
+  return r;
+}
+
+}

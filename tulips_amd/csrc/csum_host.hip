@@ -1,0 +1,378 @@
+// csum_host.hip — end-to-end path for host-resident segments
+// (tulips_csum_ctx_* / tulips_csum_batch_host in include/tulips_csum.h).
+//
+// The reference's segments live in host memory delivered by src/transport
+// (one mmap of nbuf x 2048 B for OFED RX, src/transport/ofed/Utils.cpp:241;
+// a reused read buffer for npipe, include/tulips/transport/npipe/Device.h:103)
+// and are checksummed per frame on the CPU. Here a batch is cut into chunks
+// of <= chunk_bytes; each chunk goes host -> pinned staging -> HBM -> kernel
+// -> results back, on two pipeline slots with their own streams so that
+// packing chunk k+1 on the CPU overlaps the copy and kernel of chunk k.
+//
+// When the caller's arena is already pinned (hipHostMalloc/hipHostRegister,
+// as a registered NIC ring would be) and a chunk's segments lie in a compact
+// span, the span is DMA'd straight from the caller's memory (no CPU copy).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/tulips_csum.h"
+#include "csum_common.h"
+#include "csum_launch.h"
+
+using namespace tulips_amd;
+
+namespace {
+
+constexpr uint64_t DEFAULT_CHUNK = 64ull << 20;
+constexpr uint32_t MAX_SEGS_PER_CHUNK = 1u << 20;
+constexpr int PACK_THREADS = 4;
+
+struct Slot
+{
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* h_bytes = nullptr;
+  uint64_t* h_offs = nullptr;
+  uint16_t* h_lens = nullptr;
+  uint16_t* h_seeds = nullptr;
+  uint32_t* h_src = nullptr;
+  uint32_t* h_dst = nullptr;
+  uint16_t* h_out = nullptr;
+  uint8_t* d_bytes = nullptr;
+  uint64_t* d_offs = nullptr;
+  uint16_t* d_lens = nullptr;
+  uint16_t* d_seeds = nullptr;
+  uint32_t* d_src = nullptr;
+  uint32_t* d_dst = nullptr;
+  uint16_t* d_out = nullptr;
+  bool busy = false;
+  uint32_t i0 = 0, i1 = 0;
+};
+
+int
+status_of(hipError_t e)
+{
+  if (e == hipSuccess) {
+    return TULIPS_STATUS_OK;
+  }
+  return e == hipErrorOutOfMemory ? TULIPS_STATUS_NO_MORE_RESOURCES
+                                  : TULIPS_STATUS_HARDWARE_ERROR;
+}
+
+bool
+is_pinned(const void* p)
+{
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+} // namespace
+
+struct tulips_csum_ctx
+{
+  int device = 0;
+  uint64_t chunk = DEFAULT_CHUNK;
+  Slot slots[2];
+};
+
+namespace {
+
+void
+free_slot(Slot& s)
+{
+  if (s.stream) {
+    (void)hipStreamSynchronize(s.stream);
+  }
+  (void)hipHostFree(s.h_bytes);
+  (void)hipHostFree(s.h_offs);
+  (void)hipHostFree(s.h_lens);
+  (void)hipHostFree(s.h_seeds);
+  (void)hipHostFree(s.h_src);
+  (void)hipHostFree(s.h_dst);
+  (void)hipHostFree(s.h_out);
+  (void)hipFree(s.d_bytes);
+  (void)hipFree(s.d_offs);
+  (void)hipFree(s.d_lens);
+  (void)hipFree(s.d_seeds);
+  (void)hipFree(s.d_src);
+  (void)hipFree(s.d_dst);
+  (void)hipFree(s.d_out);
+  if (s.done) {
+    (void)hipEventDestroy(s.done);
+  }
+  if (s.stream) {
+    (void)hipStreamDestroy(s.stream);
+  }
+  s = Slot();
+}
+
+hipError_t
+alloc_slot(Slot& s, uint64_t chunk)
+{
+  hipError_t e;
+#define TCS_TRY(x)                                                             \
+  if ((e = (x)) != hipSuccess) {                                               \
+    return e;                                                                  \
+  }
+  const size_t m = MAX_SEGS_PER_CHUNK;
+  TCS_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  TCS_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_bytes), chunk, 0));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_offs), m * 8, 0));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_lens), m * 2, 0));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_seeds), m * 2, 0));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_src), m * 4, 0));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_dst), m * 4, 0));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), m * 2, 0));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_bytes), chunk));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_offs), m * 8));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_lens), m * 2));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_seeds), m * 2));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_src), m * 4));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_dst), m * 4));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_out), m * 2));
+#undef TCS_TRY
+  return hipSuccess;
+}
+
+// Collect the results of a finished slot into the caller's array.
+hipError_t
+retire(Slot& s, uint16_t* out)
+{
+  if (!s.busy) {
+    return hipSuccess;
+  }
+  const hipError_t e = hipEventSynchronize(s.done);
+  if (e == hipSuccess) {
+    memcpy(out + s.i0, s.h_out, size_t(s.i1 - s.i0) * 2);
+  }
+  s.busy = false;
+  return e;
+}
+
+// Copy segments [i0, i1) into the slot's pinned staging, back to back.
+void
+pack(Slot& s, const uint8_t* base, const uint64_t* offsets,
+     const uint16_t* lengths, uint32_t i0, uint32_t i1)
+{
+  auto copy_range = [&](uint32_t a, uint32_t b) {
+    for (uint32_t j = a; j < b; ++j) {
+      memcpy(s.h_bytes + s.h_offs[j - i0], base + offsets[j], lengths[j]);
+    }
+  };
+  const uint64_t total = s.h_offs[i1 - 1 - i0] + lengths[i1 - 1];
+  if (total < (8ull << 20) || i1 - i0 < 64) {
+    copy_range(i0, i1);
+    return;
+  }
+  std::thread ts[PACK_THREADS];
+  const uint32_t cnt = i1 - i0;
+  for (int t = 0; t < PACK_THREADS; ++t) {
+    const uint32_t a = i0 + uint32_t(uint64_t(cnt) * t / PACK_THREADS);
+    const uint32_t b = i0 + uint32_t(uint64_t(cnt) * (t + 1) / PACK_THREADS);
+    ts[t] = std::thread(copy_range, a, b);
+  }
+  for (auto& t : ts) {
+    t.join();
+  }
+}
+
+} // namespace
+
+extern "C" {
+
+int
+tulips_csum_ctx_create(int device, uint64_t chunk_bytes, tulips_csum_ctx** ctx)
+{
+  if (!ctx) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  *ctx = nullptr;
+  if (chunk_bytes == 0) {
+    chunk_bytes = DEFAULT_CHUNK;
+  }
+  if (chunk_bytes < TULIPS_CSUM_MAX_SEGMENT + 16) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || device < 0 || device >= ndev) {
+    return e != hipSuccess ? status_of(e) : TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if ((e = hipSetDevice(device)) != hipSuccess) {
+    return status_of(e);
+  }
+  auto* c = new (std::nothrow) tulips_csum_ctx();
+  if (!c) {
+    (void)hipSetDevice(prev);
+    return TULIPS_STATUS_NO_MORE_RESOURCES;
+  }
+  c->device = device;
+  c->chunk = chunk_bytes;
+  for (auto& s : c->slots) {
+    if ((e = alloc_slot(s, chunk_bytes)) != hipSuccess) {
+      for (auto& t : c->slots) {
+        free_slot(t);
+      }
+      delete c;
+      (void)hipSetDevice(prev);
+      return status_of(e);
+    }
+  }
+  (void)hipSetDevice(prev);
+  *ctx = c;
+  return TULIPS_STATUS_OK;
+}
+
+int
+tulips_csum_ctx_destroy(tulips_csum_ctx* ctx)
+{
+  if (!ctx) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(ctx->device);
+  for (auto& s : ctx->slots) {
+    free_slot(s);
+  }
+  (void)hipSetDevice(prev);
+  delete ctx;
+  return TULIPS_STATUS_OK;
+}
+
+int
+tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
+                       const uint64_t* offsets, const uint16_t* lengths,
+                       const uint16_t* seeds, const uint32_t* src,
+                       const uint32_t* dst, uint16_t* out, uint32_t n,
+                       uint32_t mode)
+{
+  if (!ctx) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  const uint32_t m = mode & TULIPS_CSUM_MODE_MASK;
+  if (!base || !offsets || !lengths || !out ||
+      (mode & ~(TULIPS_CSUM_MODE_MASK | TULIPS_CSUM_COMPLEMENT)) ||
+      m > TULIPS_CSUM_TCP || (m == TULIPS_CSUM_TCP && (!src || !dst))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  const bool pinned = is_pinned(base);
+  const bool tcp = m == TULIPS_CSUM_TCP;
+  int slot = 0;
+  uint32_t i = 0;
+  while (i < n && e == hipSuccess) {
+    Slot& s = ctx->slots[slot];
+    if ((e = retire(s, out)) != hipSuccess) {
+      break;
+    }
+    // Cut the chunk: segments [i, j) with at most ctx->chunk bytes.
+    uint64_t bytes = 0, lo = UINT64_MAX, hi = 0;
+    uint32_t j = i;
+    while (j < n && j - i < MAX_SEGS_PER_CHUNK &&
+           bytes + lengths[j] <= ctx->chunk) {
+      s.h_offs[j - i] = bytes;
+      bytes += lengths[j];
+      lo = std::min<uint64_t>(lo, offsets[j]);
+      hi = std::max<uint64_t>(hi, offsets[j] + lengths[j]);
+      ++j;
+    }
+    const uint32_t cnt = j - i;
+    const uint8_t* dbase = s.d_bytes;
+    const uint8_t* hsrc;
+    uint64_t hbytes;
+    if (pinned && hi > lo && hi - lo <= ctx->chunk && hi - lo <= 2 * bytes) {
+      // Direct DMA of the caller's span; offsets rebased onto it.
+      for (uint32_t k = 0; k < cnt; ++k) {
+        s.h_offs[k] = offsets[i + k] - lo;
+      }
+      hsrc = base + lo;
+      hbytes = hi - lo;
+    } else {
+      pack(s, base, offsets, lengths, i, j);
+      hsrc = s.h_bytes;
+      hbytes = bytes;
+    }
+    memcpy(s.h_lens, lengths + i, size_t(cnt) * 2);
+    if (seeds && !tcp) {
+      memcpy(s.h_seeds, seeds + i, size_t(cnt) * 2);
+    }
+    if (tcp) {
+      memcpy(s.h_src, src + i, size_t(cnt) * 4);
+      memcpy(s.h_dst, dst + i, size_t(cnt) * 4);
+    }
+    hipStream_t st = s.stream;
+#define TCS_Q(x)                                                               \
+  if (e == hipSuccess) {                                                       \
+    e = (x);                                                                   \
+  }
+    TCS_Q(hipMemcpyAsync(s.d_bytes, hsrc, hbytes, hipMemcpyHostToDevice, st));
+    TCS_Q(hipMemcpyAsync(s.d_offs, s.h_offs, size_t(cnt) * 8,
+                         hipMemcpyHostToDevice, st));
+    TCS_Q(hipMemcpyAsync(s.d_lens, s.h_lens, size_t(cnt) * 2,
+                         hipMemcpyHostToDevice, st));
+    if (seeds && !tcp) {
+      TCS_Q(hipMemcpyAsync(s.d_seeds, s.h_seeds, size_t(cnt) * 2,
+                           hipMemcpyHostToDevice, st));
+    }
+    if (tcp) {
+      TCS_Q(hipMemcpyAsync(s.d_src, s.h_src, size_t(cnt) * 4,
+                           hipMemcpyHostToDevice, st));
+      TCS_Q(hipMemcpyAsync(s.d_dst, s.h_dst, size_t(cnt) * 4,
+                           hipMemcpyHostToDevice, st));
+    }
+    LaunchArgs a{};
+    a.seeds = (seeds && !tcp) ? s.d_seeds : nullptr;
+    a.src = tcp ? s.d_src : nullptr;
+    a.dst = tcp ? s.d_dst : nullptr;
+    a.out = s.d_out;
+    a.bad = nullptr;
+    a.n = cnt;
+    a.mode = mode;
+    a.group = 64;
+    a.unroll = 4;
+    a.nontemporal = false;
+    a.max_blocks = 0;
+    TCS_Q(launch_var(dbase, s.d_offs, s.d_lens, a, st));
+    TCS_Q(hipMemcpyAsync(s.h_out, s.d_out, size_t(cnt) * 2,
+                         hipMemcpyDeviceToHost, st));
+    TCS_Q(hipEventRecord(s.done, st));
+#undef TCS_Q
+    s.busy = e == hipSuccess;
+    s.i0 = i;
+    s.i1 = j;
+    i = j;
+    slot ^= 1;
+  }
+  for (auto& s : ctx->slots) {
+    const hipError_t r = retire(s, out);
+    if (e == hipSuccess) {
+      e = r;
+    }
+  }
+  (void)hipSetDevice(prev);
+  return status_of(e);
+}
+
+} // extern "C"

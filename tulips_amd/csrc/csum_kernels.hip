@@ -1,0 +1,336 @@
+// csum_kernels.hip — gfx950 (MI355X, CDNA4) kernels for batched TULIPS
+// checksums. Reference semantics: src/stack/Utils.cpp:14-42 (a1),
+// src/stack/tcpv4/Processor.cpp:337-357 (a2), src/stack/IPv4.cpp:75-82 (a5),
+// src/stack/ICMPv4.cpp:10-15 (a6); closed form in csum_common.h.
+//
+// Design: the op is an HBM-read-bound integer reduction
+// (~0.5 VALU op per byte), so the kernel is built for bytes in flight, not
+// arithmetic:
+//   * a SUBGROUP of G lanes (G = 16/32/64, a divisor of the 64-wide wave)
+//     owns one segment at a time; lane l reads the 16-byte-aligned chunks
+//     l, l+G, l+2G, ... of the segment with global_load_dwordx4, so one
+//     wave-instruction streams G*16 contiguous bytes per segment;
+//   * U chunks per lane are issued before any is consumed (U*1 KiB in flight
+//     per wave at G=64) and occupancy stays at 8 waves/SIMD;
+//   * chunks are taken at ABSOLUTE 16-byte alignment; bytes outside
+//     [start, start+len) are masked (only the first and last chunk of a
+//     segment ever need it) — this never touches another page, and it makes
+//     any start alignment (packed arenas, odd offsets) take the same path;
+//   * partials are summed as little-endian dwords in 64-bit lanes, folded mod
+//     65535, reduced across the subgroup with cross-lane shuffles, then
+//     byte-swapped iff the segment starts at an even address (csum_common.h);
+//   * a grid-stride loop over segments with a capped grid keeps launches
+//     independent of batch size.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "csum_common.h"
+#include "csum_launch.h"
+
+namespace tulips_amd {
+
+namespace {
+
+struct __attribute__((aligned(16))) u32x4
+{
+  uint32_t x, y, z, w;
+};
+
+template<bool NT>
+__device__ __forceinline__ u32x4
+load_chunk(const u32x4* p)
+{
+  if constexpr (NT) {
+    u32x4 v;
+    v.x = __builtin_nontemporal_load(&p->x);
+    v.y = __builtin_nontemporal_load(&p->y);
+    v.z = __builtin_nontemporal_load(&p->z);
+    v.w = __builtin_nontemporal_load(&p->w);
+    return v;
+  } else {
+    return *p;
+  }
+}
+
+// Mask of the bytes [lo, hi) of a dword whose first byte is byte `b` of its
+// chunk (lo/hi are chunk-relative, 0..16).
+__device__ __forceinline__ uint32_t
+byte_mask(int lo, int hi, int b)
+{
+  int ml = min(max(lo - b, 0), 4);
+  int mh = min(max(hi - b, 0), 4);
+  uint32_t keep_hi = uint32_t((1ull << (8 * mh)) - 1ull);
+  uint32_t drop_lo = uint32_t((1ull << (8 * ml)) - 1ull);
+  return keep_hi & ~drop_lo;
+}
+
+// Sum of the bytes of segment [sa, sa+len) held by this lane, as a 64-bit
+// little-endian dword sum over absolute 16-byte-aligned chunks.
+template<int G, int U, bool NT>
+__device__ __forceinline__ uint64_t
+lane_partial(uintptr_t sa, uint32_t len, int lane)
+{
+  const uintptr_t a0 = sa & ~uintptr_t(15);
+  const uintptr_t ea = sa + len;
+  const int nch = len ? int((ea - a0 + 15) >> 4) : 0;
+  const int head = int(sa - a0);               // valid from byte `head` of chunk 0
+  const int tail = int(ea - a0) - 16 * (nch - 1); // valid up to byte `tail` of the last chunk
+  const u32x4* p = reinterpret_cast<const u32x4*>(a0);
+  uint64_t acc = 0;
+  for (int c = lane; c < nch; c += G * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cc = c + u * G;
+      if (cc < nch) {
+        v[u] = load_chunk<NT>(p + cc);
+      } else {
+        v[u] = u32x4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cc = c + u * G;
+      const int lo = cc == 0 ? head : 0;
+      const int hi = cc == nch - 1 ? tail : 16;
+      if (lo != 0 || hi != 16) {
+        v[u].x &= byte_mask(lo, hi, 0);
+        v[u].y &= byte_mask(lo, hi, 4);
+        v[u].z &= byte_mask(lo, hi, 8);
+        v[u].w &= byte_mask(lo, hi, 12);
+      }
+      acc += uint64_t(v[u].x) + uint64_t(v[u].y) + uint64_t(v[u].z) +
+             uint64_t(v[u].w);
+    }
+  }
+  return acc;
+}
+
+template<int G>
+__device__ __forceinline__ uint32_t
+subgroup_sum(uint32_t x)
+{
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) {
+    x += __shfl_xor(x, m, 64);
+  }
+  return x;
+}
+
+struct FixedSegs
+{
+  const uint8_t* base;
+  uint64_t stride;
+  uint32_t len;
+  __device__ __forceinline__ uint64_t off(uint32_t i) const
+  {
+    return uint64_t(i) * stride;
+  }
+  __device__ __forceinline__ uint32_t length(uint32_t) const { return len; }
+};
+
+struct VarSegs
+{
+  const uint8_t* base;
+  const uint64_t* offs;
+  const uint16_t* lens;
+  __device__ __forceinline__ uint64_t off(uint32_t i) const { return offs[i]; }
+  __device__ __forceinline__ uint32_t length(uint32_t i) const
+  {
+    return lens[i];
+  }
+};
+
+template<int G, int U, bool NT, class Segs>
+__global__ __launch_bounds__(256) void
+csum_kernel(Segs segs, const uint16_t* __restrict__ seeds,
+            const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+            uint16_t* __restrict__ out, uint32_t* __restrict__ bad,
+            uint32_t n, uint32_t mode)
+{
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t groups_per_block = blockDim.x / G;
+  const uint32_t nsub = gridDim.x * groups_per_block;
+  uint32_t seg = blockIdx.x * groups_per_block + threadIdx.x / G;
+  for (; seg < n; seg += nsub) {
+    const uint64_t off = segs.off(seg);
+    const uint32_t len = segs.length(seg);
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(segs.base) + off;
+    const uint64_t acc = lane_partial<G, U, NT>(sa, len, lane);
+    const uint32_t part = subgroup_sum<G>(fold64(acc));
+    if (lane == 0) {
+      const uint32_t m = mode & MODE_MASK;
+      const uint32_t seed = (m != MODE_TCP && seeds) ? seeds[seg] : 0u;
+      const uint32_t s = m == MODE_TCP ? src[seg] : 0u;
+      const uint32_t d = m == MODE_TCP ? dst[seg] : 0u;
+      const uint32_t r = finish(part, (sa & 1) != 0, mode, seed, s, d, len);
+      if (out) {
+        out[seg] = uint16_t(r);
+      }
+      if (bad && (r ^ ((mode & FLAG_COMPLEMENT) ? 0u : 0xffffu)) != 0) {
+        atomicAdd(bad, 1u);
+      }
+    }
+  }
+}
+
+template<int G, int U, bool NT, class Segs>
+hipError_t
+launch_one(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
+{
+  constexpr int block = 256;
+  constexpr uint32_t per_block = block / G;
+  uint64_t blocks = (uint64_t(a.n) + per_block - 1) / per_block;
+  if (a.max_blocks && blocks > a.max_blocks) {
+    blocks = a.max_blocks;
+  }
+  if (blocks == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL((csum_kernel<G, U, NT, Segs>), dim3(uint32_t(blocks)),
+                     dim3(block), 0, stream, segs, a.seeds, a.src, a.dst,
+                     a.out, a.bad, a.n, a.mode);
+  return hipGetLastError();
+}
+
+template<class Segs>
+hipError_t
+dispatch(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
+{
+#define TCS_CASE(G_, U_)                                                       \
+  if (a.group == G_ && a.unroll == U_) {                                       \
+    return a.nontemporal ? launch_one<G_, U_, true>(segs, a, stream)           \
+                         : launch_one<G_, U_, false>(segs, a, stream);         \
+  }
+  TCS_CASE(16, 2)
+  TCS_CASE(16, 4)
+  TCS_CASE(16, 8)
+  TCS_CASE(32, 2)
+  TCS_CASE(32, 4)
+  TCS_CASE(32, 8)
+  TCS_CASE(64, 2)
+  TCS_CASE(64, 4)
+  TCS_CASE(64, 8)
+#undef TCS_CASE
+  return hipErrorInvalidValue;
+}
+
+} // namespace
+
+hipError_t
+launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,
+             const LaunchArgs& a, hipStream_t stream)
+{
+  return dispatch(FixedSegs{base, stride, len}, a, stream);
+}
+
+hipError_t
+launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
+           const LaunchArgs& a, hipStream_t stream)
+{
+  return dispatch(VarSegs{base, offs, lens}, a, stream);
+}
+
+// ---------------------------------------------------------------------------
+// Bench/test utilities (include/tulips_csum_util.h).
+// ---------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ uint64_t
+splitmix_mix(uint64_t z)
+{
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Thread t produces draw k = k0 + t (8 arena bytes) and stores the part of
+// it that falls in [byte_off, byte_off + nbytes).
+__global__ __launch_bounds__(256) void
+fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t nbytes, uint64_t seed,
+                     uint64_t byte_off, uint64_t ndraws)
+{
+  const uint64_t k0 = byte_off >> 3;
+  for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+       t < ndraws; t += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t k = k0 + t;
+    const uint64_t z = splitmix_mix(seed + (k + 1) * 0x9E3779B97F4A7C15ull);
+    const int64_t rel = int64_t(k * 8) - int64_t(byte_off); // dst index of byte 0
+    if (rel >= 0 && uint64_t(rel) + 8 <= nbytes && ((rel & 7) == 0) &&
+        ((reinterpret_cast<uintptr_t>(dst) & 7) == 0)) {
+      *reinterpret_cast<uint64_t*>(dst + rel) = z;
+    } else {
+      for (int b = 0; b < 8; ++b) {
+        const int64_t i = rel + b;
+        if (i >= 0 && uint64_t(i) < nbytes) {
+          dst[i] = uint8_t(z >> (8 * b));
+        }
+      }
+    }
+  }
+}
+
+// Plain streaming read of [p, p+nbytes) (16-byte chunks, nbytes % 16 == 0):
+// the calibration ceiling for the checksum kernel's HBM read rate.
+__global__ __launch_bounds__(256) void
+stream_read_kernel(const u32x4* __restrict__ p, uint64_t nchunks,
+                   uint32_t* __restrict__ sink)
+{
+  uint32_t x = 0;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < nchunks; i += 4 * stride) {
+    const u32x4 a = p[i], b = p[i + stride], c = p[i + 2 * stride],
+                d = p[i + 3 * stride];
+    x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^
+         c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+  }
+  for (; i < nchunks; i += stride) {
+    const u32x4 a = p[i];
+    x ^= a.x ^ a.y ^ a.z ^ a.w;
+  }
+  if (x == 0x9e3779b9u) { // practically never; keeps the loads live
+    sink[0] = x;
+  }
+}
+
+} // namespace
+
+hipError_t
+launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
+                     uint64_t byte_off, hipStream_t stream)
+{
+  if (nbytes == 0) {
+    return hipSuccess;
+  }
+  const uint64_t first = byte_off >> 3;
+  const uint64_t last = (byte_off + nbytes - 1) >> 3;
+  const uint64_t ndraws = last - first + 1;
+  uint64_t blocks = (ndraws + 255) / 256;
+  if (blocks > 8192) {
+    blocks = 8192;
+  }
+  hipLaunchKernelGGL(fill_splitmix_kernel, dim3(uint32_t(blocks)), dim3(256),
+                     0, stream, dst, nbytes, seed, byte_off, ndraws);
+  return hipGetLastError();
+}
+
+hipError_t
+launch_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
+                   uint32_t max_blocks, hipStream_t stream)
+{
+  const uint64_t nchunks = nbytes / 16;
+  if (nchunks == 0) {
+    return hipSuccess;
+  }
+  uint64_t blocks = (nchunks + 255) / 256;
+  const uint64_t cap = max_blocks ? max_blocks : 4096;
+  if (blocks > cap) {
+    blocks = cap;
+  }
+  hipLaunchKernelGGL(stream_read_kernel, dim3(uint32_t(blocks)), dim3(256), 0,
+                     stream, reinterpret_cast<const u32x4*>(p), nchunks, sink);
+  return hipGetLastError();
+}
+
+} // namespace tulips_amd

@@ -1,0 +1,37 @@
+// csum_launch.h — internal launcher interface between the C ABI
+// (csum_capi.hip) and the kernels (csum_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tulips_amd {
+
+struct LaunchArgs
+{
+  const uint16_t* seeds; // nullable
+  const uint32_t* src;   // TCP only
+  const uint32_t* dst;   // TCP only
+  uint16_t* out;         // nullable when only counting
+  uint32_t* bad;         // nullable: count of results != 0xffff
+  uint32_t n;
+  uint32_t mode;
+  int group;             // lanes per segment: 16, 32, 64
+  int unroll;            // chunks in flight per lane: 2, 4, 8
+  bool nontemporal;      // nt loads
+  uint32_t max_blocks;   // grid cap (0 = one subgroup per segment)
+};
+
+hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,
+                        const LaunchArgs& a, hipStream_t stream);
+hipError_t launch_var(const uint8_t* base, const uint64_t* offs,
+                      const uint16_t* lens, const LaunchArgs& a,
+                      hipStream_t stream);
+
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
+                                uint64_t byte_off, hipStream_t stream);
+hipError_t launch_stream_read(const uint8_t* p, uint64_t nbytes,
+                              uint32_t* sink, uint32_t max_blocks,
+                              hipStream_t stream);
+
+}

@@ -1,0 +1,346 @@
+"""Python binding of the MI355X checksum library (``libtulips_csum.so``).
+
+The product is the C ABI in ``include/tulips_csum.h``; this module is the thin
+ctypes layer tests and ``bench.py`` use to drive it. Device buffers are
+passed as torch tensors on a ROCm device (PyTorch is the allocator/stream
+plumbing here, nothing more) or as raw integer device addresses.
+
+There is deliberately no CPU fallback: if the shared library is missing,
+importing this module raises, and every batch call goes to the gfx950
+kernels.
+
+Names mirror the reference (xenogenics/tulips @ 2024-12-20):
+  checksum(seed, data)          tulips::stack::utils::checksum   src/stack/Utils.cpp:14-42
+  ipv4_checksum(header)         tulips::stack::ipv4::checksum    src/stack/IPv4.cpp:75-82
+  icmpv4_checksum(header)       tulips::stack::icmpv4::checksum  src/stack/ICMPv4.cpp:10-15
+  tcp_checksum(src, dst, seg)   tcpv4::Processor::checksum       src/stack/tcpv4/Processor.cpp:337-357
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libtulips_csum.so")
+
+# include/tulips_csum.h
+STATUS_OK = 0
+STATUS_INVALID_ARGUMENT = 1
+STATUS_HARDWARE_ERROR = 2
+STATUS_NO_MORE_RESOURCES = 3
+RAW, INET, TCP = 0, 1, 2
+COMPLEMENT = 0x100
+MAX_SEGMENT = 65535
+
+_STATUS_NAMES = {0: "Ok", 1: "InvalidArgument", 2: "HardwareError",
+                 3: "NoMoreResources", 18: "UnsupportedOperation"}
+
+
+class CsumError(RuntimeError):
+    """A non-Ok tulips::Status from the library."""
+
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {_STATUS_NAMES.get(status, status)}")
+
+
+class InvalidArgument(CsumError, ValueError):
+    pass
+
+
+def _check(rc: int, what: str) -> None:
+    if rc == STATUS_OK:
+        return
+    if rc == STATUS_INVALID_ARGUMENT:
+        raise InvalidArgument(rc, what)
+    raise CsumError(rc, what)
+
+
+class Tuning(C.Structure):
+    """tulips_csum_tuning (include/tulips_csum_util.h)."""
+    _fields_ = [("group", C.c_int32), ("unroll", C.c_int32),
+                ("nontemporal", C.c_int32), ("max_blocks", C.c_uint32)]
+
+    def __repr__(self):
+        return (f"Tuning(group={self.group}, unroll={self.unroll}, "
+                f"nontemporal={self.nontemporal}, max_blocks={self.max_blocks})")
+
+
+_vp = C.c_void_p
+_u8p = C.POINTER(C.c_uint8)
+
+_SIGNATURES = {
+    "tulips_csum_host": (C.c_uint16, [C.c_uint16, _u8p, C.c_uint16]),
+    "tulips_csum_ipv4_host": (C.c_uint16, [_u8p]),
+    "tulips_csum_icmpv4_host": (C.c_uint16, [_u8p]),
+    "tulips_csum_tcp_host": (C.c_uint16, [C.c_uint32, C.c_uint32, C.c_uint16, _u8p]),
+    "tulips_csum_batch": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    C.c_uint32, C.c_uint32, _vp]),
+    "tulips_csum_batch_fixed": (C.c_int, [_vp, C.c_uint64, C.c_uint32, _vp, _vp,
+                                          _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
+    "tulips_csum_verify": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     C.c_uint32, C.c_uint32, _vp]),
+    "tulips_csum_ctx_create": (C.c_int, [C.c_int, C.c_uint64, C.POINTER(_vp)]),
+    "tulips_csum_ctx_destroy": (C.c_int, [_vp]),
+    "tulips_csum_batch_host": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                         C.c_uint32, C.c_uint32]),
+    "tulips_csum_status_string": (C.c_char_p, [C.c_int]),
+    "tulips_csum_version": (C.c_char_p, []),
+    "tulips_csum_default_tuning": (C.c_int, [C.c_uint32, C.c_int, C.POINTER(Tuning)]),
+    "tulips_csum_batch_fixed_tuned": (C.c_int, [_vp, C.c_uint64, C.c_uint32, _vp,
+                                                _vp, _vp, _vp, C.c_uint32,
+                                                C.c_uint32, C.POINTER(Tuning), _vp]),
+    "tulips_csum_batch_tuned": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          C.c_uint32, C.c_uint32,
+                                          C.POINTER(Tuning), _vp]),
+    "tulips_csum_fill_splitmix": (C.c_int, [_vp, C.c_uint64, C.c_uint64,
+                                            C.c_uint64, _vp]),
+    "tulips_csum_stream_read": (C.c_int, [_vp, C.c_uint64, _vp, C.c_uint32, _vp]),
+}
+
+# Exported C++ symbols of the reference surface (host scalar drop-ins).
+CXX_SYMBOLS = (
+    "_ZN6tulips5stack5utils8checksumEtPKht",
+    "_ZN6tulips5stack4ipv48checksumEPKh",
+    "_ZN6tulips5stack6icmpv48checksumEPKh",
+)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make lib` or "
+            "`python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+# ---------------------------------------------------------------------------
+# host scalar drop-ins
+# ---------------------------------------------------------------------------
+def _buf(data: bytes):
+    data = bytes(data)
+    b = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    return C.cast(b, _u8p), b
+
+
+def checksum(seed: int, data: bytes, length: int | None = None) -> int:
+    """utils::checksum(seed, data, len) on the host (no GPU)."""
+    length = len(data) if length is None else length
+    if not 0 <= length <= MAX_SEGMENT or length > len(data):
+        raise ValueError("length out of range")
+    p, _keep = _buf(data)
+    return lib.tulips_csum_host(seed & 0xFFFF, p, length)
+
+
+def ipv4_checksum(header: bytes) -> int:
+    if len(header) < 20:
+        raise ValueError("IPv4 header is 20 bytes")
+    p, _keep = _buf(header)
+    return lib.tulips_csum_ipv4_host(p)
+
+
+def icmpv4_checksum(header: bytes) -> int:
+    if len(header) < 8:
+        raise ValueError("ICMPv4 header is 8 bytes")
+    p, _keep = _buf(header)
+    return lib.tulips_csum_icmpv4_host(p)
+
+
+def tcp_checksum(src: int, dst: int, segment: bytes, length: int | None = None) -> int:
+    length = len(segment) if length is None else length
+    if not 0 <= length <= MAX_SEGMENT or length > len(segment):
+        raise ValueError("length out of range")
+    p, _keep = _buf(segment)
+    return lib.tulips_csum_tcp_host(src, dst, length, p)
+
+
+# ---------------------------------------------------------------------------
+# device batches
+# ---------------------------------------------------------------------------
+def _addr(x) -> int | None:
+    """Device address of a torch tensor (or pass-through int / None)."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if not x.is_cuda:
+        raise ValueError("device batch arguments must be ROCm device tensors")
+    if not x.is_contiguous():
+        raise ValueError("device tensors must be contiguous")
+    return x.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _check_sizes(n: int, **arrays) -> None:
+    for name, a in arrays.items():
+        if a is not None and not isinstance(a, int) and int(a.numel()) < n:
+            raise ValueError(f"{name} holds {int(a.numel())} entries, batch has {n}")
+
+
+def _alloc_out(n: int, like):
+    import torch
+    return torch.empty(n, dtype=torch.uint16, device=like.device)
+
+
+def batch(arena, offsets, lengths, *, seeds=None, src=None, dst=None,
+          mode: int = RAW, out=None, stream=None, tuning: Tuning | None = None):
+    """Checksum segment i = arena[offsets[i] : offsets[i] + lengths[i]].
+
+    arena: uint8 device tensor; offsets: uint64/int64; lengths: uint16;
+    seeds: uint16 (RAW/INET); src/dst: uint32/int32 address words (TCP).
+    Returns the uint16 result tensor (enqueued on `stream`).
+    """
+    n = int(offsets.numel())
+    if int(lengths.numel()) != n:
+        raise ValueError("offsets/lengths size mismatch")
+    _check_sizes(n, seeds=seeds, src=src, dst=dst, out=out)
+    if out is None:
+        out = _alloc_out(n, arena)
+    args = (_addr(arena), _addr(offsets), _addr(lengths), _addr(seeds),
+            _addr(src), _addr(dst), _addr(out), n, mode)
+    if tuning is None:
+        rc = lib.tulips_csum_batch(*args, _stream(stream))
+    else:
+        rc = lib.tulips_csum_batch_tuned(*args, C.byref(tuning), _stream(stream))
+    _check(rc, "tulips_csum_batch")
+    return out
+
+
+def batch_fixed(arena, stride: int, length: int, n: int, *, seeds=None,
+                src=None, dst=None, mode: int = RAW, out=None, stream=None,
+                tuning: Tuning | None = None, base_offset: int = 0):
+    """Checksum segment i = arena[base_offset + i*stride :][:length]."""
+    _check_sizes(n, seeds=seeds, src=src, dst=dst, out=out)
+    if n and not isinstance(arena, int):
+        end = base_offset + (n - 1) * stride + length
+        if end > arena.numel() * arena.element_size():
+            raise ValueError(f"segments end at byte {end}, past the arena")
+    if out is None:
+        out = _alloc_out(n, arena)
+    base = _addr(arena) + base_offset
+    args = (base, stride, length, _addr(seeds), _addr(src), _addr(dst),
+            _addr(out), n, mode)
+    if tuning is None:
+        rc = lib.tulips_csum_batch_fixed(*args, _stream(stream))
+    else:
+        rc = lib.tulips_csum_batch_fixed_tuned(*args, C.byref(tuning), _stream(stream))
+    _check(rc, "tulips_csum_batch_fixed")
+    return out
+
+
+def verify(arena, offsets, lengths, *, src=None, dst=None, mode: int = TCP,
+           out=None, bad=None, stream=None):
+    """Count segments whose INET/TCP result is not 0xffff; returns the uint32
+    device counter (and fills `out` when given)."""
+    import torch
+    n = int(offsets.numel())
+    if bad is None:
+        bad = torch.zeros(1, dtype=torch.int32, device=arena.device)
+    rc = lib.tulips_csum_verify(_addr(arena), _addr(offsets), _addr(lengths),
+                                _addr(src), _addr(dst), _addr(out), _addr(bad),
+                                n, mode, _stream(stream))
+    _check(rc, "tulips_csum_verify")
+    return bad
+
+
+def default_tuning(fixed_length: int = 0, variable: bool = False) -> Tuning:
+    t = Tuning()
+    _check(lib.tulips_csum_default_tuning(fixed_length, int(variable), C.byref(t)),
+           "tulips_csum_default_tuning")
+    return t
+
+
+def fill_splitmix(dst, nbytes: int | None = None, seed: int = 0x54554C495053,
+                  byte_off: int = 0, stream=None) -> None:
+    """Device fill with the SURVEY.md §8c SplitMix64 byte stream."""
+    nbytes = int(dst.numel()) if nbytes is None else nbytes
+    _check(lib.tulips_csum_fill_splitmix(_addr(dst), nbytes, seed, byte_off,
+                                         _stream(stream)),
+           "tulips_csum_fill_splitmix")
+
+
+def stream_read(buf, sink, nbytes: int | None = None, max_blocks: int = 0,
+                stream=None) -> None:
+    nbytes = int(buf.numel()) if nbytes is None else nbytes
+    _check(lib.tulips_csum_stream_read(_addr(buf), nbytes, _addr(sink),
+                                       max_blocks, _stream(stream)),
+           "tulips_csum_stream_read")
+
+
+@dataclass
+class _Arr:
+    ptr: int | None
+    keep: object = None
+
+
+def _host(a, dtype):
+    import numpy as np
+    if a is None:
+        return _Arr(None)
+    a = np.ascontiguousarray(a, dtype=dtype)
+    return _Arr(a.ctypes.data, a)
+
+
+class HostContext:
+    """tulips_csum_ctx: host-resident batches through pinned staging."""
+
+    def __init__(self, device: int = 0, chunk_bytes: int = 0):
+        h = C.c_void_p()
+        _check(lib.tulips_csum_ctx_create(device, chunk_bytes, C.byref(h)),
+               "tulips_csum_ctx_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib.tulips_csum_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def batch(self, arena, offsets, lengths, *, seeds=None, src=None, dst=None,
+              mode: int = RAW, out=None):
+        import numpy as np
+        ar = arena if isinstance(arena, int) else _host(arena, np.uint8)
+        base = ar if isinstance(ar, int) else ar.ptr
+        off = _host(offsets, np.uint64)
+        ln = _host(lengths, np.uint16)
+        n = len(off.keep)
+        if out is None:
+            out = np.empty(n, dtype=np.uint16)
+        sd, s, d = _host(seeds, np.uint16), _host(src, np.uint32), _host(dst, np.uint32)
+        rc = lib.tulips_csum_batch_host(self._h, base, off.ptr, ln.ptr, sd.ptr,
+                                        s.ptr, d.ptr, out.ctypes.data, n, mode)
+        _check(rc, "tulips_csum_batch_host")
+        return out
+
+
+def version() -> str:
+    return lib.tulips_csum_version().decode()
