@@ -139,6 +139,9 @@ int tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
 /* ---- misc ---------------------------------------------------------------- */
 
 const char* tulips_csum_status_string(int status);
+/* The HIP error behind the calling thread's last HardwareError /
+ * NoMoreResources from a device entry point ("" if none). */
+const char* tulips_csum_last_error(void);
 const char* tulips_csum_version(void);
 
 #ifdef __cplusplus

@@ -3,6 +3,7 @@
 // reference's C++ symbols (tulips::stack::utils::checksum & co.).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -114,9 +115,15 @@ tulips_csum_tcp_host(uint32_t src, uint32_t dst, uint16_t len,
 // ---------------------------------------------------------------------------
 namespace {
 
+thread_local char last_error[160] = "";
+
 inline int
 status_of(hipError_t e)
 {
+  if (e != hipSuccess) {
+    snprintf(last_error, sizeof(last_error), "%s (%d): %s", hipGetErrorName(e),
+             int(e), hipGetErrorString(e));
+  }
   switch (e) {
     case hipSuccess:
       return TULIPS_STATUS_OK;
@@ -370,6 +377,12 @@ tulips_csum_status_string(int status)
     default:
       return "Unknown";
   }
+}
+
+const char*
+tulips_csum_last_error(void)
+{
+  return last_error;
 }
 
 const char*

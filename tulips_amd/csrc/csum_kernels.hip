@@ -31,25 +31,26 @@ namespace tulips_amd {
 
 namespace {
 
-struct __attribute__((aligned(16))) u32x4
-{
-  uint32_t x, y, z, w;
-};
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Global (address space 1) pointers: global_load_* instead of flat_load_*,
+// which would also tie every load to lgkmcnt.
+typedef const __attribute__((address_space(1))) u32x4* gchunk_ptr;
 
 template<bool NT>
 __device__ __forceinline__ u32x4
-load_chunk(const u32x4* p)
+load_chunk(gchunk_ptr p)
 {
   if constexpr (NT) {
-    u32x4 v;
-    v.x = __builtin_nontemporal_load(&p->x);
-    v.y = __builtin_nontemporal_load(&p->y);
-    v.z = __builtin_nontemporal_load(&p->z);
-    v.w = __builtin_nontemporal_load(&p->w);
-    return v;
+    return __builtin_nontemporal_load(p);
   } else {
     return *p;
   }
+}
+
+__device__ __forceinline__ uint64_t
+hsum(u32x4 v)
+{
+  return (uint64_t(v.x) + uint64_t(v.y)) + (uint64_t(v.z) + uint64_t(v.w));
 }
 
 // Mask of the bytes [lo, hi) of a dword whose first byte is byte `b` of its
@@ -64,44 +65,69 @@ byte_mask(int lo, int hi, int b)
   return keep_hi & ~drop_lo;
 }
 
+// Dword sum of the bytes [lo, hi) of chunk v.
+__device__ __forceinline__ uint64_t
+masked_hsum(u32x4 v, int lo, int hi)
+{
+  return (uint64_t(v.x & byte_mask(lo, hi, 0)) +
+          uint64_t(v.y & byte_mask(lo, hi, 4))) +
+         (uint64_t(v.z & byte_mask(lo, hi, 8)) +
+          uint64_t(v.w & byte_mask(lo, hi, 12)));
+}
+
 // Sum of the bytes of segment [sa, sa+len) held by this lane, as a 64-bit
-// little-endian dword sum over absolute 16-byte-aligned chunks.
+// little-endian dword sum over absolute 16-byte-aligned chunks. The hot loop
+// adds whole chunks with no masking or predication; the bytes of the first
+// and last chunk that lie outside the segment are then subtracted exactly by
+// the (at most two) lanes that own those chunks.
 template<int G, int U, bool NT>
 __device__ __forceinline__ uint64_t
 lane_partial(uintptr_t sa, uint32_t len, int lane)
 {
+  if (len == 0) {
+    return 0;
+  }
   const uintptr_t a0 = sa & ~uintptr_t(15);
   const uintptr_t ea = sa + len;
-  const int nch = len ? int((ea - a0 + 15) >> 4) : 0;
-  const int head = int(sa - a0);               // valid from byte `head` of chunk 0
-  const int tail = int(ea - a0) - 16 * (nch - 1); // valid up to byte `tail` of the last chunk
-  const u32x4* p = reinterpret_cast<const u32x4*>(a0);
+  const int nch = int((ea - a0 + 15) >> 4);
+  const gchunk_ptr p = reinterpret_cast<gchunk_ptr>(a0);
   uint64_t acc = 0;
-  for (int c = lane; c < nch; c += G * U) {
+  int c = lane;
+  for (; c + (U - 1) * G < nch; c += U * G) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int cc = c + u * G;
-      if (cc < nch) {
-        v[u] = load_chunk<NT>(p + cc);
-      } else {
-        v[u] = u32x4{0, 0, 0, 0};
+      v[u] = load_chunk<NT>(p + c + u * G);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc += hsum(v[u]);
+    }
+  }
+  if (c < nch) {
+    // Tail batch: this lane's remaining (< U) chunks, all issued before the
+    // first is consumed (exec-masked loads; no serial load/wait chain).
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = u32x4{ 0, 0, 0, 0 };
+      if (c + u * G < nch) {
+        v[u] = load_chunk<NT>(p + c + u * G);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int cc = c + u * G;
-      const int lo = cc == 0 ? head : 0;
-      const int hi = cc == nch - 1 ? tail : 16;
-      if (lo != 0 || hi != 16) {
-        v[u].x &= byte_mask(lo, hi, 0);
-        v[u].y &= byte_mask(lo, hi, 4);
-        v[u].z &= byte_mask(lo, hi, 8);
-        v[u].w &= byte_mask(lo, hi, 12);
-      }
-      acc += uint64_t(v[u].x) + uint64_t(v[u].y) + uint64_t(v[u].z) +
-             uint64_t(v[u].w);
+      acc += hsum(v[u]);
     }
+  }
+  // Exact removal of the out-of-segment bytes of the boundary chunks.
+  const int head = int(sa - a0);                   // bytes [0, head) of chunk 0
+  const int tail = int(ea - a0) - 16 * (nch - 1);  // bytes [tail, 16) of the last
+  if (lane == 0 && head != 0) {
+    acc -= masked_hsum(load_chunk<false>(p), 0, head);
+  }
+  if (lane == (nch - 1) % G && tail != 16) {
+    acc -= masked_hsum(load_chunk<false>(p + (nch - 1)), tail, 16);
   }
   return acc;
 }
@@ -187,6 +213,7 @@ launch_one(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
   if (blocks == 0) {
     return hipSuccess;
   }
+  (void)hipGetLastError(); // drop a stale error another runtime user left
   hipLaunchKernelGGL((csum_kernel<G, U, NT, Segs>), dim3(uint32_t(blocks)),
                      dim3(block), 0, stream, segs, a.seeds, a.src, a.dst,
                      a.out, a.bad, a.n, a.mode);
@@ -273,19 +300,31 @@ fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t nbytes, uint64_t seed,
 // Plain streaming read of [p, p+nbytes) (16-byte chunks, nbytes % 16 == 0):
 // the calibration ceiling for the checksum kernel's HBM read rate.
 __global__ __launch_bounds__(256) void
-stream_read_kernel(const u32x4* __restrict__ p, uint64_t nchunks,
+stream_read_kernel(uintptr_t base, uint64_t nchunks,
                    uint32_t* __restrict__ sink)
 {
+  // Each wave streams contiguous 8 KiB tiles: 8 nt dwordx4 loads per lane
+  // (1 KiB per wave-instruction) issued back to back, grid-stride over tiles.
+  constexpr int U = 8;
+  const gchunk_ptr p = reinterpret_cast<gchunk_ptr>(base);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = (uint64_t(gridDim.x) * blockDim.x) >> 6;
+  const uint64_t ntiles = nchunks / (64 * U);
   uint32_t x = 0;
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < nchunks; i += 4 * stride) {
-    const u32x4 a = p[i], b = p[i + stride], c = p[i + 2 * stride],
-                d = p[i + 3 * stride];
-    x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^
-         c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = __builtin_nontemporal_load(p + t * (64 * U) + u * 64 + lane);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
   }
-  for (; i < nchunks; i += stride) {
+  for (uint64_t i = ntiles * (64 * U) + wave * 64 + lane; i < nchunks;
+       i += nwaves * 64) {
     const u32x4 a = p[i];
     x ^= a.x ^ a.y ^ a.z ^ a.w;
   }
@@ -310,6 +349,7 @@ launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
   if (blocks > 8192) {
     blocks = 8192;
   }
+  (void)hipGetLastError();
   hipLaunchKernelGGL(fill_splitmix_kernel, dim3(uint32_t(blocks)), dim3(256),
                      0, stream, dst, nbytes, seed, byte_off, ndraws);
   return hipGetLastError();
@@ -328,8 +368,9 @@ launch_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
   if (blocks > cap) {
     blocks = cap;
   }
+  (void)hipGetLastError();
   hipLaunchKernelGGL(stream_read_kernel, dim3(uint32_t(blocks)), dim3(256), 0,
-                     stream, reinterpret_cast<const u32x4*>(p), nchunks, sink);
+                     stream, reinterpret_cast<uintptr_t>(p), nchunks, sink);
   return hipGetLastError();
 }
 

@@ -54,7 +54,8 @@ def _check(rc: int, what: str) -> None:
         return
     if rc == STATUS_INVALID_ARGUMENT:
         raise InvalidArgument(rc, what)
-    raise CsumError(rc, what)
+    detail = lib.tulips_csum_last_error().decode(errors="replace")
+    raise CsumError(rc, f"{what} [{detail}]" if detail else what)
 
 
 class Tuning(C.Structure):
@@ -87,6 +88,7 @@ _SIGNATURES = {
                                          C.c_uint32, C.c_uint32]),
     "tulips_csum_status_string": (C.c_char_p, [C.c_int]),
     "tulips_csum_version": (C.c_char_p, []),
+    "tulips_csum_last_error": (C.c_char_p, []),
     "tulips_csum_default_tuning": (C.c_int, [C.c_uint32, C.c_int, C.POINTER(Tuning)]),
     "tulips_csum_batch_fixed_tuned": (C.c_int, [_vp, C.c_uint64, C.c_uint32, _vp,
                                                 _vp, _vp, _vp, C.c_uint32,
@@ -108,6 +110,15 @@ CXX_SYMBOLS = (
 
 
 def _load():
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64
+    # (SONAME libamdhip64.so.7, loaded via RPATH as "libamdhip64.so"). If our
+    # library were loaded first it would pull /opt/rocm's copy and torch would
+    # then load a second runtime, which finds no device. Importing torch
+    # first makes our NEEDED libamdhip64.so.7 resolve to torch's copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `make lib` or "
