@@ -91,7 +91,23 @@ lane_partial(uintptr_t sa, uint32_t len, int lane)
   const uintptr_t ea = sa + len;
   const int nch = int((ea - a0 + 15) >> 4);
   const gchunk_ptr p = reinterpret_cast<gchunk_ptr>(a0);
+  const int head = int(sa - a0);                   // bytes [0, head) of chunk 0
+  const int last = nch - 1;
+  const int tail = int(ea - a0) - 16 * last;       // bytes [tail, 16) of the last
   uint64_t acc = 0;
+  // Add chunk `cc` (already in registers) and take out, exactly, the bytes of
+  // the two boundary chunks that lie outside the segment. The corrections run
+  // under exec masks that are empty for all but <= 2 lanes per segment, so
+  // the common path costs one compare + skip per chunk and no extra load.
+  auto consume = [&](const u32x4& v, int cc, bool may_be_first) {
+    acc += hsum(v);
+    if (may_be_first && cc == 0 && head != 0) {
+      acc -= masked_hsum(v, 0, head);
+    }
+    if (cc == last && tail != 16) {
+      acc -= masked_hsum(v, tail, 16);
+    }
+  };
   int c = lane;
   for (; c + (U - 1) * G < nch; c += U * G) {
     u32x4 v[U];
@@ -101,7 +117,7 @@ lane_partial(uintptr_t sa, uint32_t len, int lane)
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      acc += hsum(v[u]);
+      consume(v[u], c + u * G, u == 0);
     }
   }
   if (c < nch) {
@@ -117,17 +133,8 @@ lane_partial(uintptr_t sa, uint32_t len, int lane)
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      acc += hsum(v[u]);
+      consume(v[u], c + u * G, u == 0);
     }
-  }
-  // Exact removal of the out-of-segment bytes of the boundary chunks.
-  const int head = int(sa - a0);                   // bytes [0, head) of chunk 0
-  const int tail = int(ea - a0) - 16 * (nch - 1);  // bytes [tail, 16) of the last
-  if (lane == 0 && head != 0) {
-    acc -= masked_hsum(load_chunk<false>(p), 0, head);
-  }
-  if (lane == (nch - 1) % G && tail != 16) {
-    acc -= masked_hsum(load_chunk<false>(p + (nch - 1)), tail, 16);
   }
   return acc;
 }
