@@ -16,7 +16,7 @@ typedef struct tulips_csum_tuning
 {
   int32_t group;       /* lanes per segment: 16, 32 or 64 */
   int32_t unroll;      /* 16-byte chunks in flight per lane: 2, 4 or 8 */
-  int32_t nontemporal; /* 1 = nt loads, 0 = default cache policy, -1 = default */
+  int32_t nontemporal; /* bit 0: nt loads, bit 1: nt result stores; -1 = default */
   uint32_t max_blocks; /* grid cap; 0 = default */
 } tulips_csum_tuning;
 

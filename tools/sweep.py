@@ -51,7 +51,7 @@ def main():
             csum.fill_splitmix(buf, nb * bb)
             out = torch.empty(nb * NSEG, dtype=torch.uint16, device=dev)
             for g, u, nt, mb in itertools.product((16, 32, 64), (2, 4, 8), (0, 1),
-                                                  (0, 256, 512, 1024, 2048)):
+                                                  (0, 1024, 2048)):
                 t = csum.Tuning(group=g, unroll=u, nontemporal=nt, max_blocks=mb)
 
                 def fn(i, sh, buf=buf, out=out, t=t, L=L, bb=bb, nb=nb):

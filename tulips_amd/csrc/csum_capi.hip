@@ -187,8 +187,9 @@ apply_tuning(LaunchArgs& a, const tulips_csum_tuning& d,
 {
   a.group = (t && t->group) ? t->group : d.group;
   a.unroll = (t && t->unroll) ? t->unroll : d.unroll;
-  a.nontemporal = (t && t->nontemporal >= 0) ? (t->nontemporal != 0)
-                                             : (d.nontemporal != 0);
+  const int32_t nt = (t && t->nontemporal >= 0) ? t->nontemporal : d.nontemporal;
+  a.nontemporal = (nt & 1) != 0;
+  a.nt_store = (nt & 2) != 0;
   a.max_blocks = (t && t->max_blocks) ? t->max_blocks : d.max_blocks;
 }
 

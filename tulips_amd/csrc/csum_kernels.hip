@@ -100,7 +100,8 @@ lane_partial(uintptr_t sa, uint32_t len, int lane)
   // under exec masks that are empty for all but <= 2 lanes per segment, so
   // the common path costs one compare + skip per chunk and no extra load.
   auto consume = [&](const u32x4& v, int cc, bool may_be_first) {
-    acc += hsum(v);
+    const uint64_t s = hsum(v);
+    acc += cc <= last ? s : 0;  // slots past the end re-read chunk `last`
     if (may_be_first && cc == 0 && head != 0) {
       acc -= masked_hsum(v, 0, head);
     }
@@ -108,28 +109,15 @@ lane_partial(uintptr_t sa, uint32_t len, int lane)
       acc -= masked_hsum(v, tail, 16);
     }
   };
-  int c = lane;
-  for (; c + (U - 1) * G < nch; c += U * G) {
+  // Every load is unconditional: slots past the segment's last chunk load
+  // that chunk again (same line, merged by the TA, L1-resident) and are
+  // discarded by a select. Loads under exec-mask branches would make hipcc
+  // drain vmcnt after each one, i.e. one memory round trip per chunk.
+  for (int c = lane; c < nch; c += U * G) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      v[u] = load_chunk<NT>(p + c + u * G);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      consume(v[u], c + u * G, u == 0);
-    }
-  }
-  if (c < nch) {
-    // Tail batch: this lane's remaining (< U) chunks, all issued before the
-    // first is consumed (exec-masked loads; no serial load/wait chain).
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      v[u] = u32x4{ 0, 0, 0, 0 };
-      if (c + u * G < nch) {
-        v[u] = load_chunk<NT>(p + c + u * G);
-      }
+      v[u] = load_chunk<NT>(p + min(c + u * G, last));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -179,7 +167,7 @@ __global__ __launch_bounds__(256) void
 csum_kernel(Segs segs, const uint16_t* __restrict__ seeds,
             const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
             uint16_t* __restrict__ out, uint32_t* __restrict__ bad,
-            uint32_t n, uint32_t mode)
+            uint32_t n, uint32_t mode, bool nt_store)
 {
   const int lane = threadIdx.x & (G - 1);
   const uint32_t groups_per_block = blockDim.x / G;
@@ -198,7 +186,11 @@ csum_kernel(Segs segs, const uint16_t* __restrict__ seeds,
       const uint32_t d = m == MODE_TCP ? dst[seg] : 0u;
       const uint32_t r = finish(part, (sa & 1) != 0, mode, seed, s, d, len);
       if (out) {
-        out[seg] = uint16_t(r);
+        if (nt_store) {
+          __builtin_nontemporal_store(uint16_t(r), out + seg);
+        } else {
+          out[seg] = uint16_t(r);
+        }
       }
       if (bad && (r ^ ((mode & FLAG_COMPLEMENT) ? 0u : 0xffffu)) != 0) {
         atomicAdd(bad, 1u);
@@ -223,7 +215,7 @@ launch_one(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
   (void)hipGetLastError(); // drop a stale error another runtime user left
   hipLaunchKernelGGL((csum_kernel<G, U, NT, Segs>), dim3(uint32_t(blocks)),
                      dim3(block), 0, stream, segs, a.seeds, a.src, a.dst,
-                     a.out, a.bad, a.n, a.mode);
+                     a.out, a.bad, a.n, a.mode, a.nt_store);
   return hipGetLastError();
 }
 

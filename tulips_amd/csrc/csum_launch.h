@@ -19,6 +19,7 @@ struct LaunchArgs
   int group;             // lanes per segment: 16, 32, 64
   int unroll;            // chunks in flight per lane: 2, 4, 8
   bool nontemporal;      // nt loads
+  bool nt_store;         // nt (streaming) result stores
   uint32_t max_blocks;   // grid cap (0 = one subgroup per segment)
 };
 
