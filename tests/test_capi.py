@@ -165,6 +165,13 @@ def test_default_tuning():
     t = csum.default_tuning(1500)
     assert t.group in (16, 32, 64) and t.unroll in (2, 4, 8)
     t = csum.default_tuning(0, variable=True)
-    assert t.group == 64
+    assert t.group == -16  # hybrid short/long kernel
+    # hybrid geometries are for variable-length batches only
+    bad = csum.Tuning(group=-16, unroll=4, nontemporal=1, max_blocks=0)
+    assert csum.lib.tulips_csum_batch_fixed_tuned(FAKE, 1500, 1500, None, None, None, FAKE,
+                                                  4, 0, C.byref(bad), None) == 1
+    bad = csum.Tuning(group=-16, unroll=3, nontemporal=1, max_blocks=0)
+    assert csum.lib.tulips_csum_batch_tuned(FAKE, FAKE, FAKE, None, None, None, FAKE, 4, 0,
+                                            C.byref(bad), None) == 1
     with pytest.raises(csum.InvalidArgument):
         csum.default_tuning(70000)

@@ -20,7 +20,10 @@ from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
 
-GEOMETRIES = [(g, u, nt) for g in (16, 32, 64) for u in (2, 4, 8) for nt in (0, 1)]
+GEOMETRIES = [(g, u, nt) for g in (16, 32, 64) for u in (2, 4, 8) for nt in (0, 1, 3)]
+# hybrid short/long variable-length kernel (negative group = short subgroup)
+GEOMETRIES += [(-8, 4, 1), (-8, 8, 0), (-16, 2, 0), (-16, 4, 1), (-16, 4, 3), (-16, 8, 1),
+               (-32, 4, 0)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -152,7 +155,7 @@ def test_zipf_digest(golden, oracle, name):
     if b["mode"] == "tcp":
         kw = dict(src=d(np.full(n, ip4(10, 1, 0, 1), np.uint32)),
                   dst=d(np.full(n, ip4(10, 1, 0, 2), np.uint32)), mode=MODE_TCP)
-    for g in (None, 16, 32, 64):
+    for g in (None, 16, 32, 64, -8, -16, -32):
         t = None if g is None else csum.Tuning(group=g, unroll=4, nontemporal=-1, max_blocks=0)
         out = tulips_amd.batch(arena, d(offs), d(lens), tuning=t, **kw)
         assert fnv(oracle, out) == b["fnv1a64"], g

@@ -71,7 +71,9 @@ def main():
         doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
         dlens = torch.from_numpy(lens).to(dev)
         zout = torch.empty(nz * NSEG, dtype=torch.uint16, device=dev)
-        for g, u, nt, mb in itertools.product((16, 32, 64), (2, 4, 8), (0, 1), (0, 512, 2048)):
+        geoms = [(g, u) for g in (16, 32, 64) for u in (2, 4, 8)]
+        geoms += [(-8, 4), (-8, 8), (-16, 2), (-16, 4), (-16, 8), (-32, 4)]
+        for (g, u), nt, mb in itertools.product(geoms, (0, 1), (0, 2048)):
             t = csum.Tuning(group=g, unroll=u, nontemporal=nt, max_blocks=mb)
 
             def fz(i, sh, t=t):

@@ -150,34 +150,43 @@ mode_ok(uint32_t mode, const uint32_t* src, const uint32_t* dst)
 }
 
 inline bool
-geometry_ok(int group, int unroll)
+geometry_ok(int group, int unroll, bool variable)
 {
+  if (group < 0) { // hybrid short/long kernel, variable-length batches only
+    return variable &&
+           ((group == -8 && (unroll == 4 || unroll == 8)) ||
+            (group == -16 && (unroll == 2 || unroll == 4 || unroll == 8)) ||
+            (group == -32 && unroll == 4));
+  }
   return (group == 16 || group == 32 || group == 64) &&
          (unroll == 2 || unroll == 4 || unroll == 8);
 }
 
-// Default geometry (tuned on MI355X; see profiles/).
+// Default geometry (measured on MI355X by tools/sweep.py,
+// profiles/sweep_r01.json): nt loads everywhere; the subgroup is sized so a
+// lane holds about one batch of chunks.
 tulips_csum_tuning
 default_tuning(uint32_t len, bool variable)
 {
   tulips_csum_tuning t;
-  t.nontemporal = 0;
+  t.nontemporal = 1;
   t.max_blocks = 0;
   if (variable) {
-    t.group = 64; // one wave per segment (BASELINE config 4)
+    t.group = -16; // hybrid: 16-lane subgroups, whole wave for > 1 KiB
     t.unroll = 4;
     return t;
   }
   const uint32_t nch = len / 16 + 2;
-  if (nch >= 256) {
+  if (nch > 256) {        // > ~4 KiB: whole wave, 8 chunks in flight per lane
     t.group = 64;
-  } else if (nch >= 48) {
+    t.unroll = 8;
+  } else if (nch > 64) {  // ~1-4 KiB (F1500): 32 lanes x 4
     t.group = 32;
+    t.unroll = 4;
   } else {
     t.group = 16;
+    t.unroll = 4;
   }
-  const uint32_t per_lane = (nch + uint32_t(t.group) - 1) / uint32_t(t.group);
-  t.unroll = per_lane <= 2 ? 2 : per_lane <= 4 ? 4 : 8;
   return t;
 }
 
@@ -215,7 +224,7 @@ batch_fixed(const uint8_t* base, uint64_t stride, uint32_t length,
   a.n = n;
   a.mode = mode;
   apply_tuning(a, default_tuning(length, false), tuning);
-  if (!geometry_ok(a.group, a.unroll)) {
+  if (!geometry_ok(a.group, a.unroll, false)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   return status_of(
@@ -244,7 +253,7 @@ batch_var(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
   a.n = n;
   a.mode = mode;
   apply_tuning(a, default_tuning(0, true), tuning);
-  if (!geometry_ok(a.group, a.unroll)) {
+  if (!geometry_ok(a.group, a.unroll, true)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   return status_of(

@@ -350,9 +350,9 @@ tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
     a.bad = nullptr;
     a.n = cnt;
     a.mode = mode;
-    a.group = 64;
+    a.group = -16; // the variable-length default (hybrid short/long kernel)
     a.unroll = 4;
-    a.nontemporal = false;
+    a.nontemporal = true;
     a.max_blocks = 0;
     TCS_Q(launch_var(dbase, s.d_offs, s.d_lens, a, st));
     TCS_Q(hipMemcpyAsync(s.h_out, s.d_out, size_t(cnt) * 2,

@@ -199,6 +199,107 @@ csum_kernel(Segs segs, const uint16_t* __restrict__ seeds,
   }
 }
 
+// Finish and write one segment's result (lane 0 of its subgroup).
+__device__ __forceinline__ void
+emit(uint32_t seg, uint32_t part, uintptr_t sa, uint32_t len,
+     const uint16_t* __restrict__ seeds, const uint32_t* __restrict__ src,
+     const uint32_t* __restrict__ dst, uint16_t* __restrict__ out,
+     uint32_t* __restrict__ bad, uint32_t mode, bool nt_store)
+{
+  const uint32_t m = mode & MODE_MASK;
+  const uint32_t seed = (m != MODE_TCP && seeds) ? seeds[seg] : 0u;
+  const uint32_t s = m == MODE_TCP ? src[seg] : 0u;
+  const uint32_t d = m == MODE_TCP ? dst[seg] : 0u;
+  const uint32_t r = finish(part, (sa & 1) != 0, mode, seed, s, d, len);
+  if (out) {
+    if (nt_store) {
+      __builtin_nontemporal_store(uint16_t(r), out + seg);
+    } else {
+      out[seg] = uint16_t(r);
+    }
+  }
+  if (bad && (r ^ ((mode & FLAG_COMPLEMENT) ? 0u : 0xffffu)) != 0) {
+    atomicAdd(bad, 1u);
+  }
+}
+
+// Variable-length batches with a long tail (Zipf): one subgroup size cannot
+// serve both a 64 B and a 9 KB segment — a 16-lane subgroup needs ~9 load
+// round trips for 9 KB, and that wave then sets the kernel's length. Here
+// each wave owns 64/GS consecutive segments:
+//   phase 1: every segment of at most GS*US chunks is summed by its GS-lane
+//            subgroup in ONE batch of US loads (no loop);
+//   phase 2: the wave's longer segments (found by a ballot) are summed one at
+//            a time by all 64 lanes, UL loads per lane per batch.
+template<int GS, int US, int UL, bool NT>
+__global__ __launch_bounds__(256) void
+csum_hybrid_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
+                   const uint32_t* __restrict__ src,
+                   const uint32_t* __restrict__ dst, uint16_t* __restrict__ out,
+                   uint32_t* __restrict__ bad, uint32_t n, uint32_t mode,
+                   bool nt_store)
+{
+  constexpr int SPW = 64 / GS;
+  const int lane64 = threadIdx.x & 63;
+  const int lane = lane64 & (GS - 1);
+  const int sub = lane64 / GS;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
+  for (uint32_t w0 = wave * SPW; w0 < n; w0 += nwaves * SPW) {
+    const uint32_t seg = w0 + sub;
+    const bool valid = seg < n;
+    const uint32_t len = valid ? segs.length(seg) : 0u;
+    const uintptr_t sa = base + (valid ? segs.off(seg) : 0u);
+    const uintptr_t a0 = sa & ~uintptr_t(15);
+    const int nch = len ? int((sa + len - a0 + 15) >> 4) : 0;
+    const bool is_long = nch > GS * US;
+    // phase 1: short segments, one batch (lane_partial runs one iteration)
+    const uint64_t acc =
+      is_long ? 0 : lane_partial<GS, US, NT>(sa, is_long ? 0u : len, lane);
+    uint32_t part = subgroup_sum<GS>(fold64(acc));
+    // phase 2: long segments, whole wave
+    uint64_t longs = __ballot(is_long && lane == 0);
+    while (longs) {
+      const int j = __ffsll(static_cast<unsigned long long>(longs)) - 1;
+      longs &= longs - 1;
+      const uint32_t lsa_lo = __builtin_amdgcn_readlane(uint32_t(sa), j);
+      const uint32_t lsa_hi = __builtin_amdgcn_readlane(uint32_t(sa >> 32), j);
+      const uint32_t llen = __builtin_amdgcn_readlane(len, j);
+      const uintptr_t lsa = (uintptr_t(lsa_hi) << 32) | lsa_lo;
+      const uint64_t lacc = lane_partial<64, UL, NT>(lsa, llen, lane64);
+      const uint32_t lpart = subgroup_sum<64>(fold64(lacc));
+      if (lane64 == j) {
+        part = lpart;
+      }
+    }
+    if (valid && lane == 0) {
+      emit(seg, part, sa, len, seeds, src, dst, out, bad, mode, nt_store);
+    }
+  }
+}
+
+template<int GS, int US, int UL, bool NT>
+hipError_t
+launch_hybrid(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
+{
+  constexpr int block = 256;
+  constexpr uint32_t per_block = (block / 64) * (64 / GS);
+  uint64_t blocks = (uint64_t(a.n) + per_block - 1) / per_block;
+  if (a.max_blocks && blocks > a.max_blocks) {
+    blocks = a.max_blocks;
+  }
+  if (blocks == 0) {
+    return hipSuccess;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_hybrid_kernel<GS, US, UL, NT>),
+                     dim3(uint32_t(blocks)), dim3(block), 0, stream, segs,
+                     a.seeds, a.src, a.dst, a.out, a.bad, a.n, a.mode,
+                     a.nt_store);
+  return hipGetLastError();
+}
+
 template<int G, int U, bool NT, class Segs>
 hipError_t
 launch_one(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
@@ -254,7 +355,23 @@ hipError_t
 launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
            const LaunchArgs& a, hipStream_t stream)
 {
-  return dispatch(VarSegs{base, offs, lens}, a, stream);
+  const VarSegs segs{base, offs, lens};
+  if (a.group < 0) { // hybrid: short subgroup |group|, U short, 8 long
+#define TCS_HCASE(GS_, US_)                                                    \
+  if (-a.group == GS_ && a.unroll == US_) {                                    \
+    return a.nontemporal ? launch_hybrid<GS_, US_, 8, true>(segs, a, stream)   \
+                         : launch_hybrid<GS_, US_, 8, false>(segs, a, stream); \
+  }
+    TCS_HCASE(8, 4)
+    TCS_HCASE(8, 8)
+    TCS_HCASE(16, 2)
+    TCS_HCASE(16, 4)
+    TCS_HCASE(16, 8)
+    TCS_HCASE(32, 4)
+#undef TCS_HCASE
+    return hipErrorInvalidValue;
+  }
+  return dispatch(segs, a, stream);
 }
 
 // ---------------------------------------------------------------------------
