@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output into profiles/ (run here, after a GPU session).
+
+  python tools/pmc_traffic.py gpurun_out/prof_r01 profiles r01
+
+Reads <prof>/stats/run_kernel_stats.csv and the separate --pmc passes
+(<prof>/pmc_fetch, pmc_write, pmc_rdreq), and writes
+  profiles/rocprof_<tag>_kernel_stats.csv   (the rocprofv3 --stats summary)
+  profiles/pmc_traffic.json                 (HBM bytes per launch, per workload)
+
+HBM accounting per MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KB;
+on gfx950 FETCH_SIZE reports exactly 1/2 of the bytes of a wide coalesced
+streaming read (16 B/lane global_load), so read bytes = 2 * FETCH_SIZE * 1024.
+WRITE_SIZE is exact for 16-B/lane stores and uncalibrated for our 2-byte
+result stores (reported as-is, it is <0.2 % of the traffic).
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+# kernel name fragment -> workload label (bench.py default geometries)
+WORKLOADS = {
+    "csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>": "F1500",
+    "csum_kernel<64, 8, true, tulips_amd::(anonymous namespace)::FixedSegs>": "F9000",
+    "csum_hybrid_kernel<16, 4, 8, true>": "ZIPF",
+}
+ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673}
+
+
+def label(name):
+    for frag, wl in WORKLOADS.items():
+        if frag in name:
+            return wl
+    return None
+
+
+def counters(path):
+    per = defaultdict(lambda: defaultdict(list))
+    if not os.path.exists(path):
+        return per
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            wl = label(r["Kernel_Name"])
+            if wl:
+                per[wl][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    prof, outdir, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    os.makedirs(outdir, exist_ok=True)
+    stats = os.path.join(prof, "stats", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(outdir, f"rocprof_{tag}_kernel_stats.csv"))
+    res = {}
+    merged = defaultdict(dict)
+    for sub in ("pmc_fetch", "pmc_write", "pmc_rdreq"):
+        for wl, cs in counters(os.path.join(prof, sub, "run_counter_collection.csv")).items():
+            for cn, vals in cs.items():
+                merged[wl][cn] = sum(vals) / len(vals)
+                merged[wl][cn + "_dispatches"] = len(vals)
+    for wl, c in merged.items():
+        rd = 2.0 * c.get("FETCH_SIZE", 0.0) * 1024.0
+        wr = c.get("WRITE_SIZE", 0.0) * 1024.0
+        res[wl] = {
+            "hbm_bytes_per_launch": round(rd + wr),
+            "read_bytes_per_launch": round(rd),
+            "write_bytes_per_launch": round(wr),
+            "algorithmic_bytes_per_launch": ALGO_BYTES.get(wl),
+            "traffic_over_algorithmic": round((rd + wr) / ALGO_BYTES[wl], 4)
+            if wl in ALGO_BYTES else None,
+            "raw": {k: round(v, 3) for k, v in c.items()},
+            "method": "2*FETCH_SIZE*1024 (gfx950 half-count correction) + WRITE_SIZE*1024; "
+                      "separate rocprofv3 --pmc passes, mean over dispatches",
+            "source": f"{prof} ({tag})",
+        }
+    with open(os.path.join(outdir, "pmc_traffic.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
