@@ -53,6 +53,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=1.5,
                    help="wall seconds per CPU-baseline leg")
+    p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                   help="torch.distributed backend for N>1 (nccl = RCCL)")
+    p.add_argument("--one-device", action="store_true",
+                   help="rehearsal only: every rank uses cuda:0 (use with gloo)")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from Python instead of replaying a "
                         "captured HIP graph of one shard rotation (16 launches); "
@@ -140,25 +144,34 @@ def main():
     import torch
     import torch.distributed as dist
     from tulips_amd import csum
+    from tulips_amd.shard import (all_ranks_ok, gather_strings, max_over_ranks,
+                                  shard_for)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # control-plane reductions live on the GPU under RCCL, on the CPU under gloo
+    cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     lib = csum.lib
 
     # ---- data: M8x1500 shard <rank>, 16 batches of 65,536 x 1500 B -------------
+    shard = shard_for(rank, world)
     batch_bytes = NSEG * SEG
-    arena = torch.empty(NBATCH * batch_bytes + 256, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(arena, NBATCH * batch_bytes, seed=DATA_SEED,
-                       byte_off=rank * NBATCH * batch_bytes)
+    arena = torch.empty(shard.nbytes + 256, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(arena, shard.nbytes, seed=DATA_SEED, byte_off=shard.byte_offset)
     outs = torch.empty(NBATCH * NSEG, dtype=torch.uint16, device=dev)
     base = arena.data_ptr()
     optr = outs.data_ptr()
@@ -213,12 +226,7 @@ def main():
         dist.barrier()
     t_gpu = ev0.elapsed_time(ev1) / 1e3
     t_local = max(t_gpu, 0.0)
-    if world > 1:
-        tt = torch.tensor([t_local], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
-    else:
-        t_max = t_local
+    t_max = max_over_ranks(t_local, dist, cdev)
 
     total_bytes = float(world) * steps_done * batch_bytes
     value = total_bytes / t_max / GIB
@@ -227,13 +235,12 @@ def main():
     # ---- parity of what was measured: shard digest vs the reference's -------
     gold = golden_digests().get("M8x1500", {})
     out_np = outs.cpu().numpy().view(np.uint16)
-    parity = None
+    digest = fnv1a_u16(out_np)
+    ok = True
     if rank < 8 and gold.get("shards"):
-        parity = "ok" if fnv1a_u16(out_np) == gold["shards"][rank]["fnv1a64"] else "MISMATCH"
-    if world > 1:
-        ok = torch.tensor([1 if parity in ("ok", None) else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        parity = "ok" if int(ok.item()) == 1 else "MISMATCH"
+        ok = digest == gold["shards"][rank]["fnv1a64"]
+    parity = "ok" if all_ranks_ok(ok, dist, cdev) else "MISMATCH"
+    shard_digests = gather_strings(digest, dist)
 
     result = {
         "metric": METRIC,
@@ -258,6 +265,7 @@ def main():
             "launch": "graph" if graph is not None else "eager",
         },
         "parity": parity,
+        "shard_digests": shard_digests,
         "wall_s_timed": round(t_wall, 4),
     }
 
