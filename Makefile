@@ -29,6 +29,13 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# Diagnostic build: per-wave realtime stamps (tools/probe_stamps.py). Never
+# loaded by the product.
+stamps: tools/libcsum_stamps.so
+
+tools/libcsum_stamps.so: $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DTULIPS_CSUM_STAMPS -shared -o $@ $(SRCS)
+
 # Device assembly + resource usage of the kernels (for inspection).
 asm:
 	@mkdir -p build/asm

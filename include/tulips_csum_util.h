@@ -18,6 +18,7 @@ typedef struct tulips_csum_tuning
   int32_t unroll;      /* 16-byte chunks in flight per lane: 2, 4 or 8 */
   int32_t nontemporal; /* bit 0: nt loads, bit 1: nt result stores; -1 = default */
   uint32_t max_blocks; /* grid cap; 0 = default */
+  int32_t block;       /* threads per workgroup: 256, 512 or 1024; 0 = default */
 } tulips_csum_tuning;
 
 /* The geometry tulips_csum_batch_fixed / tulips_csum_batch would pick. */

@@ -171,6 +171,7 @@ default_tuning(uint32_t len, bool variable)
   tulips_csum_tuning t;
   t.nontemporal = 1;
   t.max_blocks = 0;
+  t.block = 256;
   if (variable) {
     t.group = -16; // hybrid: 16-lane subgroups, whole wave for > 1 KiB
     t.unroll = 4;
@@ -200,6 +201,13 @@ apply_tuning(LaunchArgs& a, const tulips_csum_tuning& d,
   a.nontemporal = (nt & 1) != 0;
   a.nt_store = (nt & 2) != 0;
   a.max_blocks = (t && t->max_blocks) ? t->max_blocks : d.max_blocks;
+  a.block = (t && t->block) ? t->block : d.block;
+}
+
+inline bool
+block_ok(int block)
+{
+  return block == 256 || block == 512 || block == 1024;
 }
 
 int
@@ -224,7 +232,7 @@ batch_fixed(const uint8_t* base, uint64_t stride, uint32_t length,
   a.n = n;
   a.mode = mode;
   apply_tuning(a, default_tuning(length, false), tuning);
-  if (!geometry_ok(a.group, a.unroll, false)) {
+  if (!geometry_ok(a.group, a.unroll, false) || !block_ok(a.block)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   return status_of(
@@ -253,7 +261,7 @@ batch_var(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
   a.n = n;
   a.mode = mode;
   apply_tuning(a, default_tuning(0, true), tuning);
-  if (!geometry_ok(a.group, a.unroll, true)) {
+  if (!geometry_ok(a.group, a.unroll, true) || !block_ok(a.block)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   return status_of(

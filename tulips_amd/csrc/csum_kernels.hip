@@ -127,6 +127,34 @@ lane_partial(uintptr_t sa, uint32_t len, int lane)
   return acc;
 }
 
+#ifdef TULIPS_CSUM_STAMPS
+// Diagnostic build only (tools/libcsum_stamps.so, tools/probe_stamps.py):
+// every wave records {start, end, hw_id} of its life in 100 MHz realtime
+// ticks. No product build defines TULIPS_CSUM_STAMPS.
+__device__ uint64_t* g_stamps;
+__device__ uint32_t g_stamp_count;
+
+__device__ __forceinline__ void
+stamp_wave(uint64_t t0)
+{
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && g_stamps) {
+    // wave index from the launch geometry: no atomic (it would serialise)
+    const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (i == 0) {
+      g_stamp_count = (gridDim.x * blockDim.x) >> 6;
+    }
+    // HW_REG_XCC_ID (20) bits [3:0]; HW_REG_HW_ID (4) all 32 bits
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));
+    const uint32_t hwid = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+    g_stamps[4 * i + 0] = t0;
+    g_stamps[4 * i + 1] = t1;
+    g_stamps[4 * i + 2] = xcc;
+    g_stamps[4 * i + 3] = hwid;
+  }
+}
+#endif
+
 template<int G>
 __device__ __forceinline__ uint32_t
 subgroup_sum(uint32_t x)
@@ -162,8 +190,34 @@ struct VarSegs
   }
 };
 
+// Per-segment side inputs (seed or TCP pseudo-header addresses).
+struct SideIn
+{
+  uint32_t seed, src, dst;
+};
+
+__device__ uint32_t k_zero_word[1] = { 0 }; // global memory, never written
+
+typedef const __attribute__((address_space(1))) uint16_t* gu16_ptr;
+typedef const __attribute__((address_space(1))) uint32_t* gu32_ptr;
+
+// Issue the side-input loads of segment `seg` UNCONDITIONALLY, before its
+// chunk loads so that they travel together: an unused input reads a zero
+// word instead (pointer select, no branch). A load under a branch would make
+// hipcc drain vmcnt(0) at the join; a load issued after the reduction would
+// cost the segment one more memory round trip.
+__device__ __forceinline__ SideIn
+load_side(uint32_t seg, const uint16_t* __restrict__ seeds,
+          const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+          uint32_t mode);
+
+__device__ __forceinline__ void
+emit_with(uint32_t seg, uint32_t part, uintptr_t sa, uint32_t len, SideIn in,
+          uint16_t* __restrict__ out, uint32_t* __restrict__ bad,
+          uint32_t mode, bool nt_store);
+
 template<int G, int U, bool NT, class Segs>
-__global__ __launch_bounds__(256) void
+__global__ __launch_bounds__(1024) void
 csum_kernel(Segs segs, const uint16_t* __restrict__ seeds,
             const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
             uint16_t* __restrict__ out, uint32_t* __restrict__ bad,
@@ -173,44 +227,53 @@ csum_kernel(Segs segs, const uint16_t* __restrict__ seeds,
   const uint32_t groups_per_block = blockDim.x / G;
   const uint32_t nsub = gridDim.x * groups_per_block;
   uint32_t seg = blockIdx.x * groups_per_block + threadIdx.x / G;
+#ifdef TULIPS_CSUM_STAMPS
+  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (; seg < n; seg += nsub) {
     const uint64_t off = segs.off(seg);
     const uint32_t len = segs.length(seg);
     const uintptr_t sa = reinterpret_cast<uintptr_t>(segs.base) + off;
+    const SideIn side = load_side(seg, seeds, src, dst, mode);
     const uint64_t acc = lane_partial<G, U, NT>(sa, len, lane);
     const uint32_t part = subgroup_sum<G>(fold64(acc));
     if (lane == 0) {
-      const uint32_t m = mode & MODE_MASK;
-      const uint32_t seed = (m != MODE_TCP && seeds) ? seeds[seg] : 0u;
-      const uint32_t s = m == MODE_TCP ? src[seg] : 0u;
-      const uint32_t d = m == MODE_TCP ? dst[seg] : 0u;
-      const uint32_t r = finish(part, (sa & 1) != 0, mode, seed, s, d, len);
-      if (out) {
-        if (nt_store) {
-          __builtin_nontemporal_store(uint16_t(r), out + seg);
-        } else {
-          out[seg] = uint16_t(r);
-        }
-      }
-      if (bad && (r ^ ((mode & FLAG_COMPLEMENT) ? 0u : 0xffffu)) != 0) {
-        atomicAdd(bad, 1u);
-      }
+      emit_with(seg, part, sa, len, side, out, bad, mode, nt_store);
     }
   }
+#ifdef TULIPS_CSUM_STAMPS
+  stamp_wave(stamp0);
+#endif
 }
 
-// Finish and write one segment's result (lane 0 of its subgroup).
-__device__ __forceinline__ void
-emit(uint32_t seg, uint32_t part, uintptr_t sa, uint32_t len,
-     const uint16_t* __restrict__ seeds, const uint32_t* __restrict__ src,
-     const uint32_t* __restrict__ dst, uint16_t* __restrict__ out,
-     uint32_t* __restrict__ bad, uint32_t mode, bool nt_store)
+__device__ __forceinline__ SideIn
+load_side(uint32_t seg, const uint16_t* __restrict__ seeds,
+          const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+          uint32_t mode)
 {
   const uint32_t m = mode & MODE_MASK;
-  const uint32_t seed = (m != MODE_TCP && seeds) ? seeds[seg] : 0u;
-  const uint32_t s = m == MODE_TCP ? src[seg] : 0u;
-  const uint32_t d = m == MODE_TCP ? dst[seg] : 0u;
-  const uint32_t r = finish(part, (sa & 1) != 0, mode, seed, s, d, len);
+  const bool tcp = m == MODE_TCP;
+  const bool seeded = !tcp && seeds != nullptr;
+  const uintptr_t zero = reinterpret_cast<uintptr_t>(k_zero_word);
+  // explicit global-address-space pointers: a generic (flat) load would make
+  // hipcc wait for vmcnt(0) and lgkmcnt(0) before any use
+  const gu16_ptr ps = reinterpret_cast<gu16_ptr>(
+    seeded ? reinterpret_cast<uintptr_t>(seeds + seg) : zero);
+  const gu32_ptr pa = reinterpret_cast<gu32_ptr>(
+    tcp ? reinterpret_cast<uintptr_t>(src + seg) : zero);
+  const gu32_ptr pb = reinterpret_cast<gu32_ptr>(
+    tcp ? reinterpret_cast<uintptr_t>(dst + seg) : zero);
+  return SideIn{ *ps, *pa, *pb };
+}
+
+// Finish and write one segment's result (lane 0 of its subgroup); no loads.
+__device__ __forceinline__ void
+emit_with(uint32_t seg, uint32_t part, uintptr_t sa, uint32_t len, SideIn in,
+          uint16_t* __restrict__ out, uint32_t* __restrict__ bad,
+          uint32_t mode, bool nt_store)
+{
+  const uint32_t r =
+    finish(part, (sa & 1) != 0, mode, in.seed, in.src, in.dst, len);
   if (out) {
     if (nt_store) {
       __builtin_nontemporal_store(uint16_t(r), out + seg);
@@ -232,7 +295,7 @@ emit(uint32_t seg, uint32_t part, uintptr_t sa, uint32_t len,
 //   phase 2: the wave's longer segments (found by a ballot) are summed one at
 //            a time by all 64 lanes, UL loads per lane per batch.
 template<int GS, int US, int UL, bool NT>
-__global__ __launch_bounds__(256) void
+__global__ __launch_bounds__(1024) void
 csum_hybrid_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
                    const uint32_t* __restrict__ src,
                    const uint32_t* __restrict__ dst, uint16_t* __restrict__ out,
@@ -254,6 +317,7 @@ csum_hybrid_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
     const uintptr_t a0 = sa & ~uintptr_t(15);
     const int nch = len ? int((sa + len - a0 + 15) >> 4) : 0;
     const bool is_long = nch > GS * US;
+    const SideIn side = load_side(valid ? seg : n - 1, seeds, src, dst, mode);
     // phase 1: short segments, one batch (lane_partial runs one iteration)
     const uint64_t acc =
       is_long ? 0 : lane_partial<GS, US, NT>(sa, is_long ? 0u : len, lane);
@@ -274,7 +338,7 @@ csum_hybrid_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
       }
     }
     if (valid && lane == 0) {
-      emit(seg, part, sa, len, seeds, src, dst, out, bad, mode, nt_store);
+      emit_with(seg, part, sa, len, side, out, bad, mode, nt_store);
     }
   }
 }
@@ -283,8 +347,8 @@ template<int GS, int US, int UL, bool NT>
 hipError_t
 launch_hybrid(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
 {
-  constexpr int block = 256;
-  constexpr uint32_t per_block = (block / 64) * (64 / GS);
+  const int block = a.block ? a.block : 256;
+  const uint32_t per_block = uint32_t(block / 64) * (64 / GS);
   uint64_t blocks = (uint64_t(a.n) + per_block - 1) / per_block;
   if (a.max_blocks && blocks > a.max_blocks) {
     blocks = a.max_blocks;
@@ -304,8 +368,8 @@ template<int G, int U, bool NT, class Segs>
 hipError_t
 launch_one(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
 {
-  constexpr int block = 256;
-  constexpr uint32_t per_block = block / G;
+  const int block = a.block ? a.block : 256;
+  const uint32_t per_block = uint32_t(block / G);
   uint64_t blocks = (uint64_t(a.n) + per_block - 1) / per_block;
   if (a.max_blocks && blocks > a.max_blocks) {
     blocks = a.max_blocks;
@@ -344,11 +408,34 @@ dispatch(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
 
 } // namespace
 
+#ifdef TULIPS_CSUM_STAMPS
+extern "C" int
+tulips_csum_stamps_arm(uint64_t* buf)
+{
+  const uint32_t zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_count), &zero, sizeof(zero)) !=
+        hipSuccess) {
+    return 2;
+  }
+  return 0;
+}
+
+extern "C" uint32_t
+tulips_csum_stamps_count()
+{
+  uint32_t c = 0;
+  (void)hipMemcpyFromSymbol(&c, HIP_SYMBOL(g_stamp_count), sizeof(c));
+  return c;
+}
+#endif
+
 hipError_t
 launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,
              const LaunchArgs& a, hipStream_t stream)
 {
-  return dispatch(FixedSegs{base, stride, len}, a, stream);
+  const FixedSegs segs{base, stride, len};
+  return dispatch(segs, a, stream);
 }
 
 hipError_t

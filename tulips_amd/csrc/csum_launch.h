@@ -21,6 +21,7 @@ struct LaunchArgs
   bool nontemporal;      // nt loads
   bool nt_store;         // nt (streaming) result stores
   uint32_t max_blocks;   // grid cap (0 = one subgroup per segment)
+  int block;             // threads per workgroup: 256, 512, 1024 (0 = 256)
 };
 
 hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,

@@ -61,11 +61,16 @@ def _check(rc: int, what: str) -> None:
 class Tuning(C.Structure):
     """tulips_csum_tuning (include/tulips_csum_util.h)."""
     _fields_ = [("group", C.c_int32), ("unroll", C.c_int32),
-                ("nontemporal", C.c_int32), ("max_blocks", C.c_uint32)]
+                ("nontemporal", C.c_int32), ("max_blocks", C.c_uint32),
+                ("block", C.c_int32)]
+
+    def __init__(self, group=0, unroll=0, nontemporal=-1, max_blocks=0, block=0):
+        super().__init__(group, unroll, nontemporal, max_blocks, block)
 
     def __repr__(self):
         return (f"Tuning(group={self.group}, unroll={self.unroll}, "
-                f"nontemporal={self.nontemporal}, max_blocks={self.max_blocks})")
+                f"nontemporal={self.nontemporal}, max_blocks={self.max_blocks}, "
+                f"block={self.block})")
 
 
 _vp = C.c_void_p
