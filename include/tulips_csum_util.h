@@ -11,14 +11,25 @@
 extern "C" {
 #endif
 
+/* Kernel families (tulips_csum_tuning.kind). */
+#define TULIPS_CSUM_KIND_DEFAULT 0
+#define TULIPS_CSUM_KIND_SUBGROUP 1 /* `group` lanes (16/32/64) per segment */
+#define TULIPS_CSUM_KIND_HYBRID 2   /* variable only: `group`-lane subgroups
+                                       (8/16/32) for short segments, `sps`
+                                       of them in flight per subgroup; whole
+                                       wave for long ones */
+
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning
 {
-  int32_t group;       /* lanes per segment: 16, 32 or 64 */
+  int32_t kind;        /* TULIPS_CSUM_KIND_* */
+  int32_t group;       /* see kind */
   int32_t unroll;      /* 16-byte chunks in flight per lane: 2, 4 or 8 */
   int32_t nontemporal; /* bit 0: nt loads, bit 1: nt result stores; -1 = default */
   uint32_t max_blocks; /* grid cap; 0 = default */
   int32_t block;       /* threads per workgroup: 256, 512 or 1024; 0 = default */
+  int32_t sps;         /* HYBRID: short segments per subgroup issued together
+                          (1, 2, 4); 0 = default */
 } tulips_csum_tuning;
 
 /* The geometry tulips_csum_batch_fixed / tulips_csum_batch would pick. */

@@ -20,10 +20,13 @@ from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
 
-GEOMETRIES = [(g, u, nt) for g in (16, 32, 64) for u in (2, 4, 8) for nt in (0, 1, 3)]
-# hybrid short/long variable-length kernel (negative group = short subgroup)
-GEOMETRIES += [(-8, 4, 1), (-8, 8, 0), (-16, 2, 0), (-16, 4, 1), (-16, 4, 3), (-16, 8, 1),
-               (-32, 4, 0)]
+SUB, HYB = csum.KIND_SUBGROUP, csum.KIND_HYBRID
+# (kind, group, unroll, nontemporal bits, sps)
+GEOMETRIES = [(SUB, g, u, nt, 0) for g in (16, 32, 64) for u in (2, 4, 8) for nt in (0, 1, 3)]
+# hybrid short/long variable-length kernel, with 1/2/4 short segments in flight
+GEOMETRIES += [(HYB, 8, 4, 1, 1), (HYB, 8, 4, 1, 2), (HYB, 8, 4, 0, 4), (HYB, 8, 8, 0, 1),
+               (HYB, 16, 2, 0, 1), (HYB, 16, 2, 1, 2), (HYB, 16, 2, 1, 4),
+               (HYB, 16, 4, 1, 1), (HYB, 16, 4, 3, 2), (HYB, 16, 8, 1, 1), (HYB, 32, 4, 0, 1)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -69,13 +72,14 @@ def test_adversarial_all_modes_default_geometry(golden):
 
 @pytest.mark.parametrize("geom", GEOMETRIES)
 def test_adversarial_every_geometry(golden, geom):
-    g, u, nt = geom
+    kind, g, u, nt, sps = geom
     adv = golden.adversarial()
     arena = d(adv["arena"])
     offs, lens = d(adv["offsets"]), d(adv["lengths"])
     src, dst, seeds = d(adv["src"]), d(adv["dst"]), d(adv["seeds"])
     for max_blocks in (0, 7):
-        t = csum.Tuning(group=g, unroll=u, nontemporal=nt, max_blocks=max_blocks)
+        t = csum.Tuning(kind=kind, group=g, unroll=u, nontemporal=nt, max_blocks=max_blocks,
+                        sps=sps)
         out = tulips_amd.batch(arena, offs, lens, src=src, dst=dst, mode=MODE_TCP, tuning=t)
         np.testing.assert_array_equal(u16(out), adv["expect_tcp"])
         out = tulips_amd.batch(arena, offs, lens, seeds=seeds, mode=MODE_RAW, tuning=t)
@@ -155,10 +159,13 @@ def test_zipf_digest(golden, oracle, name):
     if b["mode"] == "tcp":
         kw = dict(src=d(np.full(n, ip4(10, 1, 0, 1), np.uint32)),
                   dst=d(np.full(n, ip4(10, 1, 0, 2), np.uint32)), mode=MODE_TCP)
-    for g in (None, 16, 32, 64, -8, -16, -32):
-        t = None if g is None else csum.Tuning(group=g, unroll=4, nontemporal=-1, max_blocks=0)
+    geoms = [None] + [(SUB, g, 1) for g in (16, 32, 64)] + [(HYB, g, 1) for g in (8, 16, 32)]
+    geoms += [(HYB, 8, 2), (HYB, 8, 4), (HYB, 16, 2)]
+    for geo in geoms:
+        t = None if geo is None else csum.Tuning(kind=geo[0], group=geo[1], unroll=4,
+                                                 sps=geo[2])
         out = tulips_amd.batch(arena, d(offs), d(lens), tuning=t, **kw)
-        assert fnv(oracle, out) == b["fnv1a64"], g
+        assert fnv(oracle, out) == b["fnv1a64"], geo
 
 
 def test_m8_all_shards(golden, oracle):

@@ -71,17 +71,20 @@ def main():
         doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
         dlens = torch.from_numpy(lens).to(dev)
         zout = torch.empty(nz * NSEG, dtype=torch.uint16, device=dev)
-        geoms = [(g, u) for g in (16, 32, 64) for u in (2, 4, 8)]
-        geoms += [(-8, 4), (-8, 8), (-16, 2), (-16, 4), (-16, 8), (-32, 4)]
-        for (g, u), nt, mb in itertools.product(geoms, (0, 1), (0, 2048)):
-            t = csum.Tuning(group=g, unroll=u, nontemporal=nt, max_blocks=mb)
+        S, H = csum.KIND_SUBGROUP, csum.KIND_HYBRID
+        geoms = [(S, g, u, 1) for g in (16, 32, 64) for u in (4, 8)]
+        geoms += [(H, 8, 4, 1), (H, 8, 4, 2), (H, 8, 4, 4), (H, 8, 8, 1), (H, 16, 2, 1),
+                  (H, 16, 2, 2), (H, 16, 2, 4), (H, 16, 4, 1), (H, 16, 4, 2), (H, 16, 8, 1),
+                  (H, 32, 4, 1)]
+        for (k, g, u, sps), nt in itertools.product(geoms, (0, 1)):
+            t = csum.Tuning(kind=k, group=g, unroll=u, nontemporal=nt, sps=sps)
 
             def fz(i, sh, t=t):
                 b = i % nz
                 lib.tulips_csum_batch_tuned(zbuf.data_ptr() + b * zb, doffs.data_ptr(),
                                             dlens.data_ptr(), None, None, None,
                                             zout.data_ptr() + b * NSEG * 2, NSEG, 0, t, sh)
-            work.append((f"ZIPF g{g} u{u} nt{nt} mb{mb}", fz, zb))
+            work.append((f"ZIPF k{k} g{g} u{u} s{sps} nt{nt}", fz, zb))
     if "READ" in only:
         rb = 16 * NSEG * 1500
         rbuf = torch.empty(rb, dtype=torch.uint8, device=dev)

@@ -149,17 +149,25 @@ mode_ok(uint32_t mode, const uint32_t* src, const uint32_t* dst)
   return m != TULIPS_CSUM_TCP || (src && dst);
 }
 
+// The instantiated kernel geometries (csum_kernels.hip dispatch tables).
 inline bool
-geometry_ok(int group, int unroll, bool variable)
+geometry_ok(int kind, int group, int unroll, int spw, bool variable)
 {
-  if (group < 0) { // hybrid short/long kernel, variable-length batches only
-    return variable &&
-           ((group == -8 && (unroll == 4 || unroll == 8)) ||
-            (group == -16 && (unroll == 2 || unroll == 4 || unroll == 8)) ||
-            (group == -32 && unroll == 4));
+  switch (kind) {
+    case TULIPS_CSUM_KIND_SUBGROUP:
+      return spw == 1 && (group == 16 || group == 32 || group == 64) &&
+             (unroll == 2 || unroll == 4 || unroll == 8);
+    case TULIPS_CSUM_KIND_HYBRID:
+      return variable &&
+             ((group == 8 && unroll == 4 && (spw == 1 || spw == 2 || spw == 4)) ||
+              (group == 8 && unroll == 8 && spw == 1) ||
+              (group == 16 && unroll == 2 && (spw == 1 || spw == 2 || spw == 4)) ||
+              (group == 16 && unroll == 4 && (spw == 1 || spw == 2)) ||
+              (group == 16 && unroll == 8 && spw == 1) ||
+              (group == 32 && unroll == 4 && spw == 1));
+    default:
+      return false;
   }
-  return (group == 16 || group == 32 || group == 64) &&
-         (unroll == 2 || unroll == 4 || unroll == 8);
 }
 
 // Default geometry (measured on MI355X by tools/sweep.py,
@@ -169,11 +177,14 @@ tulips_csum_tuning
 default_tuning(uint32_t len, bool variable)
 {
   tulips_csum_tuning t;
+  t.kind = TULIPS_CSUM_KIND_SUBGROUP;
   t.nontemporal = 1;
   t.max_blocks = 0;
   t.block = 256;
+  t.sps = 1;
   if (variable) {
-    t.group = -16; // hybrid: 16-lane subgroups, whole wave for > 1 KiB
+    t.kind = TULIPS_CSUM_KIND_HYBRID; // 16-lane subgroups, wave for > 1 KiB
+    t.group = 16;
     t.unroll = 4;
     return t;
   }
@@ -195,13 +206,17 @@ inline void
 apply_tuning(LaunchArgs& a, const tulips_csum_tuning& d,
              const tulips_csum_tuning* t)
 {
-  a.group = (t && t->group) ? t->group : d.group;
-  a.unroll = (t && t->unroll) ? t->unroll : d.unroll;
+  // an explicit kind takes its group/unroll from the caller (0 = default)
+  const bool own = t && t->kind != TULIPS_CSUM_KIND_DEFAULT;
+  a.kind = own ? t->kind : d.kind;
+  a.group = (t && t->group) ? t->group : (own && t->kind != d.kind ? 0 : d.group);
+  a.unroll = (t && t->unroll) ? t->unroll : (own && t->kind != d.kind ? 4 : d.unroll);
   const int32_t nt = (t && t->nontemporal >= 0) ? t->nontemporal : d.nontemporal;
   a.nontemporal = (nt & 1) != 0;
   a.nt_store = (nt & 2) != 0;
   a.max_blocks = (t && t->max_blocks) ? t->max_blocks : d.max_blocks;
   a.block = (t && t->block) ? t->block : d.block;
+  a.spw = (t && t->sps) ? t->sps : (own && t->kind != d.kind ? 1 : d.sps);
 }
 
 inline bool
@@ -232,7 +247,8 @@ batch_fixed(const uint8_t* base, uint64_t stride, uint32_t length,
   a.n = n;
   a.mode = mode;
   apply_tuning(a, default_tuning(length, false), tuning);
-  if (!geometry_ok(a.group, a.unroll, false) || !block_ok(a.block)) {
+  if (!geometry_ok(a.kind, a.group, a.unroll, a.spw, false) ||
+      !block_ok(a.block)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   return status_of(
@@ -261,7 +277,8 @@ batch_var(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
   a.n = n;
   a.mode = mode;
   apply_tuning(a, default_tuning(0, true), tuning);
-  if (!geometry_ok(a.group, a.unroll, true) || !block_ok(a.block)) {
+  if (!geometry_ok(a.kind, a.group, a.unroll, a.spw, true) ||
+      !block_ok(a.block)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   return status_of(

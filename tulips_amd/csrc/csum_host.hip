@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/tulips_csum.h"
+#include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
 
@@ -350,7 +351,9 @@ tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
     a.bad = nullptr;
     a.n = cnt;
     a.mode = mode;
-    a.group = -16; // the variable-length default (hybrid short/long kernel)
+    a.kind = TULIPS_CSUM_KIND_HYBRID; // the variable-length default
+    a.group = 16;
+    a.spw = 1;
     a.unroll = 4;
     a.nontemporal = true;
     a.max_blocks = 0;

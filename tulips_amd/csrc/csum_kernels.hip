@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
 
@@ -286,16 +287,23 @@ emit_with(uint32_t seg, uint32_t part, uintptr_t sa, uint32_t len, SideIn in,
   }
 }
 
-// Variable-length batches with a long tail (Zipf): one subgroup size cannot
-// serve both a 64 B and a 9 KB segment — a 16-lane subgroup needs ~9 load
-// round trips for 9 KB, and that wave then sets the kernel's length. Here
-// each wave owns 64/GS consecutive segments:
+__device__ uint32_t k_zero_chunk[4] __attribute__((aligned(16))) = { 0, 0, 0, 0 };
+
+// Variable-length batches with a long tail (Zipf, mean 668 B, 64 B..9 KB).
+// One subgroup size cannot serve both a 64 B and a 9 KB segment, and a wave
+// that owns one short segment per subgroup spends its life on two dependent
+// round trips (metadata, then data) for a few hundred bytes — with 65,536
+// segments the kernel is then bound by generations of short waves, not by
+// bytes (tools/probe_zipf.py: ~7 us floor for 65,536 x 64 B). Here each wave
+// owns SPW*SPS consecutive segments, SPW = 64/GS subgroups x SPS each:
 //   phase 1: every segment of at most GS*US chunks is summed by its GS-lane
-//            subgroup in ONE batch of US loads (no loop);
+//            subgroup; the metadata of all SPS segments, then the US chunk
+//            loads of all SPS segments, are issued before anything is
+//            consumed (SPS*US loads in flight per lane, all unconditional);
 //   phase 2: the wave's longer segments (found by a ballot) are summed one at
 //            a time by all 64 lanes, UL loads per lane per batch.
-template<int GS, int US, int UL, bool NT>
-__global__ __launch_bounds__(1024) void
+template<int GS, int US, int UL, int SPS, bool NT>
+__global__ __launch_bounds__(256) void
 csum_hybrid_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
                    const uint32_t* __restrict__ src,
                    const uint32_t* __restrict__ dst, uint16_t* __restrict__ out,
@@ -303,52 +311,101 @@ csum_hybrid_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
                    bool nt_store)
 {
   constexpr int SPW = 64 / GS;
+  constexpr int SEGS = SPW * SPS;
   const int lane64 = threadIdx.x & 63;
   const int lane = lane64 & (GS - 1);
   const int sub = lane64 / GS;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
-  for (uint32_t w0 = wave * SPW; w0 < n; w0 += nwaves * SPW) {
-    const uint32_t seg = w0 + sub;
-    const bool valid = seg < n;
-    const uint32_t len = valid ? segs.length(seg) : 0u;
-    const uintptr_t sa = base + (valid ? segs.off(seg) : 0u);
-    const uintptr_t a0 = sa & ~uintptr_t(15);
-    const int nch = len ? int((sa + len - a0 + 15) >> 4) : 0;
-    const bool is_long = nch > GS * US;
-    const SideIn side = load_side(valid ? seg : n - 1, seeds, src, dst, mode);
-    // phase 1: short segments, one batch (lane_partial runs one iteration)
-    const uint64_t acc =
-      is_long ? 0 : lane_partial<GS, US, NT>(sa, is_long ? 0u : len, lane);
-    uint32_t part = subgroup_sum<GS>(fold64(acc));
-    // phase 2: long segments, whole wave
-    uint64_t longs = __ballot(is_long && lane == 0);
-    while (longs) {
-      const int j = __ffsll(static_cast<unsigned long long>(longs)) - 1;
-      longs &= longs - 1;
-      const uint32_t lsa_lo = __builtin_amdgcn_readlane(uint32_t(sa), j);
-      const uint32_t lsa_hi = __builtin_amdgcn_readlane(uint32_t(sa >> 32), j);
-      const uint32_t llen = __builtin_amdgcn_readlane(len, j);
-      const uintptr_t lsa = (uintptr_t(lsa_hi) << 32) | lsa_lo;
-      const uint64_t lacc = lane_partial<64, UL, NT>(lsa, llen, lane64);
-      const uint32_t lpart = subgroup_sum<64>(fold64(lacc));
-      if (lane64 == j) {
-        part = lpart;
+  const uintptr_t zero_chunk = reinterpret_cast<uintptr_t>(k_zero_chunk);
+  for (uint32_t w0 = wave * SEGS; w0 < n; w0 += nwaves * SEGS) {
+    uint32_t seg[SPS], len[SPS];
+    uintptr_t sa[SPS];
+    bool valid[SPS], is_long[SPS];
+    SideIn side[SPS];
+    u32x4 v[SPS][US];
+#pragma unroll
+    for (int k = 0; k < SPS; ++k) {
+      seg[k] = w0 + uint32_t(k * SPW + sub);
+      valid[k] = seg[k] < n;
+      const uint32_t sk = valid[k] ? seg[k] : n - 1;
+      len[k] = valid[k] ? segs.length(sk) : 0u;
+      sa[k] = base + segs.off(sk);
+      side[k] = load_side(sk, seeds, src, dst, mode);
+    }
+#pragma unroll
+    for (int k = 0; k < SPS; ++k) {
+      const uintptr_t a0 = sa[k] & ~uintptr_t(15);
+      const int nch = len[k] ? int((sa[k] + len[k] - a0 + 15) >> 4) : 0;
+      is_long[k] = nch > GS * US;
+      // short and non-empty: its chunks; otherwise a harmless zero chunk
+      const bool use = nch > 0 && !is_long[k];
+      const uintptr_t p0 = use ? a0 : zero_chunk;
+      const int last = use ? nch - 1 : 0;
+#pragma unroll
+      for (int u = 0; u < US; ++u) {
+        v[k][u] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(p0) +
+                                 min(lane + u * GS, last));
       }
     }
-    if (valid && lane == 0) {
-      emit_with(seg, part, sa, len, side, out, bad, mode, nt_store);
+    uint32_t part[SPS];
+#pragma unroll
+    for (int k = 0; k < SPS; ++k) {
+      const uintptr_t a0 = sa[k] & ~uintptr_t(15);
+      const int nch = len[k] ? int((sa[k] + len[k] - a0 + 15) >> 4) : 0;
+      const int last = nch - 1;
+      const int head = int(sa[k] - a0);
+      const int tail = int(sa[k] + len[k] - a0) - 16 * last;
+      const bool use = nch > 0 && !is_long[k];
+      uint64_t acc = 0;
+#pragma unroll
+      for (int u = 0; u < US; ++u) {
+        const int cc = lane + u * GS;
+        const uint64_t h = hsum(v[k][u]);
+        acc += (use && cc <= last) ? h : 0;
+        if (use && u == 0 && cc == 0 && head != 0) {
+          acc -= masked_hsum(v[k][u], 0, head);
+        }
+        if (use && cc == last && tail != 16) {
+          acc -= masked_hsum(v[k][u], tail, 16);
+        }
+      }
+      part[k] = subgroup_sum<GS>(fold64(acc));
+    }
+    // phase 2: long segments, whole wave, one at a time
+#pragma unroll
+    for (int k = 0; k < SPS; ++k) {
+      uint64_t longs = __ballot(is_long[k] && lane == 0);
+      while (longs) {
+        const int j = __ffsll(static_cast<unsigned long long>(longs)) - 1;
+        longs &= longs - 1;
+        const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(sa[k]), j);
+        const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(sa[k] >> 32), j);
+        const uint32_t llen = __builtin_amdgcn_readlane(len[k], j);
+        const uintptr_t lsa = (uintptr_t(hi) << 32) | lo;
+        const uint64_t lacc = lane_partial<64, UL, NT>(lsa, llen, lane64);
+        const uint32_t lpart = subgroup_sum<64>(fold64(lacc));
+        if (lane64 == j) {
+          part[k] = lpart;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SPS; ++k) {
+      if (valid[k] && lane == 0) {
+        emit_with(seg[k], part[k], sa[k], len[k], side[k], out, bad, mode,
+                  nt_store);
+      }
     }
   }
 }
 
-template<int GS, int US, int UL, bool NT>
+template<int GS, int US, int UL, int SPS, bool NT>
 hipError_t
 launch_hybrid(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
 {
-  const int block = a.block ? a.block : 256;
-  const uint32_t per_block = uint32_t(block / 64) * (64 / GS);
+  const uint64_t per_block = uint64_t(256 / 64) * uint64_t(64 / GS) * SPS;
   uint64_t blocks = (uint64_t(a.n) + per_block - 1) / per_block;
   if (a.max_blocks && blocks > a.max_blocks) {
     blocks = a.max_blocks;
@@ -357,8 +414,8 @@ launch_hybrid(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
     return hipSuccess;
   }
   (void)hipGetLastError();
-  hipLaunchKernelGGL((csum_hybrid_kernel<GS, US, UL, NT>),
-                     dim3(uint32_t(blocks)), dim3(block), 0, stream, segs,
+  hipLaunchKernelGGL((csum_hybrid_kernel<GS, US, UL, SPS, NT>),
+                     dim3(uint32_t(blocks)), dim3(256), 0, stream, segs,
                      a.seeds, a.src, a.dst, a.out, a.bad, a.n, a.mode,
                      a.nt_store);
   return hipGetLastError();
@@ -443,18 +500,26 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
            const LaunchArgs& a, hipStream_t stream)
 {
   const VarSegs segs{base, offs, lens};
-  if (a.group < 0) { // hybrid: short subgroup |group|, U short, 8 long
-#define TCS_HCASE(GS_, US_)                                                    \
-  if (-a.group == GS_ && a.unroll == US_) {                                    \
-    return a.nontemporal ? launch_hybrid<GS_, US_, 8, true>(segs, a, stream)   \
-                         : launch_hybrid<GS_, US_, 8, false>(segs, a, stream); \
+  if (a.kind == TULIPS_CSUM_KIND_HYBRID) {
+    // group = short subgroup lanes, unroll = short loads per lane,
+    // spw = segments per short subgroup in flight; 8 loads/lane when long
+#define TCS_HCASE(GS_, US_, SPS_)                                              \
+  if (a.group == GS_ && a.unroll == US_ && a.spw == SPS_) {                    \
+    return a.nontemporal                                                       \
+             ? launch_hybrid<GS_, US_, 8, SPS_, true>(segs, a, stream)         \
+             : launch_hybrid<GS_, US_, 8, SPS_, false>(segs, a, stream);       \
   }
-    TCS_HCASE(8, 4)
-    TCS_HCASE(8, 8)
-    TCS_HCASE(16, 2)
-    TCS_HCASE(16, 4)
-    TCS_HCASE(16, 8)
-    TCS_HCASE(32, 4)
+    TCS_HCASE(8, 4, 1)
+    TCS_HCASE(8, 4, 2)
+    TCS_HCASE(8, 4, 4)
+    TCS_HCASE(8, 8, 1)
+    TCS_HCASE(16, 2, 1)
+    TCS_HCASE(16, 2, 2)
+    TCS_HCASE(16, 2, 4)
+    TCS_HCASE(16, 4, 1)
+    TCS_HCASE(16, 4, 2)
+    TCS_HCASE(16, 8, 1)
+    TCS_HCASE(32, 4, 1)
 #undef TCS_HCASE
     return hipErrorInvalidValue;
   }

@@ -16,12 +16,14 @@ struct LaunchArgs
   uint32_t* bad;         // nullable: count of results != 0xffff
   uint32_t n;
   uint32_t mode;
-  int group;             // lanes per segment: 16, 32, 64
+  int kind;              // TULIPS_CSUM_KIND_* (never DEFAULT here)
+  int group;             // lanes per segment / short subgroup / segs per wave
   int unroll;            // chunks in flight per lane: 2, 4, 8
   bool nontemporal;      // nt loads
   bool nt_store;         // nt (streaming) result stores
   uint32_t max_blocks;   // grid cap (0 = one subgroup per segment)
   int block;             // threads per workgroup: 256, 512, 1024 (0 = 256)
+  int spw;               // hybrid: short segments per subgroup in flight
 };
 
 hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,

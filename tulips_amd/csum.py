@@ -58,19 +58,31 @@ def _check(rc: int, what: str) -> None:
     raise CsumError(rc, f"{what} [{detail}]" if detail else what)
 
 
-class Tuning(C.Structure):
-    """tulips_csum_tuning (include/tulips_csum_util.h)."""
-    _fields_ = [("group", C.c_int32), ("unroll", C.c_int32),
-                ("nontemporal", C.c_int32), ("max_blocks", C.c_uint32),
-                ("block", C.c_int32)]
+KIND_DEFAULT, KIND_SUBGROUP, KIND_HYBRID = 0, 1, 2
 
-    def __init__(self, group=0, unroll=0, nontemporal=-1, max_blocks=0, block=0):
-        super().__init__(group, unroll, nontemporal, max_blocks, block)
+
+class Tuning(C.Structure):
+    """tulips_csum_tuning (include/tulips_csum_util.h).
+
+    kind SUBGROUP: `group` lanes (16/32/64) per segment; HYBRID (variable
+    only): `group`-lane subgroups (8/16/32), `sps` short segments in flight
+    per subgroup, whole wave for long segments. A positive `group` with kind
+    left at DEFAULT means SUBGROUP.
+    """
+    _fields_ = [("kind", C.c_int32), ("group", C.c_int32), ("unroll", C.c_int32),
+                ("nontemporal", C.c_int32), ("max_blocks", C.c_uint32),
+                ("block", C.c_int32), ("sps", C.c_int32)]
+
+    def __init__(self, group=0, unroll=0, nontemporal=-1, max_blocks=0, block=0,
+                 kind=None, sps=0):
+        if kind is None:
+            kind = KIND_SUBGROUP if group else KIND_DEFAULT
+        super().__init__(kind, group, unroll, nontemporal, max_blocks, block, sps)
 
     def __repr__(self):
-        return (f"Tuning(group={self.group}, unroll={self.unroll}, "
+        return (f"Tuning(kind={self.kind}, group={self.group}, unroll={self.unroll}, "
                 f"nontemporal={self.nontemporal}, max_blocks={self.max_blocks}, "
-                f"block={self.block})")
+                f"block={self.block}, sps={self.sps})")
 
 
 _vp = C.c_void_p
