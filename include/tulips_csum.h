@@ -136,6 +136,24 @@ int tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
                            const uint32_t* dst, uint16_t* out, uint32_t n,
                            uint32_t mode);
 
+/* ---- Toeplitz RSS hash -------------------------------- */
+/*
+ * tulips::stack::utils::toeplitz (include/tulips/stack/Utils.h:25-28,
+ * src/stack/Utils.cpp:86-133), whose C++ symbol the library also exports:
+ * the 96-bit tuple saddr | daddr | htons(sport) | htons(dport) hashed with a
+ * `key_len`-byte key (>= 4; host pointer) starting from `init`. Addresses
+ * are ipv4::Address::m_data words (wire bytes as a native uint32).
+ */
+int tulips_rss_toeplitz_host(uint32_t saddr, uint32_t daddr, uint16_t sport,
+                             uint16_t dport, const uint8_t* key,
+                             size_t key_len, uint32_t init, uint32_t* out);
+
+/* Batch: device arrays of n tuples (structure of arrays) -> out[i]. */
+int tulips_rss_toeplitz_batch(const uint32_t* saddr, const uint32_t* daddr,
+                              const uint16_t* sport, const uint16_t* dport,
+                              uint32_t n, const uint8_t* key, size_t key_len,
+                              uint32_t init, uint32_t* out, void* stream);
+
 /* ---- misc ---------------------------------------------------------------- */
 
 const char* tulips_csum_status_string(int status);

@@ -317,3 +317,42 @@ uint64_t orc_sum_u16(const uint16_t* v, uint64_t n)
   }
   return s;
 }
+
+/* ---------------------------------------------------------------------------
+ * §8f #3 — Toeplitz RSS hash, src/stack/Utils.cpp:86-133 (restated).
+ * tuple = saddr bytes | daddr bytes | htons(sport) | htons(dport) (:101-111);
+ * for each tuple bit MSB first, XOR the big-endian first 4 key bytes into the
+ * hash when the bit is set (:117-119), then shift the key left by one bit with
+ * the reference's wrap-around, which reads the ALREADY-SHIFTED tmp[0] for the
+ * last byte (:123-125). Keys shorter than 4 bytes are rejected (the reference
+ * reads 4 bytes of the key buffer whatever its length).
+ * ------------------------------------------------------------------------- */
+int orc_toeplitz(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
+                 size_t len, const uint8_t* key, uint32_t init, uint32_t* out)
+{
+  if (len < 4 || len > 1024 || !key || !out) {
+    return -1;
+  }
+  uint8_t tmp[1024], tuple[12];
+  memcpy(tmp, key, len);
+  memcpy(tuple, &saddr, 4);
+  memcpy(tuple + 4, &daddr, 4);
+  tuple[8] = (uint8_t)(sport >> 8);
+  tuple[9] = (uint8_t)sport;
+  tuple[10] = (uint8_t)(dport >> 8);
+  tuple[11] = (uint8_t)dport;
+  uint32_t h = init;
+  for (int b = 0; b < 12; ++b) {
+    for (int j = 0; j < 8; ++j) {
+      if (tuple[b] & (1u << (7 - j))) {
+        h ^= ((uint32_t)tmp[0] << 24) | ((uint32_t)tmp[1] << 16) |
+             ((uint32_t)tmp[2] << 8) | (uint32_t)tmp[3];
+      }
+      for (size_t i = 0; i < len; ++i) {
+        tmp[i] = (uint8_t)(((tmp[i] << 1) & 0xff) | ((tmp[(i + 1) % len] & 0x80) >> 7));
+      }
+    }
+  }
+  *out = h;
+  return 0;
+}

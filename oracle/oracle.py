@@ -153,6 +153,20 @@ class Oracle(_Batchable):
         v = np.ascontiguousarray(v, dtype=np.uint16)
         return int(self.lib.orc_fnv1a_u16(_ptr(v, _u16p), len(v)))
 
+    def toeplitz(self, saddr: int, daddr: int, sport: int, dport: int, key: bytes,
+                 init: int = 0) -> int:
+        """src/stack/Utils.cpp:86-133 restated (oracle/csum_oracle.c)."""
+        f = self.lib.orc_toeplitz
+        f.restype = C.c_int
+        f.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16, C.c_size_t,
+                      _u8p, C.c_uint32, _u32p]
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        out = np.zeros(1, dtype=np.uint32)
+        if f(saddr, daddr, sport, dport, len(key), _ptr(k, _u8p), init & 0xFFFFFFFF,
+             _ptr(out, _u32p)) != 0:
+            raise ValueError("bad toeplitz arguments")
+        return int(out[0])
+
 
 class Reference(_Batchable):
     """The reference's own functions (oracle/_ref/libtulips_ref.so)."""
@@ -193,6 +207,16 @@ class Reference(_Batchable):
         length = len(data) if length is None else length
         buf = np.frombuffer(bytes(data) or b"\0", dtype=np.uint8).copy()
         return self.lib.ref_tcp_checksum(src, dst, length, _ptr(buf, _u8p))
+
+    def toeplitz(self, saddr: int, daddr: int, sport: int, dport: int, key: bytes,
+                 init: int = 0) -> int:
+        """The reference's own tulips::stack::utils::toeplitz."""
+        f = self.lib.ref_toeplitz
+        f.restype = C.c_uint32
+        f.argtypes = [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16, C.c_size_t,
+                      _u8p, C.c_uint32]
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        return int(f(saddr, daddr, sport, dport, len(key), _ptr(k, _u8p), init & 0xFFFFFFFF))
 
 
 def ip4(a: int, b: int, c: int, d: int) -> int:

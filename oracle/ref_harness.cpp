@@ -24,6 +24,7 @@
 #include <pthread.h>
 #include <sched.h>
 #include <cstdint>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -152,4 +153,18 @@ ref_batch(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
   return 0;
 }
 
+}
+
+extern "C" uint32_t
+ref_toeplitz(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
+             size_t len, const uint8_t* key, uint32_t init)
+{
+  // ipv4::Address is a packed wrapper of the 4 wire bytes
+  // (include/tulips/stack/IPv4.h:13-62); build it from them.
+  uint8_t s[4], d[4];
+  memcpy(s, &saddr, 4);
+  memcpy(d, &daddr, 4);
+  const tulips::stack::ipv4::Address sa(s[0], s[1], s[2], s[3]);
+  const tulips::stack::ipv4::Address da(d[0], d[1], d[2], d[3]);
+  return tulips::stack::utils::toeplitz(sa, da, sport, dport, len, key, init);
 }

@@ -199,9 +199,46 @@ def digests(ref: Reference, orc: Oracle) -> dict:
     return d
 
 
+RSS_KEYS = {
+    # tests/stack/utils.cpp:11-23 (DYNAMIC_KEY / STATIC_KEY, 40 bytes)
+    "dynamic40": bytes.fromhex("008be05ed4a554f83cf808"
+                               "75072c4e8b6f1dbf103b043b41b3a4a4ae56c9a4ec1376a0af04108166"),
+    "static40": bytes.fromhex("beac01fa6a42b73b8030f20c77cb2da3ae7b30b4d0ca2bcb43a38fb041"
+                              "67253d255b0ec26d5a56da"),
+}
+
+
+def rss(ref: Reference) -> dict:
+    """Toeplitz RSS (src/stack/Utils.cpp:86-133) fixtures: the reference's two
+    KATs (tests/stack/utils.cpp:37,54) plus 4096 random tuples per key for
+    keys of 4..52 bytes (short keys exercise the wrap-around quirk)."""
+    rng = np.random.default_rng(9899)
+    keys = dict(RSS_KEYS)
+    for L in (4, 5, 7, 12, 15, 16, 17, 52):
+        keys[f"rand{L}"] = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+    n = 4096
+    sa = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    da = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    sp = rng.integers(0, 65536, n, dtype=np.uint16)
+    dp = rng.integers(0, 65536, n, dtype=np.uint16)
+    sa[0], da[0], sp[0], dp[0] = ip4(10, 1, 0, 1), ip4(10, 1, 0, 2), 8888, 9999
+    out = {"saddr": sa, "daddr": da, "sport": sp, "dport": dp}
+    names = sorted(keys)
+    out["key_names"] = np.array(names)
+    for i, name in enumerate(names):
+        k = keys[name]
+        out[f"key_{i}"] = np.frombuffer(k, dtype=np.uint8)
+        for init, tag in ((0, "init0"), (0xFFFFFFFF, "initff")):
+            out[f"expect_{i}_{tag}"] = np.array(
+                [ref.toeplitz(int(sa[j]), int(da[j]), int(sp[j]), int(dp[j]), k, init)
+                 for j in range(n)], dtype=np.uint32)
+    return out
+
+
 def main():
     ref = Reference()
     orc = Oracle()
+    np.savez_compressed(os.path.join(HERE, "rss.npz"), **rss(ref))
     rows = kat(ref)
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump({"source": "oracle/_ref/libtulips_ref.so (reference src/stack compiled)",

@@ -116,6 +116,11 @@ _SIGNATURES = {
     "tulips_csum_fill_splitmix": (C.c_int, [_vp, C.c_uint64, C.c_uint64,
                                             C.c_uint64, _vp]),
     "tulips_csum_stream_read": (C.c_int, [_vp, C.c_uint64, _vp, C.c_uint32, _vp]),
+    "tulips_rss_toeplitz_host": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16,
+                                           _u8p, C.c_size_t, C.c_uint32,
+                                           C.POINTER(C.c_uint32)]),
+    "tulips_rss_toeplitz_batch": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _u8p,
+                                            C.c_size_t, C.c_uint32, _vp, _vp]),
 }
 
 # Exported C++ symbols of the reference surface (host scalar drop-ins).
@@ -123,6 +128,7 @@ CXX_SYMBOLS = (
     "_ZN6tulips5stack5utils8checksumEtPKht",
     "_ZN6tulips5stack4ipv48checksumEPKh",
     "_ZN6tulips5stack6icmpv48checksumEPKh",
+    "_ZN6tulips5stack5utils8toeplitzERKNS0_4ipv47AddressES5_ttmPKhj",
 )
 
 
@@ -368,6 +374,34 @@ class HostContext:
                                         s.ptr, d.ptr, out.ctypes.data, n, mode)
         _check(rc, "tulips_csum_batch_host")
         return out
+
+
+def toeplitz(saddr: int, daddr: int, sport: int, dport: int, key: bytes,
+             init: int = 0) -> int:
+    """utils::toeplitz (src/stack/Utils.cpp:86-133) on the host."""
+    p, _keep = _buf(key)
+    out = C.c_uint32()
+    _check(lib.tulips_rss_toeplitz_host(saddr, daddr, sport, dport, p, len(key),
+                                        init & 0xFFFFFFFF, C.byref(out)),
+           "tulips_rss_toeplitz_host")
+    return out.value
+
+
+def rss_batch(saddr, daddr, sport, dport, key: bytes, init: int = 0, out=None,
+              stream=None):
+    """Toeplitz hashes of n device-resident tuples (uint32 addresses as
+    ipv4::Address::m_data words, uint16 host-order ports) -> uint32 tensor."""
+    import torch
+    n = int(saddr.numel())
+    _check_sizes(n, daddr=daddr, sport=sport, dport=dport, out=out)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=saddr.device)
+    p, _keep = _buf(key)
+    _check(lib.tulips_rss_toeplitz_batch(_addr(saddr), _addr(daddr), _addr(sport),
+                                         _addr(dport), n, p, len(key), init & 0xFFFFFFFF,
+                                         _addr(out), _stream(stream)),
+           "tulips_rss_toeplitz_batch")
+    return out
 
 
 def version() -> str:
