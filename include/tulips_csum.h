@@ -154,6 +154,50 @@ int tulips_rss_toeplitz_batch(const uint32_t* saddr, const uint32_t* daddr,
                               uint32_t n, const uint8_t* key, size_t key_len,
                               uint32_t init, uint32_t* out, void* stream);
 
+/* ---- receive-side frame validation ------------------ */
+/*
+ * Per-frame result of the checks the reference stack makes before a segment
+ * reaches TCP — ethernet/Processor.cpp:69,91 (ethertype), ipv4/Processor.cpp:
+ * 67-122 (vhl 0x45, no fragments, header checksum, protocol), tcpv4/
+ * Processor.cpp:121-131 (pseudo-header checksum) — in the role of the NIC
+ * offload bits that transport::Device::VALIDATE_IP_CSUM / VALIDATE_L4_CSUM
+ * consult (include/tulips/transport/Device.h:29-30,
+ * src/transport/ena/Device.cpp:318-340).
+ *
+ *   0                    not IPv4 (short frame, other ethertype, IP options)
+ *   IPV4                 an option-less IPv4 header follows the Ethernet one
+ *   IP_CSUM_OK           ... and its header checksum verifies
+ *   TCP                  ... unfragmented, protocol 6
+ *   L4_CSUM_OK           ... and the TCP checksum over ntohs(len) - 20 bytes
+ *                        verifies (never set with TRUNCATED)
+ *   TRUNCATED            the frame ends before the IPv4 header (alone) or
+ *                        before the TCP segment the IP length announces
+ */
+#define TULIPS_FRAME_IPV4 0x01u
+#define TULIPS_FRAME_IP_CSUM_OK 0x02u
+#define TULIPS_FRAME_TCP 0x04u
+#define TULIPS_FRAME_L4_CSUM_OK 0x08u
+#define TULIPS_FRAME_TRUNCATED 0x10u
+
+/*
+ * Frame i is base[offsets[i] .. offsets[i] + lengths[i]) (device pointers;
+ * a frame is read only within its length). Writes flags[i] (uint8, may be
+ * NULL) and, when `counters` (device uint32[4], may be NULL) is given, zeroes
+ * it and counts { IPv4 frames, bad IP checksums, TCP frames, TCP frames
+ * without L4_CSUM_OK }. At least one of flags / counters is required.
+ */
+int tulips_csum_validate_frames(const uint8_t* base, const uint64_t* offsets,
+                                const uint16_t* lengths, uint32_t n,
+                                uint8_t* flags, uint32_t* counters,
+                                void* stream);
+
+/* Host-resident frames through a context's pinned pipeline; `flags` is a
+ * host array of n bytes, `counters` (may be NULL) a host uint32[4]. */
+int tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
+                                     const uint64_t* offsets,
+                                     const uint16_t* lengths, uint32_t n,
+                                     uint8_t* flags, uint32_t* counters);
+
 /* ---- misc ---------------------------------------------------------------- */
 
 const char* tulips_csum_status_string(int status);

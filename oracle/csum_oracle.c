@@ -356,3 +356,63 @@ int orc_toeplitz(uint32_t saddr, uint32_t daddr, uint16_t sport, uint16_t dport,
   *out = h;
   return 0;
 }
+
+/* ---------------------------------------------------------------------------
+ * §8f #1/#2 — receive-side validation of one Ethernet frame, restating the
+ * checks the stack applies before a segment reaches TCP:
+ *   ethernet/Processor.cpp:69,91      type 0x0800 -> IPv4
+ *   ipv4/Processor.cpp:67-73          vhl must be 0x45
+ *   ipv4/Processor.cpp:77-82          no fragments
+ *   ipv4/Processor.cpp:94-103         ipv4::checksum(header) == 0xffff
+ *   ipv4/Processor.cpp:108,116-122    proto 6 -> TCP over ntohs(len) - 20 bytes
+ *   tcpv4/Processor.cpp:121-131       tcpv4 checksum == 0xffff
+ * The destination-address filter (ipv4/Processor.cpp:86-92) is the caller's.
+ * Flags (numerically equal to TULIPS_FRAME_* in include/tulips_csum.h):
+ * ------------------------------------------------------------------------- */
+#define ORC_FRAME_IPV4 0x01u
+#define ORC_FRAME_IP_CSUM_OK 0x02u
+#define ORC_FRAME_TCP 0x04u
+#define ORC_FRAME_L4_CSUM_OK 0x08u
+#define ORC_FRAME_TRUNCATED 0x10u
+
+uint8_t orc_validate_frame(const uint8_t* f, uint32_t len)
+{
+  if (len < 14 || ((unsigned)f[12] << 8 | f[13]) != 0x0800u) {
+    return 0;
+  }
+  if (len < 34) {
+    return ORC_FRAME_TRUNCATED;
+  }
+  const uint8_t* ip = f + 14;
+  if (ip[0] != 0x45) {
+    return 0;
+  }
+  uint8_t fl = ORC_FRAME_IPV4;
+  if (orc_ipv4_checksum(ip) == 0xffff) {
+    fl |= ORC_FRAME_IP_CSUM_OK;
+  }
+  if ((ip[6] & 0x3f) != 0 || ip[7] != 0 || ip[9] != 6) {
+    return fl;
+  }
+  fl |= ORC_FRAME_TCP;
+  const uint16_t total = (uint16_t)((ip[2] << 8) | ip[3]);
+  const uint16_t tcplen = (uint16_t)(total - 20u);
+  if (total < 20 || 34u + tcplen > len) {
+    return (uint8_t)(fl | ORC_FRAME_TRUNCATED);
+  }
+  uint32_t src, dst;
+  memcpy(&src, ip + 12, 4);
+  memcpy(&dst, ip + 16, 4);
+  if (orc_tcp_checksum(src, dst, tcplen, ip + 20) == 0xffff) {
+    fl |= ORC_FRAME_L4_CSUM_OK;
+  }
+  return fl;
+}
+
+void orc_validate_frames(const uint8_t* base, const uint64_t* offsets,
+                         const uint16_t* lengths, uint64_t n, uint8_t* flags)
+{
+  for (uint64_t i = 0; i < n; ++i) {
+    flags[i] = orc_validate_frame(base + offsets[i], lengths[i]);
+  }
+}

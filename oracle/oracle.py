@@ -153,6 +153,19 @@ class Oracle(_Batchable):
         v = np.ascontiguousarray(v, dtype=np.uint16)
         return int(self.lib.orc_fnv1a_u16(_ptr(v, _u16p), len(v)))
 
+    def validate_frames(self, arena, offsets, lengths) -> np.ndarray:
+        """Per-frame TULIPS_FRAME_* flags (oracle/csum_oracle.c)."""
+        f = self.lib.orc_validate_frames
+        f.restype = None
+        f.argtypes = [_u8p, _u64p, _u16p, C.c_uint64, _u8p]
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint16)
+        out = np.zeros(len(offsets), dtype=np.uint8)
+        f(_ptr(arena, _u8p), _ptr(offsets, _u64p), _ptr(lengths, _u16p), len(offsets),
+          _ptr(out, _u8p))
+        return out
+
     def toeplitz(self, saddr: int, daddr: int, sport: int, dport: int, key: bytes,
                  init: int = 0) -> int:
         """src/stack/Utils.cpp:86-133 restated (oracle/csum_oracle.c)."""

@@ -235,9 +235,113 @@ def rss(ref: Reference) -> dict:
     return out
 
 
+def _ref_frame_flags(ref: Reference, f: bytes) -> int:
+    """Expected TULIPS_FRAME_* flags: the receive chain's checks
+    (ethernet/Processor.cpp:69,91; ipv4/Processor.cpp:67-122;
+    tcpv4/Processor.cpp:121-131) evaluated with the REFERENCE's own
+    ipv4::checksum and tcpv4::Processor::checksum."""
+    if len(f) < 14 or (f[12] << 8 | f[13]) != 0x0800:
+        return 0
+    if len(f) < 34:
+        return 0x10
+    ip = f[14:]
+    if ip[0] != 0x45:
+        return 0
+    fl = 0x01 | (0x02 if ref.ipv4_checksum(ip[:20]) == 0xFFFF else 0)
+    if (ip[6] & 0x3F) != 0 or ip[7] != 0 or ip[9] != 6:
+        return fl
+    fl |= 0x04
+    total = ip[2] << 8 | ip[3]
+    tcplen = (total - 20) & 0xFFFF
+    if total < 20 or 34 + tcplen > len(f):
+        return fl | 0x10
+    src = int.from_bytes(ip[12:16], "little")
+    dst = int.from_bytes(ip[16:20], "little")
+    if ref.tcp_checksum(src, dst, ip[20:20 + tcplen]) == 0xFFFF:
+        fl |= 0x08
+    return fl
+
+
+def _make_frame(ref: Reference, rng, payload: int, pad_to: int = 0) -> bytearray:
+    """A well-formed Ethernet/IPv4/TCP frame, checksums generated as the send
+    path writes them (ipv4/Producer.cpp:79-82, tcpv4/Send.cpp:441-449)."""
+    eth = rng.integers(0, 256, 12, dtype=np.uint8).tobytes() + b"\x08\x00"
+    src, dst = rng.integers(0, 256, 4, dtype=np.uint8), rng.integers(0, 256, 4, dtype=np.uint8)
+    tcp = bytearray(rng.integers(0, 256, 20, dtype=np.uint8).tobytes())
+    tcp[12] = 0x50
+    tcp[16:18] = b"\0\0"
+    seg = bytes(tcp) + rng.integers(0, 256, payload, dtype=np.uint8).tobytes()
+    s32, d32 = int.from_bytes(bytes(src), "little"), int.from_bytes(bytes(dst), "little")
+    c = (~ref.tcp_checksum(s32, d32, seg)) & 0xFFFF
+    seg = seg[:16] + c.to_bytes(2, "little") + seg[18:]
+    total = 20 + len(seg)
+    ip = bytearray(b"\x45\x00" + total.to_bytes(2, "big") +
+                   rng.integers(0, 256, 2, dtype=np.uint8).tobytes() + b"\x40\x00\x40\x06\x00\x00" +
+                   bytes(src) + bytes(dst))
+    c = (~ref.ipv4_checksum(bytes(ip))) & 0xFFFF
+    ip[10:12] = c.to_bytes(2, "little")
+    f = bytearray(eth + bytes(ip) + seg)
+    if len(f) < pad_to:
+        f += bytes(pad_to - len(f))        # Ethernet minimum-size padding
+    return f
+
+
+def frames(ref: Reference, orc: Oracle) -> dict:
+    rng = np.random.default_rng(2020)
+    out = []
+    for i in range(3000):
+        kind = i % 16
+        payload = int(rng.choice([0, 1, 2, 7, 8, 31, 64, 100, 512, 1459, 1460,
+                                  int(rng.integers(0, 1461))]))
+        f = _make_frame(ref, rng, payload, pad_to=60)
+        if kind == 1:                                   # IP header bit flip
+            b = 14 + int(rng.integers(0, 20))
+            f[b] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 2 and len(f) > 34:                 # TCP bit flip
+            b = 34 + int(rng.integers(0, len(f) - 34))
+            f[b] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 3:
+            f[14] = 0x46                                # IP options: unsupported
+        elif kind == 4:
+            f[20] |= 0x01                               # fragment offset
+        elif kind == 5:
+            f[23] = 17                                  # UDP
+        elif kind == 6:
+            f[12:14] = b"\x08\x06"                      # ARP
+        elif kind == 7:
+            f = f[:max(34, len(f) - int(rng.integers(1, 40)))]   # truncated
+        elif kind == 8:
+            f[16:18] = (10).to_bytes(2, "big")          # total length < 20
+        elif kind == 9:
+            f = f[:int(rng.integers(0, 34))]            # runt
+        elif kind == 10:
+            f[21] = 1                                   # fragment (low offset byte)
+        elif kind == 11:
+            f[20] = 0x80 | (f[20] & 0x3F)               # reserved flag bit only
+        if kind in (4, 5, 8, 10, 11) and i % 32 < 16:   # re-seal the IP header
+            f[24:26] = b"\0\0"
+            c = (~ref.ipv4_checksum(bytes(f[14:34]))) & 0xFFFF
+            f[24:26] = c.to_bytes(2, "little")
+        out.append(bytes(f))
+    lens = np.array([len(f) for f in out], dtype=np.uint16)
+    gaps = rng.integers(0, 16, len(out))
+    offs, pos, chunks = [], 3, [rng.integers(0, 256, 3, dtype=np.uint8).tobytes()]
+    for f, g in zip(out, gaps):
+        offs.append(pos)
+        chunks.append(f + rng.integers(0, 256, int(g), dtype=np.uint8).tobytes())
+        pos += len(f) + int(g)
+    arena = np.frombuffer(b"".join(chunks) + bytes(64), dtype=np.uint8)
+    offs = np.array(offs, dtype=np.uint64)
+    expect = np.array([_ref_frame_flags(ref, f) for f in out], dtype=np.uint8)
+    np.testing.assert_array_equal(orc.validate_frames(arena, offs, lens), expect)
+    return dict(arena=arena, offsets=offs, lengths=lens, expect=expect)
+
+
 def main():
     ref = Reference()
     orc = Oracle()
+    fr = frames(ref, orc)
+    np.savez_compressed(os.path.join(HERE, "frames.npz"), **fr)
     np.savez_compressed(os.path.join(HERE, "rss.npz"), **rss(ref))
     rows = kat(ref)
     with open(os.path.join(HERE, "kat.json"), "w") as f:

@@ -1,0 +1,219 @@
+"""Batched receive-side frame validation.
+
+Pins: tests/golden/frames.npz — 3000 Ethernet frames (well-formed, with IP /
+TCP bit flips, IP options, fragments, UDP, ARP, truncations, runts, bogus
+total lengths) whose expected TULIPS_FRAME_* flags were computed with the
+REFERENCE's own ipv4::checksum and tcpv4::Processor::checksum
+(tests/golden/make_golden.py::frames). Larger cases (mutations, jumbo
+frames, every base alignment) are checked against the oracle's
+orc_validate_frames, itself pinned to the fixture here.
+"""
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "frames.npz")
+
+IPV4, IP_OK, TCP, L4_OK, TRUNC = 0x01, 0x02, 0x04, 0x08, 0x10
+
+
+def frames_fixture():
+    with np.load(GOLDEN, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def counters_of(flags):
+    f = np.asarray(flags)
+    ipv4 = (f & IPV4) != 0
+    tcp = (f & TCP) != 0
+    return np.array([ipv4.sum(), (ipv4 & ((f & IP_OK) == 0)).sum(), tcp.sum(),
+                     (tcp & ((f & L4_OK) == 0)).sum()], dtype=np.uint32)
+
+
+def make_frame(oracle, rng, payload):
+    """Well-formed Ethernet/IPv4/TCP frame, checksums from the oracle."""
+    src = int(rng.integers(0, 2**32))
+    dst = int(rng.integers(0, 2**32))
+    tcp = bytearray(rng.integers(0, 256, 20, dtype=np.uint8).tobytes())
+    tcp[12] = 0x50
+    tcp[16:18] = b"\0\0"
+    seg = bytes(tcp) + rng.integers(0, 256, payload, dtype=np.uint8).tobytes()
+    c = (~oracle.tcp_checksum(src, dst, seg)) & 0xFFFF
+    seg = seg[:16] + c.to_bytes(2, "little") + seg[18:]
+    ip = bytearray(b"\x45\x00" + (20 + len(seg)).to_bytes(2, "big") + b"\x12\x34\x40\x00\x40\x06"
+                   + b"\0\0" + src.to_bytes(4, "little") + dst.to_bytes(4, "little"))
+    c = (~oracle.ipv4_checksum(bytes(ip))) & 0xFFFF
+    ip[10:12] = c.to_bytes(2, "little")
+    return bytes(rng.integers(0, 256, 12, dtype=np.uint8).tobytes() + b"\x08\x00" + ip + seg)
+
+
+def pack(frames, rng, gap=16, lead=0):
+    offs, pos, parts = [], lead, [bytes(lead)]
+    for f in frames:
+        offs.append(pos)
+        g = int(rng.integers(0, gap)) if gap else 0
+        parts.append(f + bytes(g))
+        pos += len(f) + g
+    arena = np.frombuffer(b"".join(parts) + bytes(64), dtype=np.uint8)
+    return arena, np.array(offs, dtype=np.uint64), np.array([len(f) for f in frames],
+                                                             dtype=np.uint16)
+
+
+def mutate(fx, rng, nflips):
+    """The fixture arena with random byte flips (header-heavy)."""
+    arena = fx["arena"].copy()
+    offs, lens = fx["offsets"], fx["lengths"]
+    pick = rng.integers(0, len(offs), nflips)
+    where = np.minimum(rng.integers(0, 64, nflips), np.maximum(lens[pick].astype(np.int64) - 1, 0))
+    arena[offs[pick].astype(np.int64) + where] ^= rng.integers(1, 256, nflips, dtype=np.uint8)
+    return arena
+
+
+# ---------------------------------------------------------------- CPU -----
+def test_oracle_matches_fixture(oracle):
+    fx = frames_fixture()
+    got = oracle.validate_frames(fx["arena"], fx["offsets"], fx["lengths"])
+    np.testing.assert_array_equal(got, fx["expect"])
+
+
+def test_fixture_covers_every_outcome():
+    fx = frames_fixture()
+    seen = set(int(x) for x in np.unique(fx["expect"]))
+    # not IPv4, runt, IPv4 only (bad/good csum), TCP good/bad, truncated
+    for want in (0, TRUNC, IPV4, IPV4 | IP_OK, IPV4 | IP_OK | TCP | L4_OK,
+                 IPV4 | IP_OK | TCP, IPV4 | TCP | L4_OK, IPV4 | IP_OK | TCP | TRUNC):
+        assert want in seen, hex(want)
+    assert int(fx["lengths"].min()) == 0 and int(fx["lengths"].max()) >= 1514
+
+
+def test_oracle_jumbo_frames(oracle):
+    rng = np.random.default_rng(5)
+    fr = [make_frame(oracle, rng, p) for p in (8946, 9000 - 54, 65535 - 54)]
+    arena, offs, lens = pack(fr, rng)
+    assert list(oracle.validate_frames(arena, offs, lens)) == [0x0F] * 3
+
+
+def test_capi_arguments_without_gpu():
+    from tulips_amd import csum
+    L = csum.lib
+    assert L.tulips_csum_validate_frames(None, None, None, 0, None, None, None) == 0
+    # neither flags nor counters
+    assert L.tulips_csum_validate_frames(0x1000, 0x1000, 0x1000, 4, None, None, None) == 1
+    assert L.tulips_csum_validate_frames(None, 0x1000, 0x1000, 4, 0x1000, None, None) == 1
+    assert L.tulips_csum_validate_frames_host(None, None, None, None, 0, None, None) == 1
+    for name in ("FRAME_IPV4", "FRAME_IP_CSUM_OK", "FRAME_TCP", "FRAME_L4_CSUM_OK",
+                 "FRAME_TRUNCATED"):
+        assert hasattr(csum, name)
+    assert (csum.FRAME_IPV4, csum.FRAME_IP_CSUM_OK, csum.FRAME_TCP, csum.FRAME_L4_CSUM_OK,
+            csum.FRAME_TRUNCATED) == (IPV4, IP_OK, TCP, L4_OK, TRUNC)
+
+
+# ---------------------------------------------------------------- GPU -----
+def _dev(*arrs):
+    import torch
+    return [torch.from_numpy(np.array(a, copy=True)).to("cuda:0") for a in arrs]
+
+
+def _run(arena, offs, lens, counters=True):
+    import torch
+    from tulips_amd import csum
+    a, o, l = _dev(arena, offs.astype(np.int64), lens.view(np.int16))
+    cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda:0") if counters else None
+    fl = csum.validate_frames(a, o, l, counters=cnt)
+    torch.cuda.synchronize()
+    c = cnt.cpu().numpy().view(np.uint32) if counters else None
+    return fl.cpu().numpy(), c
+
+
+@pytest.mark.gpu
+def test_gpu_fixture():
+    fx = frames_fixture()
+    got, cnt = _run(fx["arena"], fx["offsets"], fx["lengths"])
+    np.testing.assert_array_equal(got, fx["expect"])
+    np.testing.assert_array_equal(cnt, counters_of(fx["expect"]))
+
+
+@pytest.mark.gpu
+def test_gpu_counters_only():
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    a, o, l = _dev(fx["arena"], fx["offsets"].astype(np.int64), fx["lengths"].view(np.int16))
+    cnt = torch.zeros(4, dtype=torch.int32, device="cuda:0")
+    assert csum.validate_frames(a, o, l, counters=cnt, want_flags=False) is None
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),
+                                  counters_of(fx["expect"]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", range(16))
+def test_gpu_every_base_alignment(shift):
+    fx = frames_fixture()
+    arena = np.concatenate([np.zeros(shift, np.uint8), fx["arena"]])
+    got, _ = _run(arena, fx["offsets"] + np.uint64(shift), fx["lengths"], counters=False)
+    np.testing.assert_array_equal(got, fx["expect"])
+
+
+@pytest.mark.gpu
+def test_gpu_mutations_vs_oracle(oracle):
+    fx = frames_fixture()
+    rng = np.random.default_rng(11)
+    for rnd in range(4):
+        arena = mutate(fx, rng, 2000)
+        exp = oracle.validate_frames(arena, fx["offsets"], fx["lengths"])
+        got, cnt = _run(arena, fx["offsets"], fx["lengths"])
+        np.testing.assert_array_equal(got, exp, err_msg=f"round {rnd}")
+        np.testing.assert_array_equal(cnt, counters_of(exp))
+
+
+@pytest.mark.gpu
+def test_gpu_jumbo_and_max_frames(oracle):
+    rng = np.random.default_rng(6)
+    pays = [8946, 9000 - 54, 16000, 32768, 65535 - 54, 0, 1, 1460]
+    fr = [make_frame(oracle, rng, p) for p in pays]
+    bad = bytearray(fr[4])
+    bad[-1] ^= 0x40                     # last byte of a 65535-byte frame
+    fr.append(bytes(bad))
+    arena, offs, lens = pack(fr, rng)
+    exp = oracle.validate_frames(arena, offs, lens)
+    assert list(exp[:-1]) == [0x0F] * len(pays) and exp[-1] == 0x07
+    got, _ = _run(arena, offs, lens)
+    np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.gpu
+def test_gpu_large_batch_tiled():
+    """The fixture tiled 256x (768k frames, ~312 MB) — many grid-stride rounds."""
+    fx = frames_fixture()
+    reps = 256
+    span = np.uint64(len(fx["arena"]))
+    arena = np.tile(fx["arena"], reps)
+    offs = (fx["offsets"][None, :] + span * np.arange(reps, dtype=np.uint64)[:, None]).ravel()
+    lens = np.tile(fx["lengths"], reps)
+    got, cnt = _run(arena, offs, lens)
+    exp = np.tile(fx["expect"], reps)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(cnt, counters_of(exp))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [False, True])
+def test_gpu_host_context(oracle, pinned):
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(12)
+    arena = mutate(fx, rng, 1500)
+    exp = oracle.validate_frames(arena, fx["offsets"], fx["lengths"])
+    if pinned:
+        t = torch.from_numpy(arena).pin_memory()
+        src = t.numpy()
+    else:
+        src = arena
+    # a small chunk so the 1.2 MB batch crosses many pipeline stages
+    with csum.HostContext(0, chunk_bytes=1 << 17) as ctx:
+        got, cnt = ctx.validate_frames(src, fx["offsets"], fx["lengths"], with_counters=True)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(cnt, counters_of(exp))

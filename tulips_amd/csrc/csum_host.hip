@@ -45,6 +45,7 @@ struct Slot
   uint32_t* h_src = nullptr;
   uint32_t* h_dst = nullptr;
   uint16_t* h_out = nullptr;
+  uint32_t* h_cnt = nullptr;
   uint8_t* d_bytes = nullptr;
   uint64_t* d_offs = nullptr;
   uint16_t* d_lens = nullptr;
@@ -52,6 +53,7 @@ struct Slot
   uint32_t* d_src = nullptr;
   uint32_t* d_dst = nullptr;
   uint16_t* d_out = nullptr;
+  uint32_t* d_cnt = nullptr;
   bool busy = false;
   uint32_t i0 = 0, i1 = 0;
 };
@@ -101,6 +103,7 @@ free_slot(Slot& s)
   (void)hipHostFree(s.h_src);
   (void)hipHostFree(s.h_dst);
   (void)hipHostFree(s.h_out);
+  (void)hipHostFree(s.h_cnt);
   (void)hipFree(s.d_bytes);
   (void)hipFree(s.d_offs);
   (void)hipFree(s.d_lens);
@@ -108,6 +111,7 @@ free_slot(Slot& s)
   (void)hipFree(s.d_src);
   (void)hipFree(s.d_dst);
   (void)hipFree(s.d_out);
+  (void)hipFree(s.d_cnt);
   if (s.done) {
     (void)hipEventDestroy(s.done);
   }
@@ -135,6 +139,7 @@ alloc_slot(Slot& s, uint64_t chunk)
   TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_src), m * 4, 0));
   TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_dst), m * 4, 0));
   TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), m * 2, 0));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_cnt), 16, 0));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_bytes), chunk));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_offs), m * 8));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_lens), m * 2));
@@ -142,20 +147,41 @@ alloc_slot(Slot& s, uint64_t chunk)
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_src), m * 4));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_dst), m * 4));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_out), m * 2));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_cnt), 16));
 #undef TCS_TRY
   return hipSuccess;
 }
 
-// Collect the results of a finished slot into the caller's array.
+// What a pipeline run computes: checksums (uint16 per segment) or frame
+// flags (uint8 per frame, plus optional counters).
+struct Job
+{
+  bool frames = false;
+  const uint16_t* seeds = nullptr;
+  const uint32_t* src = nullptr;
+  const uint32_t* dst = nullptr;
+  uint32_t mode = 0;
+  uint8_t* out = nullptr; // host results, elem() bytes per entry
+  uint32_t* counters = nullptr;
+  size_t elem() const { return frames ? 1 : 2; }
+};
+
+// Collect the results of a finished slot into the caller's arrays.
 hipError_t
-retire(Slot& s, uint16_t* out)
+retire(Slot& s, const Job& job)
 {
   if (!s.busy) {
     return hipSuccess;
   }
   const hipError_t e = hipEventSynchronize(s.done);
   if (e == hipSuccess) {
-    memcpy(out + s.i0, s.h_out, size_t(s.i1 - s.i0) * 2);
+    memcpy(job.out + size_t(s.i0) * job.elem(), s.h_out,
+           size_t(s.i1 - s.i0) * job.elem());
+    if (job.counters) {
+      for (int k = 0; k < 4; ++k) {
+        job.counters[k] += s.h_cnt[k];
+      }
+    }
   }
   s.busy = false;
   return e;
@@ -254,25 +280,14 @@ tulips_csum_ctx_destroy(tulips_csum_ctx* ctx)
   return TULIPS_STATUS_OK;
 }
 
+} // extern "C"
+
+namespace {
+
 int
-tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
-                       const uint64_t* offsets, const uint16_t* lengths,
-                       const uint16_t* seeds, const uint32_t* src,
-                       const uint32_t* dst, uint16_t* out, uint32_t n,
-                       uint32_t mode)
+run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
+    const uint16_t* lengths, uint32_t n, const Job& job)
 {
-  if (!ctx) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  if (n == 0) {
-    return TULIPS_STATUS_OK;
-  }
-  const uint32_t m = mode & TULIPS_CSUM_MODE_MASK;
-  if (!base || !offsets || !lengths || !out ||
-      (mode & ~(TULIPS_CSUM_MODE_MASK | TULIPS_CSUM_COMPLEMENT)) ||
-      m > TULIPS_CSUM_TCP || (m == TULIPS_CSUM_TCP && (!src || !dst))) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
   int prev = 0;
   (void)hipGetDevice(&prev);
   hipError_t e = hipSetDevice(ctx->device);
@@ -280,12 +295,11 @@ tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
     return status_of(e);
   }
   const bool pinned = is_pinned(base);
-  const bool tcp = m == TULIPS_CSUM_TCP;
   int slot = 0;
   uint32_t i = 0;
   while (i < n && e == hipSuccess) {
     Slot& s = ctx->slots[slot];
-    if ((e = retire(s, out)) != hipSuccess) {
+    if ((e = retire(s, job)) != hipSuccess) {
       break;
     }
     // Cut the chunk: segments [i, j) with at most ctx->chunk bytes.
@@ -316,12 +330,12 @@ tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
       hbytes = bytes;
     }
     memcpy(s.h_lens, lengths + i, size_t(cnt) * 2);
-    if (seeds && !tcp) {
-      memcpy(s.h_seeds, seeds + i, size_t(cnt) * 2);
+    if (job.seeds) {
+      memcpy(s.h_seeds, job.seeds + i, size_t(cnt) * 2);
     }
-    if (tcp) {
-      memcpy(s.h_src, src + i, size_t(cnt) * 4);
-      memcpy(s.h_dst, dst + i, size_t(cnt) * 4);
+    if (job.src) {
+      memcpy(s.h_src, job.src + i, size_t(cnt) * 4);
+      memcpy(s.h_dst, job.dst + i, size_t(cnt) * 4);
     }
     hipStream_t st = s.stream;
 #define TCS_Q(x)                                                               \
@@ -333,32 +347,44 @@ tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
                          hipMemcpyHostToDevice, st));
     TCS_Q(hipMemcpyAsync(s.d_lens, s.h_lens, size_t(cnt) * 2,
                          hipMemcpyHostToDevice, st));
-    if (seeds && !tcp) {
+    if (job.seeds) {
       TCS_Q(hipMemcpyAsync(s.d_seeds, s.h_seeds, size_t(cnt) * 2,
                            hipMemcpyHostToDevice, st));
     }
-    if (tcp) {
+    if (job.src) {
       TCS_Q(hipMemcpyAsync(s.d_src, s.h_src, size_t(cnt) * 4,
                            hipMemcpyHostToDevice, st));
       TCS_Q(hipMemcpyAsync(s.d_dst, s.h_dst, size_t(cnt) * 4,
                            hipMemcpyHostToDevice, st));
     }
-    LaunchArgs a{};
-    a.seeds = (seeds && !tcp) ? s.d_seeds : nullptr;
-    a.src = tcp ? s.d_src : nullptr;
-    a.dst = tcp ? s.d_dst : nullptr;
-    a.out = s.d_out;
-    a.bad = nullptr;
-    a.n = cnt;
-    a.mode = mode;
-    a.kind = TULIPS_CSUM_KIND_HYBRID; // the variable-length default
-    a.group = 16;
-    a.spw = 1;
-    a.unroll = 4;
-    a.nontemporal = true;
-    a.max_blocks = 0;
-    TCS_Q(launch_var(dbase, s.d_offs, s.d_lens, a, st));
-    TCS_Q(hipMemcpyAsync(s.h_out, s.d_out, size_t(cnt) * 2,
+    if (job.frames) {
+      if (job.counters) {
+        TCS_Q(hipMemsetAsync(s.d_cnt, 0, 16, st));
+      }
+      TCS_Q(launch_frames(dbase, s.d_offs, s.d_lens, cnt,
+                          reinterpret_cast<uint8_t*>(s.d_out),
+                          job.counters ? s.d_cnt : nullptr, st));
+      if (job.counters) {
+        TCS_Q(hipMemcpyAsync(s.h_cnt, s.d_cnt, 16, hipMemcpyDeviceToHost, st));
+      }
+    } else {
+      LaunchArgs a{};
+      a.seeds = job.seeds ? s.d_seeds : nullptr;
+      a.src = job.src ? s.d_src : nullptr;
+      a.dst = job.src ? s.d_dst : nullptr;
+      a.out = s.d_out;
+      a.bad = nullptr;
+      a.n = cnt;
+      a.mode = job.mode;
+      a.kind = TULIPS_CSUM_KIND_HYBRID; // the variable-length default
+      a.group = 16;
+      a.spw = 1;
+      a.unroll = 4;
+      a.nontemporal = true;
+      a.max_blocks = 0;
+      TCS_Q(launch_var(dbase, s.d_offs, s.d_lens, a, st));
+    }
+    TCS_Q(hipMemcpyAsync(s.h_out, s.d_out, size_t(cnt) * job.elem(),
                          hipMemcpyDeviceToHost, st));
     TCS_Q(hipEventRecord(s.done, st));
 #undef TCS_Q
@@ -369,13 +395,70 @@ tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
     slot ^= 1;
   }
   for (auto& s : ctx->slots) {
-    const hipError_t r = retire(s, out);
+    const hipError_t r = retire(s, job);
     if (e == hipSuccess) {
       e = r;
     }
   }
   (void)hipSetDevice(prev);
   return status_of(e);
+}
+
+} // namespace
+
+extern "C" {
+
+int
+tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
+                       const uint64_t* offsets, const uint16_t* lengths,
+                       const uint16_t* seeds, const uint32_t* src,
+                       const uint32_t* dst, uint16_t* out, uint32_t n,
+                       uint32_t mode)
+{
+  if (!ctx) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  const uint32_t m = mode & TULIPS_CSUM_MODE_MASK;
+  if (!base || !offsets || !lengths || !out ||
+      (mode & ~(TULIPS_CSUM_MODE_MASK | TULIPS_CSUM_COMPLEMENT)) ||
+      m > TULIPS_CSUM_TCP || (m == TULIPS_CSUM_TCP && (!src || !dst))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  Job job;
+  job.mode = mode;
+  job.seeds = m == TULIPS_CSUM_TCP ? nullptr : seeds;
+  job.src = m == TULIPS_CSUM_TCP ? src : nullptr;
+  job.dst = m == TULIPS_CSUM_TCP ? dst : nullptr;
+  job.out = reinterpret_cast<uint8_t*>(out);
+  return run(ctx, base, offsets, lengths, n, job);
+}
+
+int
+tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
+                                 const uint64_t* offsets,
+                                 const uint16_t* lengths, uint32_t n,
+                                 uint8_t* flags, uint32_t* counters)
+{
+  if (!ctx) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (counters) {
+    memset(counters, 0, 4 * sizeof(uint32_t));
+  }
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths || !flags) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  Job job;
+  job.frames = true;
+  job.out = flags;
+  job.counters = counters;
+  return run(ctx, base, offsets, lengths, n, job);
 }
 
 } // extern "C"

@@ -121,7 +121,17 @@ _SIGNATURES = {
                                            C.POINTER(C.c_uint32)]),
     "tulips_rss_toeplitz_batch": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _u8p,
                                             C.c_size_t, C.c_uint32, _vp, _vp]),
+    "tulips_csum_validate_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
+    "tulips_csum_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
+                                                   _vp]),
 }
+
+# include/tulips_csum.h TULIPS_FRAME_* (per-frame validation flags)
+FRAME_IPV4 = 0x01
+FRAME_IP_CSUM_OK = 0x02
+FRAME_TCP = 0x04
+FRAME_L4_CSUM_OK = 0x08
+FRAME_TRUNCATED = 0x10
 
 # Exported C++ symbols of the reference surface (host scalar drop-ins).
 CXX_SYMBOLS = (
@@ -375,6 +385,26 @@ class HostContext:
         _check(rc, "tulips_csum_batch_host")
         return out
 
+    def validate_frames(self, arena, offsets, lengths, *, flags=None,
+                        with_counters: bool = False):
+        """Host-resident frames -> uint8 FRAME_* flags (and the 4 counters)."""
+        import numpy as np
+        ar = arena if isinstance(arena, int) else _host(arena, np.uint8)
+        base = ar if isinstance(ar, int) else ar.ptr
+        off = _host(offsets, np.uint64)
+        ln = _host(lengths, np.uint16)
+        n = len(off.keep)
+        if len(ln.keep) != n:
+            raise ValueError("offsets/lengths size mismatch")
+        if flags is None:
+            flags = np.empty(n, dtype=np.uint8)
+        cnt = np.zeros(4, dtype=np.uint32)
+        rc = lib.tulips_csum_validate_frames_host(
+            self._h, base, off.ptr, ln.ptr, n, flags.ctypes.data,
+            cnt.ctypes.data if with_counters else None)
+        _check(rc, "tulips_csum_validate_frames_host")
+        return (flags, cnt) if with_counters else flags
+
 
 def toeplitz(saddr: int, daddr: int, sport: int, dport: int, key: bytes,
              init: int = 0) -> int:
@@ -402,6 +432,30 @@ def rss_batch(saddr, daddr, sport, dport, key: bytes, init: int = 0, out=None,
                                          _addr(out), _stream(stream)),
            "tulips_rss_toeplitz_batch")
     return out
+
+
+def validate_frames(arena, offsets, lengths, *, flags=None, counters=None,
+                    want_flags: bool = True, stream=None):
+    """Validate Ethernet/IPv4/TCP frames arena[offsets[i]:][:lengths[i]].
+
+    Returns the uint8 FRAME_* flags tensor (None when want_flags is False and
+    no `flags` is given); `counters` (int32[4] device tensor, zeroed by the
+    call) receives {IPv4, bad IP checksum, TCP, TCP without L4_CSUM_OK}.
+    """
+    import torch
+    n = int(offsets.numel())
+    if int(lengths.numel()) != n:
+        raise ValueError("offsets/lengths size mismatch")
+    _check_sizes(n, flags=flags)
+    if flags is None and want_flags:
+        flags = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    if counters is not None and int(counters.numel()) < 4:
+        raise ValueError("counters needs 4 entries")
+    _check(lib.tulips_csum_validate_frames(_addr(arena), _addr(offsets), _addr(lengths),
+                                           n, _addr(flags), _addr(counters),
+                                           _stream(stream)),
+           "tulips_csum_validate_frames")
+    return flags
 
 
 def version() -> str:
