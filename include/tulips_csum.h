@@ -129,6 +129,11 @@ int tulips_csum_ctx_create(int device, uint64_t chunk_bytes,
                            tulips_csum_ctx** ctx);
 int tulips_csum_ctx_destroy(tulips_csum_ctx* ctx);
 
+/* Page-locked host memory (hipHostMalloc): an arena staged here is DMA'd
+ * straight to HBM by the *_host entry points, skipping their packing copy. */
+int tulips_csum_host_alloc(size_t bytes, void** ptr);
+int tulips_csum_host_free(void* ptr);
+
 /* All pointers are host pointers; blocks until `out` holds every result. */
 int tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
                            const uint64_t* offsets, const uint16_t* lengths,

@@ -1,0 +1,158 @@
+#pragma once
+/*
+ * tulips::transport::gpucsum::Device — batched receive-side checksum
+ * validation on an MI355X.
+ *
+ * A transport decorator in the pattern of the reference's check::Device
+ * (include/tulips/transport/check/Device.h, src/transport/check/Device.cpp:
+ * 14-36): it wraps any transport::Device, drains up to `burst` frames per
+ * poll from it into a page-locked staging arena, validates the whole burst
+ * in one GPU launch (tulips_csum_validate_frames_host: Ethernet -> IPv4
+ * header checksum -> TCP pseudo-header checksum, include/tulips_csum.h),
+ * and forwards to the stack only the frames that pass, in arrival order.
+ *
+ * It realises the Device::VALIDATE_IP_CSUM / VALIDATE_L4_CSUM hints
+ * (include/tulips/transport/Device.h:29-30) the way the ENA and OFED
+ * transports do with NIC offload bits (src/transport/ena/Device.cpp:
+ * 316-340, src/transport/ofed/Device.cpp:528-545): a frame whose IPv4
+ * header checksum fails is dropped under VALIDATE_IP_CSUM; a TCP frame whose
+ * checksum fails, or that is shorter than its IP length announces, is
+ * dropped under VALIDATE_L4_CSUM; everything else is forwarded untouched.
+ * api::Client/Server set both hints when the stack is built with
+ * TULIPS_DISABLE_CHECKSUM_CHECK (src/api/Client.cpp:39-41,
+ * src/api/Server.cpp:32-34); the `hints` constructor argument sets them up
+ * front for stacks that do not.
+ *
+ * Ownership follows the reference: the inner device's buffer is borrowed
+ * only for the process() call, so each frame is copied into the staging
+ * arena there; forwarded frames point into the arena and are valid for the
+ * duration of the downstream process() call.
+ */
+
+#include <tulips/transport/Device.h>
+#include <cstdint>
+#include <vector>
+
+struct tulips_csum_ctx;
+
+namespace tulips::transport::gpucsum {
+
+class Device
+  : public transport::Device
+  , public Processor
+{
+public:
+  struct Statistics
+  {
+    uint64_t frames = 0;     // received from the inner device
+    uint64_t forwarded = 0;  // handed to the stack
+    uint64_t bad_ip = 0;     // dropped: IPv4 header checksum
+    uint64_t bad_l4 = 0;     // dropped: TCP checksum / truncation
+    uint64_t batches = 0;    // GPU launches
+  };
+
+  static constexpr uint32_t DEFAULT_BURST = 1024;
+
+  static Ref allocate(system::Logger& log, transport::Device::Ref device,
+                      const int gpu = 0, const uint32_t burst = DEFAULT_BURST,
+                      const uint16_t hints = 0)
+  {
+    return std::make_unique<Device>(log, std::move(device), gpu, burst, hints);
+  }
+
+  /*
+   * Throws std::runtime_error when the GPU context cannot be created (no
+   * device, no libtulips_csum): there is no CPU fallback.
+   */
+  Device(system::Logger& log, transport::Device::Ref device, const int gpu,
+         const uint32_t burst, const uint16_t hints);
+  ~Device() override;
+
+  /*
+   * Device interface: everything but poll/wait passes through.
+   */
+
+  std::string_view name() const override { return m_device->name(); }
+
+  stack::ethernet::Address const& address() const override
+  {
+    return m_device->address();
+  }
+
+  Status listen(const stack::ipv4::Protocol proto,
+                stack::ipv4::Address const& laddr, const uint16_t lport,
+                stack::ipv4::Address const& raddr,
+                const uint16_t rport) override
+  {
+    return m_device->listen(proto, laddr, lport, raddr, rport);
+  }
+
+  void unlisten(const stack::ipv4::Protocol proto,
+                stack::ipv4::Address const& laddr, const uint16_t lport,
+                stack::ipv4::Address const& raddr,
+                const uint16_t rport) override
+  {
+    m_device->unlisten(proto, laddr, lport, raddr, rport);
+  }
+
+  Status poll(Processor& proc) override;
+  Status wait(Processor& proc, const uint64_t ns) override;
+
+  uint32_t mtu() const override { return m_device->mtu(); }
+  uint32_t mss() const override { return m_device->mss(); }
+
+  uint8_t receiveBufferLengthLog2() const override
+  {
+    return m_device->receiveBufferLengthLog2();
+  }
+
+  uint16_t receiveBuffersAvailable() const override
+  {
+    return m_device->receiveBuffersAvailable();
+  }
+
+  bool identify(const uint8_t* const buf) const override
+  {
+    return m_device->identify(buf);
+  }
+
+  Status prepare(uint8_t*& buf) override { return m_device->prepare(buf); }
+
+  Status commit(const uint16_t len, uint8_t* const buf,
+                const uint16_t mss = 0) override
+  {
+    return m_device->commit(len, buf, mss);
+  }
+
+  Status release(uint8_t* const buf) override
+  {
+    return m_device->release(buf);
+  }
+
+  Statistics const& statistics() const { return m_stats; }
+
+private:
+  Status run() override { return Status::Ok; }
+  Status process(const uint16_t len, const uint8_t* const data,
+                 const Timestamp ts) override;
+  Status sent(const uint16_t len, uint8_t* const buf) override;
+
+  Status drain();
+  Status flush();
+
+  transport::Device::Ref m_device;
+  Processor* m_proc;
+  tulips_csum_ctx* m_ctx;
+  uint32_t m_burst;
+  uint8_t* m_arena;
+  size_t m_capacity;
+  size_t m_used;
+  std::vector<uint64_t> m_offsets;
+  std::vector<uint16_t> m_lengths;
+  std::vector<Timestamp> m_stamps;
+  std::vector<uint8_t> m_flags;
+  Status m_error;
+  Statistics m_stats;
+};
+
+}

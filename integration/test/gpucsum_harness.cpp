@@ -1,0 +1,111 @@
+// TEST INFRASTRUCTURE — drives tulips::transport::gpucsum::Device the way
+// the reference's stack does: frames committed on one reference
+// list::Device (src/transport/list/Device.cpp) arrive on its peer, which is
+// wrapped by the decorator; a recording Processor stands where the stack's
+// ethernet::Processor would. Called from tests/test_gpucsum_device.py.
+#include <tulips/stack/Ethernet.h>
+#include <tulips/system/Logger.h>
+#include <tulips/transport/gpucsum/Device.h>
+#include <tulips/transport/list/Device.h>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <vector>
+
+using namespace tulips;
+
+namespace {
+
+uint64_t
+fnv1a(const uint8_t* p, size_t n)
+{
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (size_t i = 0; i < n; ++i) {
+    h = (h ^ p[i]) * 0x100000001b3ull;
+  }
+  return h;
+}
+
+struct Recorder : transport::Processor
+{
+  std::vector<std::pair<uint16_t, uint64_t>> got;
+  uint64_t sent_count = 0;
+
+  Status run() override { return Status::Ok; }
+
+  Status process(const uint16_t len, const uint8_t* const data,
+                 const Timestamp) override
+  {
+    got.emplace_back(len, fnv1a(data, len));
+    return Status::Ok;
+  }
+
+  Status sent(const uint16_t, uint8_t* const) override
+  {
+    sent_count += 1;
+    return Status::Ok;
+  }
+};
+
+constexpr uint32_t LIST_MTU = 65536;
+
+}
+
+extern "C" int
+gpucsum_run(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
+            uint32_t n, uint32_t burst, uint16_t hints, int use_wait,
+            uint8_t* forwarded, uint64_t* stats)
+{
+  try {
+    system::ConsoleLogger log(system::Logger::Level::Error);
+    transport::list::Device::List a2b, b2a;
+    stack::ethernet::Address mac(0x02, 0, 0, 0, 0, 1);
+    auto peer = transport::list::Device::allocate(log, mac, LIST_MTU, b2a, a2b);
+    auto rx = transport::list::Device::allocate(log, mac, LIST_MTU, a2b, b2a);
+    for (uint32_t i = 0; i < n; ++i) {
+      uint8_t* buf = nullptr;
+      if (peer->prepare(buf) != Status::Ok) {
+        return -3;
+      }
+      memcpy(buf, arena + offs[i], lens[i]);
+      if (peer->commit(lens[i], buf, 0) != Status::Ok) {
+        return -3;
+      }
+    }
+    transport::gpucsum::Device dev(log, std::move(rx), 0, burst, hints);
+    Recorder rec;
+    Status s = Status::Ok;
+    for (uint64_t it = 0; it <= uint64_t(n) + 2; ++it) {
+      s = use_wait ? dev.wait(rec, 1000) : dev.poll(rec);
+      if (s != Status::Ok) {
+        break;
+      }
+    }
+    if (s != Status::NoDataAvailable) {
+      fprintf(stderr, "gpucsum_run: poll ended with %s\n", toString(s).c_str());
+      return -4;
+    }
+    // Forwarded frames keep arrival order: match them to the inputs.
+    memset(forwarded, 0, n);
+    uint32_t j = 0;
+    for (auto const& [len, h] : rec.got) {
+      while (j < n && !(lens[j] == len && fnv1a(arena + offs[j], lens[j]) == h)) {
+        ++j;
+      }
+      if (j == n) {
+        return -2;
+      }
+      forwarded[j++] = 1;
+    }
+    auto const& st = dev.statistics();
+    stats[0] = st.frames;
+    stats[1] = st.forwarded;
+    stats[2] = st.bad_ip;
+    stats[3] = st.bad_l4;
+    stats[4] = st.batches;
+    return 0;
+  } catch (std::exception const& e) {
+    fprintf(stderr, "gpucsum_run: %s\n", e.what());
+    return -1;
+  }
+}

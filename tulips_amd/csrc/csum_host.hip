@@ -409,6 +409,22 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
 extern "C" {
 
 int
+tulips_csum_host_alloc(size_t bytes, void** ptr)
+{
+  if (!ptr || bytes == 0) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  *ptr = nullptr;
+  return status_of(hipHostMalloc(ptr, bytes, 0));
+}
+
+int
+tulips_csum_host_free(void* ptr)
+{
+  return ptr ? status_of(hipHostFree(ptr)) : TULIPS_STATUS_OK;
+}
+
+int
 tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
                        const uint64_t* offsets, const uint16_t* lengths,
                        const uint16_t* seeds, const uint32_t* src,

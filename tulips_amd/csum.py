@@ -121,6 +121,8 @@ _SIGNATURES = {
                                            C.POINTER(C.c_uint32)]),
     "tulips_rss_toeplitz_batch": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _u8p,
                                             C.c_size_t, C.c_uint32, _vp, _vp]),
+    "tulips_csum_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(_vp)]),
+    "tulips_csum_host_free": (C.c_int, [_vp]),
     "tulips_csum_validate_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     "tulips_csum_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
                                                    _vp]),
