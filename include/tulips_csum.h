@@ -196,6 +196,51 @@ int tulips_csum_validate_frames(const uint8_t* base, const uint64_t* offsets,
                                 uint8_t* flags, uint32_t* counters,
                                 void* stream);
 
+/* ---- send-side checksum generation --------------------- */
+/*
+ * Writes, in place, the IPv4 header checksum of every option-less IPv4 frame
+ * (`ipchksum = ~ipv4::checksum(header)`, src/stack/ipv4/Producer.cpp:79-82)
+ * and the TCP checksum of every unfragmented TCP frame over ntohs(len) - 20
+ * segment bytes (`chksum = ~tcpv4 checksum`, src/stack/tcpv4/Send.cpp:
+ * 441-449) — what the reference leaves to the NIC under
+ * TULIPS_HAS_HW_CHECKSUM. The current field contents are ignored (as if
+ * zeroed). Frames must not overlap. flags[i] (may be NULL) reports what was
+ * written with the TULIPS_FRAME_* bits: IP_CSUM_OK = IP checksum written,
+ * L4_CSUM_OK = TCP checksum written (TRUNCATED: the segment did not fit).
+ */
+int tulips_csum_generate_frames(uint8_t* base, const uint64_t* offsets,
+                                const uint16_t* lengths, uint32_t n,
+                                uint8_t* flags, void* stream);
+
+/*
+ * Segmentation offload (what src/transport/ofed/Device.cpp:688-772 asks of
+ * the NIC with IBV_WR_TSO; header length per stack::utils::headerLength,
+ * src/stack/Utils.cpp:67-84). Frame i = in_base[in_offsets[i]..][..
+ * in_lengths[i]]. An option-less IPv4 / unfragmented TCP super-frame whose
+ * payload P = ntohs(len) - 20 - doff*4 exceeds `mss` becomes ceil(P / mss)
+ * frames, segment k carrying payload [k*mss, min(P, (k+1)*mss)) behind the
+ * super-frame's header with: IPv4 total length and id + k, TCP seq +
+ * k*mss, FIN/PSH kept on the last segment only, CWR on the first only, and
+ * both checksums generated. Any other frame is copied whole with checksum
+ * generation as tulips_csum_generate_frames does.
+ *
+ * out_first (n + 1 entries, device) receives the exclusive prefix sum of
+ * the per-frame segment counts: frame i's segments are j = out_first[i] ..
+ * out_first[i+1] - 1, out_first[n] is the total. Segment j is written to
+ * out_base + j * out_stride (out_base 16-byte aligned, out_stride a multiple
+ * of 16) with its length in out_lengths[j]; a segment longer than out_stride
+ * is not written (length 0), nor is any j >= out_capacity. With
+ * out_capacity == 0 only out_first is computed (to size the output).
+ * n <= 2^24, 1 <= mss <= 65535. Input frames are not modified.
+ */
+int tulips_csum_segment_frames(const uint8_t* in_base,
+                               const uint64_t* in_offsets,
+                               const uint16_t* in_lengths, uint32_t n,
+                               uint32_t mss, uint8_t* out_base,
+                               uint64_t out_stride, uint32_t out_capacity,
+                               uint16_t* out_lengths, uint32_t* out_first,
+                               void* stream);
+
 /* Host-resident frames through a context's pinned pipeline; `flags` is a
  * host array of n bytes, `counters` (may be NULL) a host uint32[4]. */
 int tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,

@@ -416,3 +416,164 @@ void orc_validate_frames(const uint8_t* base, const uint64_t* offsets,
     flags[i] = orc_validate_frame(base + offsets[i], lengths[i]);
   }
 }
+
+/* ---------------------------------------------------------------------------
+ * §8f #4 — send-side checksum generation of one frame, in place:
+ *   ipv4/Producer.cpp:79-82   ipchksum = 0; ipchksum = ~ipv4::checksum(hdr)
+ *   tcpv4/Send.cpp:441-449    chksum = 0;   chksum = ~checksum(src, dst, len, seg)
+ * applied to option-less IPv4 frames and unfragmented TCP ones whose
+ * ntohs(len) - 20 byte segment (>= 18 bytes, so the field exists) fits.
+ * Returns the TULIPS_FRAME_* bits: IP_CSUM_OK / L4_CSUM_OK = field written.
+ * ------------------------------------------------------------------------- */
+uint8_t orc_generate_frame(uint8_t* f, uint32_t len)
+{
+  if (len < 14 || ((unsigned)f[12] << 8 | f[13]) != 0x0800u) {
+    return 0;
+  }
+  if (len < 34) {
+    return ORC_FRAME_TRUNCATED;
+  }
+  uint8_t* ip = f + 14;
+  if (ip[0] != 0x45) {
+    return 0;
+  }
+  ip[10] = ip[11] = 0;
+  uint16_t c = (uint16_t)~orc_ipv4_checksum(ip);
+  memcpy(ip + 10, &c, 2);
+  uint8_t fl = ORC_FRAME_IPV4 | ORC_FRAME_IP_CSUM_OK;
+  if ((ip[6] & 0x3f) != 0 || ip[7] != 0 || ip[9] != 6) {
+    return fl;
+  }
+  fl |= ORC_FRAME_TCP;
+  const uint16_t total = (uint16_t)((ip[2] << 8) | ip[3]);
+  const uint16_t tcplen = (uint16_t)(total - 20u);
+  if (total < 20 || 34u + tcplen > len) {
+    return (uint8_t)(fl | ORC_FRAME_TRUNCATED);
+  }
+  if (tcplen < 18) {
+    return fl;
+  }
+  uint32_t src, dst;
+  memcpy(&src, ip + 12, 4);
+  memcpy(&dst, ip + 16, 4);
+  ip[36] = ip[37] = 0;
+  c = (uint16_t)~orc_tcp_checksum(src, dst, tcplen, ip + 20);
+  memcpy(ip + 36, &c, 2);
+  return (uint8_t)(fl | ORC_FRAME_L4_CSUM_OK);
+}
+
+void orc_generate_frames(uint8_t* base, const uint64_t* offsets,
+                         const uint16_t* lengths, uint64_t n, uint8_t* flags)
+{
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint8_t fl = orc_generate_frame(base + offsets[i], lengths[i]);
+    if (flags) {
+      flags[i] = fl;
+    }
+  }
+}
+
+/* ---------------------------------------------------------------------------
+ * §8f #4 — segmentation offload (the NIC's side of IBV_WR_TSO,
+ * src/transport/ofed/Device.cpp:688-772; header length as
+ * stack::utils::headerLength, src/stack/Utils.cpp:67-84). Standard LSO
+ * fixups (PARITY UNPINNED: the reference has no software TSO) followed by
+ * orc_generate_frame, which is pinned to the reference's generation.
+ * ------------------------------------------------------------------------- */
+static uint32_t orc_seg_count(const uint8_t* f, uint32_t len, uint32_t mss,
+                              int* seg_ok, uint32_t* hlen, uint32_t* payload)
+{
+  *seg_ok = 0;
+  *hlen = 0;
+  *payload = 0;
+  const uint8_t fl = orc_validate_frame(f, len);
+  if (!(fl & ORC_FRAME_TCP) || (fl & ORC_FRAME_TRUNCATED)) {
+    return 1;
+  }
+  const uint32_t doff = len > 46 ? (uint32_t)(f[46] >> 4) : 0u;
+  const uint32_t total = (uint32_t)(f[16] << 8 | f[17]);
+  if (doff < 5 || 20u + 4u * doff > total) {
+    return 1;
+  }
+  *seg_ok = 1;
+  *hlen = 34u + 4u * doff;
+  *payload = total - 20u - 4u * doff;
+  return *payload > mss ? (*payload + mss - 1) / mss : 1u;
+}
+
+/* first[] gets n + 1 entries; returns the total number of segments. */
+uint32_t orc_segment_count(const uint8_t* base, const uint64_t* offsets,
+                           const uint16_t* lengths, uint32_t n, uint32_t mss,
+                           uint32_t* first)
+{
+  uint32_t acc = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    int ok;
+    uint32_t h, p;
+    first[i] = acc;
+    acc += orc_seg_count(base + offsets[i], lengths[i], mss, &ok, &h, &p);
+  }
+  first[n] = acc;
+  return acc;
+}
+
+void orc_segment_frames(const uint8_t* base, const uint64_t* offsets,
+                        const uint16_t* lengths, uint32_t n, uint32_t mss,
+                        uint8_t* out, uint64_t stride, uint32_t capacity,
+                        uint16_t* out_lengths, const uint32_t* first)
+{
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* f = base + offsets[i];
+    const uint32_t len = lengths[i];
+    int ok;
+    uint32_t hlen, payload;
+    const uint32_t nseg = orc_seg_count(f, len, mss, &ok, &hlen, &payload);
+    for (uint32_t k = 0; k < nseg; ++k) {
+      const uint32_t j = first[i] + k;
+      if (j >= capacity) {
+        break;
+      }
+      uint8_t* d = out + (uint64_t)j * stride;
+      if (nseg == 1) {
+        if (len > stride) {
+          out_lengths[j] = 0;
+          continue;
+        }
+        memcpy(d, f, len);
+        orc_generate_frame(d, len);
+        out_lengths[j] = (uint16_t)len;
+        continue;
+      }
+      const uint32_t slice = payload - k * mss < mss ? payload - k * mss : mss;
+      const uint32_t dlen = hlen + slice;
+      if (dlen > stride) {
+        out_lengths[j] = 0;
+        continue;
+      }
+      memcpy(d, f, hlen);
+      memcpy(d + hlen, f + hlen + (uint64_t)k * mss, slice);
+      const uint32_t total = dlen - 14u;
+      d[16] = (uint8_t)(total >> 8);
+      d[17] = (uint8_t)total;
+      const uint32_t id = ((uint32_t)(f[18] << 8 | f[19]) + k) & 0xffffu;
+      d[18] = (uint8_t)(id >> 8);
+      d[19] = (uint8_t)id;
+      const uint32_t seq = ((uint32_t)f[38] << 24 | (uint32_t)f[39] << 16 |
+                            (uint32_t)f[40] << 8 | f[41]) + k * mss;
+      d[38] = (uint8_t)(seq >> 24);
+      d[39] = (uint8_t)(seq >> 16);
+      d[40] = (uint8_t)(seq >> 8);
+      d[41] = (uint8_t)seq;
+      uint8_t tfl = f[47];
+      if (k + 1 < nseg) {
+        tfl &= (uint8_t)~(0x01 | 0x08); /* FIN, PSH on the last segment only */
+      }
+      if (k > 0) {
+        tfl &= (uint8_t)~0x80; /* CWR on the first segment only */
+      }
+      d[47] = tfl;
+      orc_generate_frame(d, dlen);
+      out_lengths[j] = (uint16_t)dlen;
+    }
+  }
+}

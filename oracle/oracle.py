@@ -166,6 +166,43 @@ class Oracle(_Batchable):
           _ptr(out, _u8p))
         return out
 
+    def generate_frames(self, arena, offsets, lengths):
+        """Checksum generation (oracle/csum_oracle.c orc_generate_frames) on a
+        copy of `arena`; returns (new arena, TULIPS_FRAME_* flags)."""
+        f = self.lib.orc_generate_frames
+        f.restype = None
+        f.argtypes = [_u8p, _u64p, _u16p, C.c_uint64, _u8p]
+        arena = np.array(arena, dtype=np.uint8, copy=True)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint16)
+        out = np.zeros(len(offsets), dtype=np.uint8)
+        f(_ptr(arena, _u8p), _ptr(offsets, _u64p), _ptr(lengths, _u16p), len(offsets),
+          _ptr(out, _u8p))
+        return arena, out
+
+    def segment_frames(self, arena, offsets, lengths, mss: int, stride: int):
+        """Segmentation offload (oracle/csum_oracle.c orc_segment_frames).
+        Returns (first[n+1], out bytes [total*stride], out_lengths[total])."""
+        L = self.lib
+        L.orc_segment_count.restype = C.c_uint32
+        L.orc_segment_count.argtypes = [_u8p, _u64p, _u16p, C.c_uint32, C.c_uint32, _u32p]
+        L.orc_segment_frames.restype = None
+        L.orc_segment_frames.argtypes = [_u8p, _u64p, _u16p, C.c_uint32, C.c_uint32, _u8p,
+                                         C.c_uint64, C.c_uint32, _u16p, _u32p]
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint16)
+        n = len(offsets)
+        first = np.zeros(n + 1, dtype=np.uint32)
+        total = L.orc_segment_count(_ptr(arena, _u8p), _ptr(offsets, _u64p),
+                                    _ptr(lengths, _u16p), n, mss, _ptr(first, _u32p))
+        out = np.zeros(max(total, 1) * stride, dtype=np.uint8)
+        out_lens = np.zeros(max(total, 1), dtype=np.uint16)
+        L.orc_segment_frames(_ptr(arena, _u8p), _ptr(offsets, _u64p), _ptr(lengths, _u16p),
+                             n, mss, _ptr(out, _u8p), stride, total, _ptr(out_lens, _u16p),
+                             _ptr(first, _u32p))
+        return first, out[:total * stride], out_lens[:total]
+
     def toeplitz(self, saddr: int, daddr: int, sport: int, dport: int, key: bytes,
                  init: int = 0) -> int:
         """src/stack/Utils.cpp:86-133 restated (oracle/csum_oracle.c)."""

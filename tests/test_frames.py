@@ -217,3 +217,80 @@ def test_gpu_host_context(oracle, pinned):
         got, cnt = ctx.validate_frames(src, fx["offsets"], fx["lengths"], with_counters=True)
     np.testing.assert_array_equal(got, exp)
     np.testing.assert_array_equal(cnt, counters_of(exp))
+
+
+# ------------------------------------------------- send-side generation -----
+def scramble_fields(fx, rng):
+    """The fixture arena with both checksum fields of every frame overwritten
+    by random bytes (generation must not depend on what they held)."""
+    arena = fx["arena"].copy()
+    for o, ln in zip(fx["offsets"].astype(np.int64), fx["lengths"].astype(np.int64)):
+        for fld in (24, 50):
+            if ln >= fld + 2:
+                arena[o + fld:o + fld + 2] = rng.integers(0, 256, 2, dtype=np.uint8)
+    return arena
+
+
+def test_oracle_generate_reproduces_reference_bytes(oracle):
+    """Frames the fixture built with the reference's own ipv4::checksum and
+    tcpv4 checksum (make_golden.py::_make_frame) are reproduced bit-exactly."""
+    fx = frames_fixture()
+    rng = np.random.default_rng(21)
+    gen, flags = oracle.generate_frames(scramble_fields(fx, rng), fx["offsets"], fx["lengths"])
+    good = np.nonzero(fx["expect"] == (IPV4 | IP_OK | TCP | L4_OK))[0]
+    assert len(good) > 500
+    for i in good:
+        o, ln = int(fx["offsets"][i]), int(fx["lengths"][i])
+        assert bytes(gen[o:o + ln]) == bytes(fx["arena"][o:o + ln]), i
+        assert flags[i] == (IPV4 | IP_OK | TCP | L4_OK)
+    # after generation every complete frame verifies
+    v = oracle.validate_frames(gen, fx["offsets"], fx["lengths"])
+    wrote_l4 = (flags & L4_OK) != 0
+    assert np.all((v[(flags & IPV4) != 0] & IP_OK) != 0)
+    assert np.all((v[wrote_l4] & L4_OK) != 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 1, 2, 3, 5, 8, 13, 15])
+def test_gpu_generate_matches_oracle(oracle, shift):
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(100 + shift)
+    src = np.concatenate([np.zeros(shift, np.uint8), scramble_fields(fx, rng)])
+    offs = fx["offsets"] + np.uint64(shift)
+    exp_arena, exp_flags = oracle.generate_frames(src, offs, fx["lengths"])
+    a, o, l = _dev(src, offs.astype(np.int64), fx["lengths"].view(np.int16))
+    fl = csum.generate_frames(a, o, l)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(fl.cpu().numpy(), exp_flags)
+    got = a.cpu().numpy()
+    assert np.array_equal(got, exp_arena), np.nonzero(got != exp_arena)[0][:10]
+
+
+@pytest.mark.gpu
+def test_gpu_generate_mutated_and_jumbo(oracle):
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(31)
+    arena = mutate(fx, rng, 3000)
+    exp_arena, exp_flags = oracle.generate_frames(arena, fx["offsets"], fx["lengths"])
+    a, o, l = _dev(arena, fx["offsets"].astype(np.int64), fx["lengths"].view(np.int16))
+    fl = csum.generate_frames(a, o, l)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(fl.cpu().numpy(), exp_flags)
+    assert np.array_equal(a.cpu().numpy(), exp_arena)
+    # jumbo / maximum frames, fields zeroed
+    fr = [bytearray(make_frame(oracle, rng, p)) for p in (8946, 32768, 65535 - 54, 0)]
+    want = [bytes(f) for f in fr]
+    for f in fr:
+        f[24:26] = b"\0\0"
+        f[50:52] = b"\0\0"
+    arena, offs, lens = pack([bytes(f) for f in fr], rng)
+    a, o, l = _dev(arena, offs.astype(np.int64), lens.view(np.int16))
+    csum.generate_frames(a, o, l, want_flags=False)
+    torch.cuda.synchronize()
+    got = a.cpu().numpy()
+    for i, w in enumerate(want):
+        assert bytes(got[int(offs[i]):int(offs[i]) + len(w)]) == w, i

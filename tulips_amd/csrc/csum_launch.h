@@ -32,6 +32,9 @@ hipError_t launch_var(const uint8_t* base, const uint64_t* offs,
                       const uint16_t* lens, const LaunchArgs& a,
                       hipStream_t stream);
 // frames.hip: per-frame TULIPS_FRAME_* flags (and optional counters[4]).
+hipError_t launch_generate(uint8_t* base, const uint64_t* offs,
+                           const uint16_t* lens, uint32_t n, uint8_t* flags,
+                           hipStream_t stream);
 hipError_t launch_frames(const uint8_t* base, const uint64_t* offs,
                          const uint16_t* lens, uint32_t n, uint8_t* flags,
                          uint32_t* counters, hipStream_t stream);

@@ -1,0 +1,195 @@
+// frame_common.h — device helpers shared by the frame kernels (frames.hip,
+// segment.hip): absolute-chunk sums, subgroup reductions, and the header
+// fields of an Ethernet/IPv4/TCP frame gathered by one subgroup.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tulips_csum.h"
+#include "csum_common.h"
+
+namespace tulips_amd {
+namespace frame {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4* gchunk_ptr;
+typedef const __attribute__((address_space(1))) uint8_t* gbyte_ptr;
+
+__device__ __forceinline__ uint64_t
+hsum(u32x4 v)
+{
+  return (uint64_t(v.x) + uint64_t(v.y)) + (uint64_t(v.z) + uint64_t(v.w));
+}
+
+__device__ __forceinline__ uint32_t
+byte_mask(int lo, int hi, int b)
+{
+  int ml = min(max(lo - b, 0), 4);
+  int mh = min(max(hi - b, 0), 4);
+  return uint32_t((1ull << (8 * mh)) - 1ull) & ~uint32_t((1ull << (8 * ml)) - 1ull);
+}
+
+__device__ __forceinline__ uint64_t
+masked_hsum(u32x4 v, int lo, int hi)
+{
+  return (uint64_t(v.x & byte_mask(lo, hi, 0)) +
+          uint64_t(v.y & byte_mask(lo, hi, 4))) +
+         (uint64_t(v.z & byte_mask(lo, hi, 8)) +
+          uint64_t(v.w & byte_mask(lo, hi, 12)));
+}
+
+// This lane's LE dword sum of [sa, sa+len) over absolute 16-byte chunks
+// (G lanes, U unconditional clamped loads per lane per batch).
+template<int G, int U, bool NT>
+__device__ __forceinline__ uint64_t
+lane_sum(uintptr_t sa, uint32_t len, int lane)
+{
+  if (len == 0) {
+    return 0;
+  }
+  const uintptr_t a0 = sa & ~uintptr_t(15);
+  const int nch = int((sa + len - a0 + 15) >> 4);
+  const int last = nch - 1;
+  const int head = int(sa - a0);
+  const int tail = int(sa + len - a0) - 16 * last;
+  const gchunk_ptr p = reinterpret_cast<gchunk_ptr>(a0);
+  uint64_t acc = 0;
+  for (int c = lane; c < nch; c += U * G) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cc = min(c + u * G, last);
+      v[u] = NT ? __builtin_nontemporal_load(p + cc) : p[cc];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cc = c + u * G;
+      acc += cc <= last ? hsum(v[u]) : 0;
+      if (u == 0 && cc == 0 && head != 0) {
+        acc -= masked_hsum(v[u], 0, head);
+      }
+      if (cc == last && tail != 16) {
+        acc -= masked_hsum(v[u], tail, 16);
+      }
+    }
+  }
+  return acc;
+}
+
+template<int G>
+__device__ __forceinline__ uint32_t
+sub_sum(uint32_t x)
+{
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) {
+    x += __shfl_xor(x, m, 64);
+  }
+  return x;
+}
+
+// The fields of an Ethernet/IPv4/TCP header the frame kernels act on.
+struct Header
+{
+  uint32_t type, vhl, total, frag0, frag1, proto, src, dst;
+  bool runt, ipv4, tcp, trunc;
+  uint32_t tcplen;
+  uint32_t ipck0, ipck1, tcpck0, tcpck1; // checksum field bytes (W >= 40)
+  uint32_t id, seq, doff, tflags;         // IP id, TCP seq/offset/flags (W >= 40)
+};
+
+// Parse from a byte accessor `byte(off)` (0 for bytes outside the frame);
+// `full` also reads the send-side fields (bytes up to 51).
+template<bool full, typename ByteAt>
+__device__ __forceinline__ Header
+parse_header(ByteAt byte, uint32_t flen)
+{
+  Header h;
+  h.type = (byte(12) << 8) | byte(13);
+  h.vhl = byte(14);
+  h.total = (byte(16) << 8) | byte(17);
+  h.frag0 = byte(20);
+  h.frag1 = byte(21);
+  h.proto = byte(23);
+  h.src = byte(26) | (byte(27) << 8) | (byte(28) << 16) | (byte(29) << 24);
+  h.dst = byte(30) | (byte(31) << 8) | (byte(32) << 16) | (byte(33) << 24);
+  if (full) {
+    h.ipck0 = byte(24);
+    h.ipck1 = byte(25);
+    h.tcpck0 = byte(50);
+    h.tcpck1 = byte(51);
+    h.id = (byte(18) << 8) | byte(19);
+    h.seq = (byte(38) << 24) | (byte(39) << 16) | (byte(40) << 8) | byte(41);
+    h.doff = byte(46) >> 4;
+    h.tflags = byte(47);
+  } else {
+    h.ipck0 = h.ipck1 = h.tcpck0 = h.tcpck1 = 0;
+    h.id = h.seq = h.doff = h.tflags = 0;
+  }
+  const bool eth_ip = flen >= 14 && h.type == 0x0800u;
+  h.runt = eth_ip && flen < 34;
+  h.ipv4 = eth_ip && !h.runt && h.vhl == 0x45u;
+  h.tcp = h.ipv4 && (h.frag0 & 0x3fu) == 0 && h.frag1 == 0 && h.proto == 6u;
+  h.tcplen = (h.total - 20u) & 0xffffu;
+  h.trunc = h.tcp && (h.total < 20u || 34u + h.tcplen > flen);
+  return h;
+}
+
+// One subgroup: lanes 0..W-1 each fetch one of frame bytes 12 .. 12+W-1
+// (only bytes inside the frame) and share them by cross-lane shuffles.
+template<int W>
+__device__ __forceinline__ Header
+gather_header(uintptr_t fa, uint32_t flen, int lane, int sub0)
+{
+  uint32_t hb = 0;
+  if (lane < W && uint32_t(12 + lane) < flen) {
+    hb = *reinterpret_cast<gbyte_ptr>(fa + 12 + lane);
+  }
+  return parse_header<(W >= 40)>(
+    [&](int off) { return __shfl(hb, sub0 + off - 12, 64); }, flen);
+}
+
+// One thread reads the header bytes itself.
+__device__ __forceinline__ Header
+load_header(uintptr_t fa, uint32_t flen)
+{
+  return parse_header<true>(
+    [&](int off) -> uint32_t {
+      return uint32_t(off) < flen ? uint32_t(*reinterpret_cast<gbyte_ptr>(fa + off))
+                                  : 0u;
+    },
+    flen);
+}
+
+__device__ __forceinline__ uint32_t
+frame_flags(const Header& h, bool ip_ok, bool l4_ok)
+{
+  if (h.runt) {
+    return TULIPS_FRAME_TRUNCATED;
+  }
+  if (!h.ipv4) {
+    return 0;
+  }
+  return TULIPS_FRAME_IPV4 | (ip_ok ? TULIPS_FRAME_IP_CSUM_OK : 0u) |
+         (h.tcp ? TULIPS_FRAME_TCP : 0u) | (h.trunc ? TULIPS_FRAME_TRUNCATED : 0u) |
+         (l4_ok ? TULIPS_FRAME_L4_CSUM_OK : 0u);
+}
+
+// Contribution of the 16-bit field {b0 @ a, b1 @ a+1} to an LE dword sum
+// taken at absolute addresses, modulo 65535 (2^16 == 1).
+__device__ __forceinline__ uint32_t
+field_contrib(uintptr_t a, uint32_t b0, uint32_t b1)
+{
+  return (a & 1) ? ((b0 << 8) | b1) : (b0 | (b1 << 8));
+}
+
+__device__ __forceinline__ void
+store_field(uintptr_t a, uint32_t v)
+{
+  typedef __attribute__((address_space(1))) uint8_t* gbyte_wptr;
+  reinterpret_cast<gbyte_wptr>(a)[0] = uint8_t(v & 0xff);
+  reinterpret_cast<gbyte_wptr>(a)[1] = uint8_t(v >> 8);
+}
+
+} // namespace frame
+} // namespace tulips_amd

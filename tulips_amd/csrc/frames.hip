@@ -17,94 +17,26 @@
 // the subgroup shares them by cross-lane shuffles, then the IPv4 header and
 // the TCP segment are summed with the same absolute-chunk machinery as the
 // checksum kernels (csum_kernels.hip) and finished per csum_common.h.
+//
+// The send side is here too: in-place generation of both
+// checksum fields for a burst of frames, as ipv4/Producer.cpp:79-82 and
+// tcpv4/Send.cpp:441-449 write them (the job of the NIC's IBV_SEND_IP_CSUM /
+// checksum offload in src/transport/ofed/Device.cpp:756).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/tulips_csum.h"
 #include "csum_common.h"
 #include "csum_launch.h"
+#include "frame_common.h"
 
 namespace tulips_amd {
 namespace {
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(1))) u32x4* gchunk_ptr;
-typedef const __attribute__((address_space(1))) uint8_t* gbyte_ptr;
+using namespace frame;
 
-__device__ __forceinline__ uint64_t
-hsum(u32x4 v)
-{
-  return (uint64_t(v.x) + uint64_t(v.y)) + (uint64_t(v.z) + uint64_t(v.w));
-}
-
-__device__ __forceinline__ uint32_t
-byte_mask(int lo, int hi, int b)
-{
-  int ml = min(max(lo - b, 0), 4);
-  int mh = min(max(hi - b, 0), 4);
-  return uint32_t((1ull << (8 * mh)) - 1ull) & ~uint32_t((1ull << (8 * ml)) - 1ull);
-}
-
-__device__ __forceinline__ uint64_t
-masked_hsum(u32x4 v, int lo, int hi)
-{
-  return (uint64_t(v.x & byte_mask(lo, hi, 0)) +
-          uint64_t(v.y & byte_mask(lo, hi, 4))) +
-         (uint64_t(v.z & byte_mask(lo, hi, 8)) +
-          uint64_t(v.w & byte_mask(lo, hi, 12)));
-}
-
-// This lane's LE dword sum of [sa, sa+len) over absolute 16-byte chunks
-// (G lanes, U unconditional clamped loads per lane per batch).
-template<int G, int U, bool NT>
-__device__ __forceinline__ uint64_t
-lane_sum(uintptr_t sa, uint32_t len, int lane)
-{
-  if (len == 0) {
-    return 0;
-  }
-  const uintptr_t a0 = sa & ~uintptr_t(15);
-  const int nch = int((sa + len - a0 + 15) >> 4);
-  const int last = nch - 1;
-  const int head = int(sa - a0);
-  const int tail = int(sa + len - a0) - 16 * last;
-  const gchunk_ptr p = reinterpret_cast<gchunk_ptr>(a0);
-  uint64_t acc = 0;
-  for (int c = lane; c < nch; c += U * G) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int cc = min(c + u * G, last);
-      v[u] = NT ? __builtin_nontemporal_load(p + cc) : p[cc];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int cc = c + u * G;
-      acc += cc <= last ? hsum(v[u]) : 0;
-      if (u == 0 && cc == 0 && head != 0) {
-        acc -= masked_hsum(v[u], 0, head);
-      }
-      if (cc == last && tail != 16) {
-        acc -= masked_hsum(v[u], tail, 16);
-      }
-    }
-  }
-  return acc;
-}
-
-template<int G>
-__device__ __forceinline__ uint32_t
-sub_sum(uint32_t x)
-{
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) {
-    x += __shfl_xor(x, m, 64);
-  }
-  return x;
-}
-
-constexpr int G = 32; // >= 24 header bytes, one per lane
-constexpr int U = 4;  // 128 chunks = a 1514 B frame in one batch per lane
+constexpr int VG = 32; // validate: >= 24 header bytes, one per lane
+constexpr int VU = 4;  // 128 chunks = a 1514 B frame in one batch per lane
 
 __global__ __launch_bounds__(256) void
 frame_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
@@ -112,63 +44,36 @@ frame_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ counters)
 {
   const int lane64 = threadIdx.x & 63;
-  const int lane = lane64 & (G - 1);
+  const int lane = lane64 & (VG - 1);
   const int sub0 = lane64 - lane; // first lane of this subgroup
-  const uint32_t per_block = blockDim.x / G;
+  const uint32_t per_block = blockDim.x / VG;
   const uint32_t nsub = gridDim.x * per_block;
-  for (uint32_t f = blockIdx.x * per_block + threadIdx.x / G; f < n; f += nsub) {
+  for (uint32_t f = blockIdx.x * per_block + threadIdx.x / VG; f < n; f += nsub) {
     const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + offs[f];
-    const uint32_t flen = lens[f];
-    // header bytes 12..35 (only bytes inside the frame are read)
-    uint32_t hb = 0;
-    if (lane < 24 && uint32_t(12 + lane) < flen) {
-      hb = *reinterpret_cast<gbyte_ptr>(fa + 12 + lane);
-    }
-    auto byte = [&](int off) { return __shfl(hb, sub0 + off - 12, 64); };
-    const uint32_t type = (byte(12) << 8) | byte(13);
-    const uint32_t vhl = byte(14);
-    const uint32_t total = (byte(16) << 8) | byte(17);
-    const uint32_t off0 = byte(20), off1 = byte(21);
-    const uint32_t proto = byte(23);
-    const uint32_t src = byte(26) | (byte(27) << 8) | (byte(28) << 16) | (byte(29) << 24);
-    const uint32_t dst = byte(30) | (byte(31) << 8) | (byte(32) << 16) | (byte(33) << 24);
-    const bool eth_ip = flen >= 14 && type == 0x0800u;
-    const bool runt = eth_ip && flen < 34;
-    const bool ipv4 = eth_ip && !runt && vhl == 0x45u;
-    const bool tcp = ipv4 && (off0 & 0x3fu) == 0 && off1 == 0 && proto == 6u;
-    const uint32_t tcplen = (total - 20u) & 0xffffu;
-    const bool trunc = tcp && (total < 20u || 34u + tcplen > flen);
-    const bool do_l4 = tcp && !trunc;
+    const Header h = gather_header<24>(fa, lens[f], lane, sub0);
+    const bool do_l4 = h.tcp && !h.trunc;
     // IPv4 header [14, 34) and TCP segment [34, 34 + tcplen)
     const uint32_t ip_part =
-      sub_sum<G>(fold64(lane_sum<G, 1, false>(fa + 14, ipv4 ? 20u : 0u, lane)));
+      sub_sum<VG>(fold64(lane_sum<VG, 1, false>(fa + 14, h.ipv4 ? 20u : 0u, lane)));
     const uint32_t l4_part =
-      sub_sum<G>(fold64(lane_sum<G, U, true>(fa + 34, do_l4 ? tcplen : 0u, lane)));
+      sub_sum<VG>(fold64(lane_sum<VG, VU, true>(fa + 34, do_l4 ? h.tcplen : 0u, lane)));
     if (lane == 0) {
       const bool ip_ok =
-        ipv4 && finish(ip_part, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20) == 0xffffu;
+        h.ipv4 && finish(ip_part, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20) == 0xffffu;
       const bool l4_ok =
-        do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0, src, dst,
-                        tcplen) == 0xffffu;
-      uint32_t fl = 0;
-      if (runt) {
-        fl = TULIPS_FRAME_TRUNCATED;
-      } else if (ipv4) {
-        fl = TULIPS_FRAME_IPV4 | (ip_ok ? TULIPS_FRAME_IP_CSUM_OK : 0u) |
-             (tcp ? TULIPS_FRAME_TCP : 0u) | (trunc ? TULIPS_FRAME_TRUNCATED : 0u) |
-             (l4_ok ? TULIPS_FRAME_L4_CSUM_OK : 0u);
-      }
+        do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst,
+                        h.tcplen) == 0xffffu;
       if (flags) {
-        flags[f] = uint8_t(fl);
+        flags[f] = uint8_t(frame_flags(h, ip_ok, l4_ok));
       }
       if (counters) {
-        if (ipv4) {
+        if (h.ipv4) {
           atomicAdd(counters + 0, 1u);
           if (!ip_ok) {
             atomicAdd(counters + 1, 1u);
           }
         }
-        if (tcp) {
+        if (h.tcp) {
           atomicAdd(counters + 2, 1u);
           if (!l4_ok) {
             atomicAdd(counters + 3, 1u);
@@ -177,6 +82,59 @@ frame_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
       }
     }
   }
+}
+
+// Checksum generation in place (the send side: ipv4/Producer.cpp:79-82
+// `ipchksum = ~checksum(header)`, tcpv4/Send.cpp:441-449 `chksum = ~csum`),
+// one wave per frame. Each field's current bytes are taken out of the sum
+// arithmetically (field_contrib) so the frame is read once and written 4 B.
+constexpr int GG = 64; // header window 12..51 covers both checksum fields
+constexpr int GU = 2;
+
+__global__ __launch_bounds__(256) void
+generate_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
+                const uint16_t* __restrict__ lens, uint32_t n,
+                uint8_t* __restrict__ flags)
+{
+  const int lane = threadIdx.x & 63;
+  const uint32_t per_block = blockDim.x / GG;
+  const uint32_t nsub = gridDim.x * per_block;
+  for (uint32_t f = blockIdx.x * per_block + threadIdx.x / GG; f < n; f += nsub) {
+    const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + offs[f];
+    const uint32_t flen = lens[f];
+    const Header h = gather_header<40>(fa, flen, lane, 0);
+    // the TCP checksum field (segment bytes 16..17) must lie in the frame
+    const bool do_l4 = h.tcp && !h.trunc && h.tcplen >= 18u;
+    const uint32_t ip_part =
+      sub_sum<GG>(fold64(lane_sum<GG, 1, false>(fa + 14, h.ipv4 ? 20u : 0u, lane)));
+    const uint32_t l4_part =
+      sub_sum<GG>(fold64(lane_sum<GG, GU, false>(fa + 34, do_l4 ? h.tcplen : 0u, lane)));
+    if (lane == 0) {
+      if (h.ipv4) {
+        const uint32_t p =
+          fold32(ip_part) + (0xffffu - field_contrib(fa + 24, h.ipck0, h.ipck1));
+        const uint32_t r = finish(p, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20);
+        store_field(fa + 24, ~r & 0xffffu);
+      }
+      if (do_l4) {
+        const uint32_t p =
+          fold32(l4_part) + (0xffffu - field_contrib(fa + 50, h.tcpck0, h.tcpck1));
+        const uint32_t r =
+          finish(p, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst, h.tcplen);
+        store_field(fa + 50, ~r & 0xffffu);
+      }
+      if (flags) {
+        flags[f] = uint8_t(frame_flags(h, h.ipv4, do_l4));
+      }
+    }
+  }
+}
+
+uint32_t
+grid_for(uint32_t n, uint32_t per_block)
+{
+  uint64_t blocks = (uint64_t(n) + per_block - 1) / per_block;
+  return uint32_t(blocks > 65535 ? 65535 : blocks);
 }
 
 } // namespace
@@ -188,14 +146,22 @@ launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
   if (n == 0) {
     return hipSuccess;
   }
-  const uint64_t per_block = 256 / G;
-  uint64_t blocks = (uint64_t(n) + per_block - 1) / per_block;
-  if (blocks > 65535) {
-    blocks = 65535;
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(frame_kernel, dim3(grid_for(n, 256 / VG)), dim3(256), 0,
+                     stream, base, offs, lens, n, flags, counters);
+  return hipGetLastError();
+}
+
+hipError_t
+launch_generate(uint8_t* base, const uint64_t* offs, const uint16_t* lens,
+                uint32_t n, uint8_t* flags, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
   }
   (void)hipGetLastError();
-  hipLaunchKernelGGL(frame_kernel, dim3(uint32_t(blocks)), dim3(256), 0, stream,
-                     base, offs, lens, n, flags, counters);
+  hipLaunchKernelGGL(generate_kernel, dim3(grid_for(n, 256 / GG)), dim3(256), 0,
+                     stream, base, offs, lens, n, flags);
   return hipGetLastError();
 }
 
@@ -221,5 +187,21 @@ tulips_csum_validate_frames(const uint8_t* base, const uint64_t* offsets,
   }
   const hipError_t e =
     tulips_amd::launch_frames(base, offsets, lengths, n, flags, counters, st);
+  return e == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
+}
+
+extern "C" int
+tulips_csum_generate_frames(uint8_t* base, const uint64_t* offsets,
+                            const uint16_t* lengths, uint32_t n, uint8_t* flags,
+                            void* stream)
+{
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  const hipError_t e = tulips_amd::launch_generate(
+    base, offsets, lengths, n, flags, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
 }

@@ -124,7 +124,10 @@ _SIGNATURES = {
     "tulips_csum_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(_vp)]),
     "tulips_csum_host_free": (C.c_int, [_vp]),
     "tulips_csum_validate_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
-    "tulips_csum_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
+    "tulips_csum_generate_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp]),
+    "tulips_csum_segment_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp,
+                                             C.c_uint64, C.c_uint32, _vp, _vp, _vp]),
+    "tulips_csum_validate_frames_host":(C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
                                                    _vp]),
 }
 
@@ -458,6 +461,60 @@ def validate_frames(arena, offsets, lengths, *, flags=None, counters=None,
                                            _stream(stream)),
            "tulips_csum_validate_frames")
     return flags
+
+
+def generate_frames(arena, offsets, lengths, *, flags=None, want_flags: bool = True,
+                    stream=None):
+    """Write the IPv4 and TCP checksum fields of frames in `arena` in place
+    (ipv4/Producer.cpp:79-82, tcpv4/Send.cpp:441-449). Returns the uint8
+    FRAME_* flags of what was written (None when want_flags is False)."""
+    import torch
+    n = int(offsets.numel())
+    if int(lengths.numel()) != n:
+        raise ValueError("offsets/lengths size mismatch")
+    _check_sizes(n, flags=flags)
+    if flags is None and want_flags:
+        flags = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    _check(lib.tulips_csum_generate_frames(_addr(arena), _addr(offsets), _addr(lengths), n,
+                                           _addr(flags), _stream(stream)),
+           "tulips_csum_generate_frames")
+    return flags
+
+
+def segment_frames(arena, offsets, lengths, mss: int, *, stride: int = 2048,
+                   out=None, out_lengths=None, capacity: int | None = None, stream=None):
+    """Segmentation offload of device-resident frames.
+
+    Returns (out, out_lengths, first): `first` (int32[n+1]) is the exclusive
+    prefix sum of the per-frame segment counts. Without `out` the function
+    sizes it itself (one synchronising read of first[n]); segment j occupies
+    out[j*stride:][:out_lengths[j]].
+    """
+    import torch
+    n = int(offsets.numel())
+    if int(lengths.numel()) != n:
+        raise ValueError("offsets/lengths size mismatch")
+    dev = arena.device
+    first = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    st = _stream(stream)
+    if out is None:
+        _check(lib.tulips_csum_segment_frames(_addr(arena), _addr(offsets), _addr(lengths), n,
+                                              mss, None, stride, 0, None, _addr(first), st),
+               "tulips_csum_segment_frames")
+        total = int(first[n].item())
+        out = torch.empty(max(total, 1) * stride, dtype=torch.uint8, device=dev)
+        capacity = total
+    elif capacity is None:
+        capacity = int(out.numel()) // stride
+    if out_lengths is None:
+        out_lengths = torch.zeros(max(capacity, 1), dtype=torch.int16, device=dev)
+    if int(out_lengths.numel()) < capacity or int(out.numel()) < capacity * stride:
+        raise ValueError("output smaller than its capacity")
+    _check(lib.tulips_csum_segment_frames(_addr(arena), _addr(offsets), _addr(lengths), n, mss,
+                                          _addr(out), stride, capacity, _addr(out_lengths),
+                                          _addr(first), st),
+           "tulips_csum_segment_frames")
+    return out, out_lengths, first
 
 
 def version() -> str:
