@@ -395,6 +395,129 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                          "parity": "ok" if fnv1a_u16(out) == gold.get("F1500", {}).get(
                              "fnv1a64") else "MISMATCH"}
     ex["e2e_host_F1500"] = e2e
+    ex.update(frame_extras(torch, csum, dev, timer))
+    return ex
+
+
+def rate_entry(alg_bytes, t, **kw):
+    gbs = alg_bytes / t / 1e9
+    d = {"GBps": round(gbs, 1), "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4),
+         "avg_launch_us": round(t * 1e6, 2), "bytes_per_launch": int(alg_bytes)}
+    d.update(kw)
+    return d
+
+
+def frame_extras(torch, csum, dev, timer):
+    """§8f rows: frame validation / generation (receive and send sides),
+    segmentation offload and the Toeplitz RSS batch, each on device-resident
+    synthetic frames with its own parity check."""
+    lib = csum.lib
+    ex = {}
+    # 8 bursts x 65,536 TCP frames of 1514 B (MTU 1500) in 2 KiB receive
+    # slots (the OFED RX layout, include/tulips/transport/ofed/Device.h:25),
+    # 1.07 GB in all so the rotation streams from HBM.
+    nf, slot, flen, nb = NSEG, 2048, SEG + 14, 8
+    ar = torch.empty(nb * nf * slot, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(ar, seed=0xF4A3E5)
+    v = ar.view(nb * nf, slot)
+    for off, val in ((12, 0x08), (13, 0), (14, 0x45), (15, 0), (16, SEG >> 8),
+                     (17, SEG & 0xFF), (20, 0x40), (21, 0), (23, 6), (46, 0x50)):
+        v[:, off] = val
+    offs = torch.arange(nf, dtype=torch.int64, device=dev) * slot
+    lens = torch.full((nf,), flen, dtype=torch.int16, device=dev)
+    flags = torch.empty(nb * nf, dtype=torch.uint8, device=dev)
+    burst = nf * slot
+    alg = nf * flen
+    gen, val = lib.tulips_csum_generate_frames, lib.tulips_csum_validate_frames
+
+    def fgen(i, st):
+        b = i % nb
+        gen(ar.data_ptr() + b * burst, offs.data_ptr(), lens.data_ptr(), nf, None, st)
+
+    def fval(i, st):
+        b = i % nb
+        val(ar.data_ptr() + b * burst, offs.data_ptr(), lens.data_ptr(), nf,
+            flags.data_ptr() + b * nf, None, st)
+    for i in range(nb):
+        fgen(i, torch.cuda.current_stream().cuda_stream)
+    t = timer(fgen, 64)
+    ex["frames_generate_F1514"] = rate_entry(
+        alg, t, kernel="generate_kernel (wave per frame)",
+        workload="65,536 x 1514 B TCP frames per launch, 2 KiB slots, 8 bursts rotated")
+    t = timer(fval, 64)
+    ok = bool((flags == 0x0F).all().item())
+    ex["frames_validate_F1514"] = rate_entry(
+        alg, t, kernel="frame_kernel (32-lane subgroup per frame)",
+        workload="same frames: generated checksums verified (flags == 0x0F)",
+        parity="ok" if ok else "MISMATCH")
+    del ar, v, flags
+
+    # Segmentation offload: 4 batches x 1024 super-frames of 64,294 B (44 x
+    # 1460 B payload) -> 45,056 segments of <= 1514 B in 1536 B slots.
+    nsf, pay, mss = 1024, 44 * 1460, 1460
+    sflen = 54 + pay
+    sslot = 65536
+    sb = 4
+    sa = torch.empty(sb * nsf * sslot, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(sa, seed=0x7505)
+    sv = sa.view(sb * nsf, sslot)
+    tot = sflen - 14
+    for off, val_ in ((12, 0x08), (13, 0), (14, 0x45), (15, 0), (16, tot >> 8),
+                      (17, tot & 0xFF), (20, 0x40), (21, 0), (23, 6), (46, 0x50)):
+        sv[:, off] = val_
+    soffs = torch.arange(nsf, dtype=torch.int64, device=dev) * sslot
+    slens = torch.full((nsf,), sflen - 65536 if sflen > 32767 else sflen,  # u16 bits
+                       dtype=torch.int16, device=dev)
+    nseg = nsf * (pay // mss)
+    ostride = 1536
+    sout = torch.empty(sb * nseg * ostride, dtype=torch.uint8, device=dev)
+    solen = torch.zeros(sb * nseg, dtype=torch.int16, device=dev)
+    sfirst = torch.empty(sb * (nsf + 1), dtype=torch.int32, device=dev)
+    seg = lib.tulips_csum_segment_frames
+
+    def fseg(i, st):
+        b = i % sb
+        seg(sa.data_ptr() + b * nsf * sslot, soffs.data_ptr(), slens.data_ptr(), nsf, mss,
+            sout.data_ptr() + b * nseg * ostride, ostride, nseg,
+            solen.data_ptr() + b * nseg * 2, sfirst.data_ptr() + b * (nsf + 1) * 4, st)
+    for i in range(sb):
+        fseg(i, torch.cuda.current_stream().cuda_stream)
+    t = timer(fseg, 32)
+    moved = nsf * sflen + nseg * (54 + mss)       # read super-frames + write segments
+    so = torch.arange(nseg, dtype=torch.int64, device=dev) * ostride
+    sfl = csum.validate_frames(sout[:nseg * ostride], so, solen[:nseg])
+    ok = bool((sfl == 0x0F).all().item()) and int(sfirst[nsf].item()) == nseg
+    ex["segment_TSO_64K_mss1460"] = rate_entry(
+        moved, t, kernel="seg_count + scan + segment_kernel (wave per super-frame)",
+        workload="1024 super-frames of 64,294 B -> 45,056 segments of 1514 B per call",
+        segments_per_s=round(nseg / t / 1e6, 2) * 1e6,
+        parity="ok" if ok else "MISMATCH")
+    del sa, sv, sout
+
+    # Toeplitz RSS over 16M tuples (12 B in, 4 B out per tuple)
+    nt = 1 << 24
+    g = torch.Generator(device="cpu").manual_seed(5)
+    tup = torch.randint(0, 2**31 - 1, (4, nt), generator=g, dtype=torch.int64)
+    sa_, da_ = tup[0].to(torch.int32).to(dev), tup[1].to(torch.int32).to(dev)
+    sp_, dp_ = tup[2].to(torch.int16).to(dev), tup[3].to(torch.int16).to(dev)
+    key = bytes(range(1, 41))
+    rout = torch.empty(nt, dtype=torch.int32, device=dev)
+    kb = (np.frombuffer(key, dtype=np.uint8)).copy()
+    kp = kb.ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_uint8))
+    rss = lib.tulips_rss_toeplitz_batch
+
+    def frss(i, st):
+        rss(sa_.data_ptr(), da_.data_ptr(), sp_.data_ptr(), dp_.data_ptr(), nt, kp, len(key),
+            0, rout.data_ptr(), st)
+    frss(0, torch.cuda.current_stream().cuda_stream)
+    t = timer(frss, 32)
+    j = nt // 3
+    exp = csum.toeplitz(int(sa_[j].item()) & 0xFFFFFFFF, int(da_[j].item()) & 0xFFFFFFFF,
+                        int(sp_[j].item()) & 0xFFFF, int(dp_[j].item()) & 0xFFFF, key, 0)
+    ok = (int(rout[j].item()) & 0xFFFFFFFF) == exp
+    ex["rss_toeplitz_16M"] = rate_entry(
+        nt * 16, t, kernel="rss_kernel (12x256 LDS tables)", Mtuples_per_s=round(nt / t / 1e6, 1),
+        parity="ok" if ok else "MISMATCH")
     return ex
 
 
