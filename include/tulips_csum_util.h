@@ -49,6 +49,17 @@ int tulips_csum_batch_tuned(const uint8_t* base, const uint64_t* offsets,
                             uint16_t* out, uint32_t n, uint32_t mode,
                             const tulips_csum_tuning* tuning, void* stream);
 
+/* Frame kernels (include/tulips_csum.h) with an explicit geometry: op 0 =
+ * tulips_csum_validate_frames, op 1 = tulips_csum_generate_frames (counters
+ * ignored). Uses tuning->group (lanes per frame, 0 = 16), unroll (chunks
+ * in flight per lane, 0 = 6; supported pairs 16x4, 16x6, 16x8, 8x8, 8x16,
+ * 32x4, 64x2), nontemporal (bit 0: nt loads, -1 = on), max_blocks and
+ * block; kind and sps are ignored. */
+int tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
+                             const uint16_t* lengths, uint32_t n,
+                             uint8_t* flags, uint32_t* counters,
+                             const tulips_csum_tuning* tuning, void* stream);
+
 /* Device fill with the SplitMix64 byte stream of SURVEY.md §8c: dst[i] =
  * stream byte (byte_off + i). Used to materialise synthetic arenas in HBM. */
 int tulips_csum_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,

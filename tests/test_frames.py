@@ -294,3 +294,48 @@ def test_gpu_generate_mutated_and_jumbo(oracle):
     got = a.cpu().numpy()
     for i, w in enumerate(want):
         assert bytes(got[int(offs[i]):int(offs[i]) + len(w)]) == w, i
+
+
+FRAME_GEOMETRIES = [(16, 4), (16, 6), (16, 8), (8, 8), (8, 16), (32, 4), (64, 2)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("geo", FRAME_GEOMETRIES)
+@pytest.mark.parametrize("nt", [1, 0])
+def test_gpu_every_frame_geometry(oracle, geo, nt):
+    """Validation and generation through tulips_csum_frames_tuned at every
+    geometry, on mutated fixture frames shifted to an odd base."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(geo[0] * 100 + geo[1] + nt)
+    arena = np.concatenate([np.zeros(5, np.uint8), mutate(fx, rng, 1500)])
+    offs = fx["offsets"] + np.uint64(5)
+    t = csum.Tuning(group=geo[0], unroll=geo[1], nontemporal=nt, block=256 if nt else 512)
+    a, o, l = _dev(arena, offs.astype(np.int64), fx["lengths"].view(np.int16))
+    fl = torch.empty(len(offs), dtype=torch.uint8, device="cuda:0")
+    cnt = torch.zeros(4, dtype=torch.int32, device="cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    ft = csum.lib.tulips_csum_frames_tuned
+    assert ft(0, a.data_ptr(), o.data_ptr(), l.data_ptr(), len(offs), fl.data_ptr(),
+              cnt.data_ptr(), t, st) == 0
+    torch.cuda.synchronize()
+    exp = oracle.validate_frames(arena, offs, fx["lengths"])
+    np.testing.assert_array_equal(fl.cpu().numpy(), exp)
+    np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32), counters_of(exp))
+    assert ft(1, a.data_ptr(), o.data_ptr(), l.data_ptr(), len(offs), fl.data_ptr(), None,
+              t, st) == 0
+    torch.cuda.synchronize()
+    exp_arena, exp_flags = oracle.generate_frames(arena, offs, fx["lengths"])
+    np.testing.assert_array_equal(fl.cpu().numpy(), exp_flags)
+    assert np.array_equal(a.cpu().numpy(), exp_arena)
+
+
+def test_frames_tuned_rejects_bad_geometry():
+    from tulips_amd import csum
+    f = csum.lib.tulips_csum_frames_tuned
+    A = 0x1000
+    assert f(0, A, A, A, 4, A, None, csum.Tuning(group=24, unroll=4), None) == 1
+    assert f(2, A, A, A, 4, A, None, csum.Tuning(group=16, unroll=4), None) == 1
+    assert f(0, A, A, A, 4, A, None, csum.Tuning(group=16, unroll=4, block=384), None) == 1
+    assert f(0, A, A, A, 0, None, None, csum.Tuning(group=16, unroll=6), None) == 0

@@ -31,13 +31,24 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,
 hipError_t launch_var(const uint8_t* base, const uint64_t* offs,
                       const uint16_t* lens, const LaunchArgs& a,
                       hipStream_t stream);
-// frames.hip: per-frame TULIPS_FRAME_* flags (and optional counters[4]).
+// frames.hip: per-frame TULIPS_FRAME_* flags (and optional counters[4]) /
+// in-place checksum generation. Zero fields = defaults.
+struct FrameLaunch
+{
+  int group = 0;           // lanes per frame: 16, 32, 64
+  int unroll = 0;          // chunks in flight per lane
+  uint32_t max_blocks = 0; // grid cap
+  uint32_t block = 0;      // threads per workgroup
+  int nontemporal = 1;     // nt chunk loads
+};
+bool frame_geometry_ok(int group, int unroll, uint32_t block);
 hipError_t launch_generate(uint8_t* base, const uint64_t* offs,
                            const uint16_t* lens, uint32_t n, uint8_t* flags,
-                           hipStream_t stream);
+                           hipStream_t stream, const FrameLaunch& fl = {});
 hipError_t launch_frames(const uint8_t* base, const uint64_t* offs,
                          const uint16_t* lens, uint32_t n, uint8_t* flags,
-                         uint32_t* counters, hipStream_t stream);
+                         uint32_t* counters, hipStream_t stream,
+                         const FrameLaunch& fl = {});
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                 uint64_t byte_off, hipStream_t stream);

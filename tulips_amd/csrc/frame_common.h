@@ -183,12 +183,119 @@ field_contrib(uintptr_t a, uint32_t b0, uint32_t b1)
   return (a & 1) ? ((b0 << 8) | b1) : (b0 | (b1 << 8));
 }
 
+// Store the 16-bit field v (LE bytes) at a, which may be odd.
 __device__ __forceinline__ void
 store_field(uintptr_t a, uint32_t v)
 {
   typedef __attribute__((address_space(1))) uint8_t* gbyte_wptr;
-  reinterpret_cast<gbyte_wptr>(a)[0] = uint8_t(v & 0xff);
-  reinterpret_cast<gbyte_wptr>(a)[1] = uint8_t(v >> 8);
+  typedef __attribute__((address_space(1))) uint16_t* gshort_wptr;
+  if ((a & 1) == 0) {
+    *reinterpret_cast<gshort_wptr>(a) = uint16_t(v);
+  } else {
+    reinterpret_cast<gbyte_wptr>(a)[0] = uint8_t(v & 0xff);
+    reinterpret_cast<gbyte_wptr>(a)[1] = uint8_t(v >> 8);
+  }
+}
+
+// ---- whole-frame loads -----------------------------------------------------
+//
+// A frame's aligned 16-byte chunks, loaded unconditionally as soon as its
+// offset and length are known: lane l of a G-lane subgroup holds chunks
+// l, l+G, ..., l+(U-1)G (clamped to the last chunk that holds frame bytes, so
+// no load ever touches a chunk without one). Header fields and both checksum
+// ranges are then taken from these registers: one memory round trip per
+// frame instead of one per dependent step (offsets -> header -> IP -> TCP).
+
+static __device__ u32x4 k_frame_zero_chunk; // what an empty frame "loads"
+
+template<int G, int U>
+struct FrameChunks
+{
+  u32x4 v[U];
+  uintptr_t a0; // 16-aligned address of chunk 0
+  int h0;       // frame start - a0
+  int last;     // last chunk holding frame bytes (-1: empty frame)
+};
+
+template<int G, int U, bool NT>
+__device__ __forceinline__ void
+load_frame(uintptr_t fa, uint32_t flen, int lane, FrameChunks<G, U>& fc)
+{
+  fc.a0 = fa & ~uintptr_t(15);
+  fc.h0 = int(fa - fc.a0);
+  fc.last = flen ? int((uint32_t(fc.h0) + flen - 1) >> 4) : -1;
+  const gchunk_ptr p =
+    flen ? reinterpret_cast<gchunk_ptr>(fc.a0)
+         : reinterpret_cast<gchunk_ptr>(reinterpret_cast<uintptr_t>(&k_frame_zero_chunk));
+  const int lim = max(fc.last, 0);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int cc = min(lane + u * G, lim);
+    fc.v[u] = NT ? __builtin_nontemporal_load(p + cc) : p[cc];
+  }
+}
+
+// Frame-aligned header dwords F[j] = frame bytes 4j .. 4j+3 for j = 3..12
+// (bytes 12..51), assembled from chunks 0..4 held by lanes 0..4 of the
+// subgroup. Bytes past the frame end are unspecified (callers bound them).
+__device__ __forceinline__ void
+header_words(const u32x4& v0, int h0, int sub0, uint32_t (&F)[13])
+{
+  uint32_t w[20];
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    w[4 * c + 0] = __shfl(v0.x, sub0 + c, 64);
+    w[4 * c + 1] = __shfl(v0.y, sub0 + c, 64);
+    w[4 * c + 2] = __shfl(v0.z, sub0 + c, 64);
+    w[4 * c + 3] = __shfl(v0.w, sub0 + c, 64);
+  }
+  const int s = h0 >> 2;
+  const uint32_t r = uint32_t(h0 & 3);
+#pragma unroll
+  for (int j = 3; j < 13; ++j) {
+    const uint32_t lo = s == 0 ? w[j] : s == 1 ? w[j + 1] : s == 2 ? w[j + 2] : w[j + 3];
+    const uint32_t hi =
+      s == 0 ? w[j + 1] : s == 1 ? w[j + 2] : s == 2 ? w[j + 3] : w[j + 4];
+    F[j] = __builtin_amdgcn_alignbyte(hi, lo, r);
+  }
+  F[0] = F[1] = F[2] = 0;
+}
+
+template<int G, int U>
+__device__ __forceinline__ Header
+frame_header(const FrameChunks<G, U>& fc, uint32_t flen, int sub0)
+{
+  uint32_t F[13];
+  header_words(fc.v[0], fc.h0, sub0, F);
+  return parse_header<true>(
+    [&](int k) -> uint32_t {
+      return uint32_t(k) < flen ? (F[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
+    },
+    flen);
+}
+
+// This lane's LE dword sum of the bytes at chunk-relative offsets [lo, hi)
+// (offsets from a0; the range must lie inside the frame). Bytes beyond the
+// G*U chunks held in registers are loaded by a trailing lane_sum (jumbo).
+template<int G, int U, bool NT>
+__device__ __forceinline__ uint64_t
+range_sum(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
+{
+  uint64_t acc = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int b = 16 * (lane + u * G);
+    const int l = max(lo - b, 0), h = min(hi - b, 16);
+    if (l < h) {
+      acc += (l == 0 && h == 16) ? hsum(fc.v[u]) : masked_hsum(fc.v[u], l, h);
+    }
+  }
+  constexpr int held = 16 * G * U;
+  if (hi > held) {
+    const int from = max(lo, held);
+    acc += lane_sum<G, U, NT>(fc.a0 + uintptr_t(from), uint32_t(hi - from), lane);
+  }
+  return acc;
 }
 
 } // namespace frame

@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include "../../include/tulips_csum.h"
+#include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
 #include "frame_common.h"
@@ -35,134 +36,186 @@ namespace {
 
 using namespace frame;
 
-constexpr int VG = 32; // validate: >= 24 header bytes, one per lane
-constexpr int VU = 4;  // 128 chunks = a 1514 B frame in one batch per lane
-
-__global__ __launch_bounds__(256) void
-frame_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
+// One G-lane subgroup per frame (two frames per wave), frames taken in
+// grid-stride order. The whole frame is loaded (load_frame) as soon as its
+// offset/length arrive, and the next frame's offset/length are fetched
+// behind those loads, so a frame costs one memory round trip. Header fields
+// come from the same registers (frame_header), and the IPv4-header and TCP
+// ranges are summed from them (range_sum).
+//
+// GENERATE = false: receive-side validation -> flags / counters.
+// GENERATE = true:  send-side generation (ipv4/Producer.cpp:79-82
+//   `ipchksum = ~checksum(header)`, tcpv4/Send.cpp:441-449 `chksum = ~csum`);
+//   each field's current bytes are taken out of the sum arithmetically
+//   (field_contrib), so the frame is read once and 4 bytes are written.
+// Geometry: FG lanes x FU chunks in flight per frame. The default, 16 x 6
+// (4 frames per wave, 96 chunks = a 1514 B frame in one batch, nt loads), is
+// the best of tools/probe_frames.py's sweep on 1514 B frames
+// (profiles/probe_frames_r01.json).
+template<bool GENERATE, int FG, int FU, bool NT>
+__global__ __launch_bounds__(1024) void
+frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ counters)
 {
   const int lane64 = threadIdx.x & 63;
-  const int lane = lane64 & (VG - 1);
+  const int lane = lane64 & (FG - 1);
   const int sub0 = lane64 - lane; // first lane of this subgroup
-  const uint32_t per_block = blockDim.x / VG;
+  const uint32_t per_block = blockDim.x / FG;
   const uint32_t nsub = gridDim.x * per_block;
-  for (uint32_t f = blockIdx.x * per_block + threadIdx.x / VG; f < n; f += nsub) {
-    const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + offs[f];
-    const Header h = gather_header<24>(fa, lens[f], lane, sub0);
-    const bool do_l4 = h.tcp && !h.trunc;
-    // IPv4 header [14, 34) and TCP segment [34, 34 + tcplen)
-    const uint32_t ip_part =
-      sub_sum<VG>(fold64(lane_sum<VG, 1, false>(fa + 14, h.ipv4 ? 20u : 0u, lane)));
-    const uint32_t l4_part =
-      sub_sum<VG>(fold64(lane_sum<VG, VU, true>(fa + 34, do_l4 ? h.tcplen : 0u, lane)));
+  uint32_t f = blockIdx.x * per_block + threadIdx.x / FG;
+  if (f >= n) {
+    return;
+  }
+  uint64_t o = offs[f];
+  uint32_t flen = lens[f];
+  while (true) {
+    const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + o;
+    FrameChunks<FG, FU> fc;
+    load_frame<FG, FU, NT>(fa, flen, lane, fc);
+    const uint32_t fn = f + nsub;
+    const uint32_t pf = min(fn, n - 1);
+    const uint64_t o_next = offs[pf];
+    const uint32_t l_next = lens[pf];
+
+    const Header h = frame_header(fc, flen, sub0);
+    const int h0 = fc.h0;
+    const bool do_l4 = h.tcp && !h.trunc && (!GENERATE || h.tcplen >= 18u);
+    const uint32_t ip_part = sub_sum<FG>(
+      fold64(h.ipv4 ? range_sum<FG, FU, NT>(fc, lane, h0 + 14, h0 + 34) : 0));
+    const uint32_t l4_part = sub_sum<FG>(fold64(
+      do_l4 ? range_sum<FG, FU, NT>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen))
+            : 0));
     if (lane == 0) {
-      const bool ip_ok =
-        h.ipv4 && finish(ip_part, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20) == 0xffffu;
-      const bool l4_ok =
-        do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst,
-                        h.tcplen) == 0xffffu;
-      if (flags) {
-        flags[f] = uint8_t(frame_flags(h, ip_ok, l4_ok));
-      }
-      if (counters) {
+      if (GENERATE) {
         if (h.ipv4) {
-          atomicAdd(counters + 0, 1u);
-          if (!ip_ok) {
-            atomicAdd(counters + 1, 1u);
-          }
+          const uint32_t p =
+            fold32(ip_part) + (0xffffu - field_contrib(fa + 24, h.ipck0, h.ipck1));
+          const uint32_t r = finish(p, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20);
+          store_field(fa + 24, ~r & 0xffffu);
         }
-        if (h.tcp) {
-          atomicAdd(counters + 2, 1u);
-          if (!l4_ok) {
-            atomicAdd(counters + 3, 1u);
+        if (do_l4) {
+          const uint32_t p =
+            fold32(l4_part) + (0xffffu - field_contrib(fa + 50, h.tcpck0, h.tcpck1));
+          const uint32_t r =
+            finish(p, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst, h.tcplen);
+          store_field(fa + 50, ~r & 0xffffu);
+        }
+        if (flags) {
+          flags[f] = uint8_t(frame_flags(h, h.ipv4, do_l4));
+        }
+      } else {
+        const bool ip_ok = h.ipv4 && finish(ip_part, ((fa + 14) & 1) != 0, MODE_INET, 0,
+                                            0, 0, 20) == 0xffffu;
+        const bool l4_ok = do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0,
+                                           h.src, h.dst, h.tcplen) == 0xffffu;
+        if (flags) {
+          flags[f] = uint8_t(frame_flags(h, ip_ok, l4_ok));
+        }
+        if (counters) {
+          if (h.ipv4) {
+            atomicAdd(counters + 0, 1u);
+            if (!ip_ok) {
+              atomicAdd(counters + 1, 1u);
+            }
+          }
+          if (h.tcp) {
+            atomicAdd(counters + 2, 1u);
+            if (!l4_ok) {
+              atomicAdd(counters + 3, 1u);
+            }
           }
         }
       }
     }
-  }
-}
-
-// Checksum generation in place (the send side: ipv4/Producer.cpp:79-82
-// `ipchksum = ~checksum(header)`, tcpv4/Send.cpp:441-449 `chksum = ~csum`),
-// one wave per frame. Each field's current bytes are taken out of the sum
-// arithmetically (field_contrib) so the frame is read once and written 4 B.
-constexpr int GG = 64; // header window 12..51 covers both checksum fields
-constexpr int GU = 2;
-
-__global__ __launch_bounds__(256) void
-generate_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
-                const uint16_t* __restrict__ lens, uint32_t n,
-                uint8_t* __restrict__ flags)
-{
-  const int lane = threadIdx.x & 63;
-  const uint32_t per_block = blockDim.x / GG;
-  const uint32_t nsub = gridDim.x * per_block;
-  for (uint32_t f = blockIdx.x * per_block + threadIdx.x / GG; f < n; f += nsub) {
-    const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + offs[f];
-    const uint32_t flen = lens[f];
-    const Header h = gather_header<40>(fa, flen, lane, 0);
-    // the TCP checksum field (segment bytes 16..17) must lie in the frame
-    const bool do_l4 = h.tcp && !h.trunc && h.tcplen >= 18u;
-    const uint32_t ip_part =
-      sub_sum<GG>(fold64(lane_sum<GG, 1, false>(fa + 14, h.ipv4 ? 20u : 0u, lane)));
-    const uint32_t l4_part =
-      sub_sum<GG>(fold64(lane_sum<GG, GU, false>(fa + 34, do_l4 ? h.tcplen : 0u, lane)));
-    if (lane == 0) {
-      if (h.ipv4) {
-        const uint32_t p =
-          fold32(ip_part) + (0xffffu - field_contrib(fa + 24, h.ipck0, h.ipck1));
-        const uint32_t r = finish(p, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20);
-        store_field(fa + 24, ~r & 0xffffu);
-      }
-      if (do_l4) {
-        const uint32_t p =
-          fold32(l4_part) + (0xffffu - field_contrib(fa + 50, h.tcpck0, h.tcpck1));
-        const uint32_t r =
-          finish(p, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst, h.tcplen);
-        store_field(fa + 50, ~r & 0xffffu);
-      }
-      if (flags) {
-        flags[f] = uint8_t(frame_flags(h, h.ipv4, do_l4));
-      }
+    if (fn >= n) {
+      break;
     }
+    f = fn;
+    o = o_next;
+    flen = l_next;
   }
 }
 
-uint32_t
-grid_for(uint32_t n, uint32_t per_block)
+constexpr int DEFAULT_G = 16, DEFAULT_U = 6;
+
+template<bool GENERATE, int G, int U, bool NT>
+hipError_t
+launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
+           uint8_t* flags, uint32_t* counters, const FrameLaunch& fl,
+           hipStream_t stream)
 {
+  const uint32_t block = fl.block ? fl.block : 256;
+  const uint32_t per_block = block / G;
   uint64_t blocks = (uint64_t(n) + per_block - 1) / per_block;
-  return uint32_t(blocks > 65535 ? 65535 : blocks);
+  const uint64_t cap = fl.max_blocks ? fl.max_blocks : 65535;
+  if (blocks > cap) {
+    blocks = cap;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((frame_kernel<GENERATE, G, U, NT>), dim3(uint32_t(blocks)),
+                     dim3(block), 0, stream, base, offs, lens, n, flags, counters);
+  return hipGetLastError();
+}
+
+template<bool GENERATE>
+hipError_t
+dispatch(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
+         uint8_t* flags, uint32_t* counters, const FrameLaunch& fl,
+         hipStream_t stream)
+{
+  const int g = fl.group ? fl.group : DEFAULT_G, u = fl.unroll ? fl.unroll : DEFAULT_U;
+  const bool nt = fl.nontemporal != 0;
+#define TCS_F(G, U)                                                            \
+  if (g == G && u == U) {                                                      \
+    return nt ? launch_one<GENERATE, G, U, true>(base, offs, lens, n, flags,    \
+                                                 counters, fl, stream)         \
+              : launch_one<GENERATE, G, U, false>(base, offs, lens, n, flags,   \
+                                                  counters, fl, stream);       \
+  }
+  TCS_F(16, 4)
+  TCS_F(16, 6)
+  TCS_F(16, 8)
+  TCS_F(8, 8)
+  TCS_F(8, 16)
+  TCS_F(32, 4)
+  TCS_F(64, 2)
+#undef TCS_F
+  return hipErrorInvalidValue;
 }
 
 } // namespace
 
+bool
+frame_geometry_ok(int group, int unroll, uint32_t block)
+{
+  const int g = group ? group : DEFAULT_G, u = unroll ? unroll : DEFAULT_U;
+  const bool geo = (g == 16 && (u == 4 || u == 6 || u == 8)) ||
+                   (g == 8 && (u == 8 || u == 16)) || (g == 32 && u == 4) ||
+                   (g == 64 && u == 2);
+  return geo && (block == 0 || block == 256 || block == 512 || block == 1024);
+}
+
 hipError_t
 launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
-              uint32_t n, uint8_t* flags, uint32_t* counters, hipStream_t stream)
+              uint32_t n, uint8_t* flags, uint32_t* counters, hipStream_t stream,
+              const FrameLaunch& fl)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  (void)hipGetLastError();
-  hipLaunchKernelGGL(frame_kernel, dim3(grid_for(n, 256 / VG)), dim3(256), 0,
-                     stream, base, offs, lens, n, flags, counters);
-  return hipGetLastError();
+  return dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n, flags, counters,
+                         fl, stream);
 }
 
 hipError_t
 launch_generate(uint8_t* base, const uint64_t* offs, const uint16_t* lens,
-                uint32_t n, uint8_t* flags, hipStream_t stream)
+                uint32_t n, uint8_t* flags, hipStream_t stream, const FrameLaunch& fl)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  (void)hipGetLastError();
-  hipLaunchKernelGGL(generate_kernel, dim3(grid_for(n, 256 / GG)), dim3(256), 0,
-                     stream, base, offs, lens, n, flags);
-  return hipGetLastError();
+  return dispatch<true>(base, offs, lens, n, flags, nullptr, fl, stream);
 }
 
 } // namespace tulips_amd
@@ -203,5 +256,41 @@ tulips_csum_generate_frames(uint8_t* base, const uint64_t* offsets,
   }
   const hipError_t e = tulips_amd::launch_generate(
     base, offsets, lengths, n, flags, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
+}
+
+extern "C" int
+tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
+                         const uint16_t* lengths, uint32_t n, uint8_t* flags,
+                         uint32_t* counters, const tulips_csum_tuning* tuning,
+                         void* stream)
+{
+  if ((op != 0 && op != 1) || !tuning ||
+      !tulips_amd::frame_geometry_ok(tuning->group, tuning->unroll,
+                                     uint32_t(tuning->block < 0 ? 0 : tuning->block))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths || (op == 0 && !flags && !counters)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  tulips_amd::FrameLaunch fl;
+  fl.group = tuning->group;
+  fl.unroll = tuning->unroll;
+  fl.max_blocks = tuning->max_blocks;
+  fl.block = uint32_t(tuning->block < 0 ? 0 : tuning->block);
+  fl.nontemporal = tuning->nontemporal < 0 ? 1 : (tuning->nontemporal & 1);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  if (op == 0) {
+    if (counters && (e = hipMemsetAsync(counters, 0, 16, st)) != hipSuccess) {
+      return TULIPS_STATUS_HARDWARE_ERROR;
+    }
+    e = tulips_amd::launch_frames(base, offsets, lengths, n, flags, counters, st, fl);
+  } else {
+    e = tulips_amd::launch_generate(base, offsets, lengths, n, flags, st, fl);
+  }
   return e == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
 }

@@ -127,7 +127,9 @@ _SIGNATURES = {
     "tulips_csum_generate_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp]),
     "tulips_csum_segment_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp,
                                              C.c_uint64, C.c_uint32, _vp, _vp, _vp]),
-    "tulips_csum_validate_frames_host":(C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
+    "tulips_csum_frames_tuned": (C.c_int, [C.c_int, _vp, _vp, _vp, C.c_uint32, _vp, _vp,
+                                           C.POINTER(Tuning), _vp]),
+    "tulips_csum_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
                                                    _vp]),
 }
 
