@@ -149,14 +149,43 @@ gather_header(uintptr_t fa, uint32_t flen, int lane, int sub0)
     [&](int off) { return __shfl(hb, sub0 + off - 12, 64); }, flen);
 }
 
-// One thread reads the header bytes itself.
+// One thread reads the header itself: the five aligned chunks holding frame
+// bytes 0..79 (clamped to the frame's last chunk, so nothing outside a chunk
+// with frame bytes is touched), funnel-shifted to frame-aligned dwords.
+// Within a subgroup that parses the same frame these are broadcast loads.
+static __device__ u32x4 k_hdr_zero_chunk;
+
 __device__ __forceinline__ Header
 load_header(uintptr_t fa, uint32_t flen)
 {
+  const uintptr_t lo = fa & ~uintptr_t(15);
+  const uintptr_t hi = flen ? (fa + flen - 1) & ~uintptr_t(15) : lo;
+  uint32_t w[20];
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    uintptr_t q = lo + 16 * c;
+    q = q > hi ? hi : q;
+    const u32x4 v = *reinterpret_cast<gchunk_ptr>(
+      flen ? q : reinterpret_cast<uintptr_t>(&k_hdr_zero_chunk));
+    w[4 * c + 0] = v.x;
+    w[4 * c + 1] = v.y;
+    w[4 * c + 2] = v.z;
+    w[4 * c + 3] = v.w;
+  }
+  const int h0 = int(fa - lo), s = h0 >> 2;
+  const uint32_t r = uint32_t(h0 & 3);
+  uint32_t D[13];
+#pragma unroll
+  for (int j = 3; j < 13; ++j) {
+    const uint32_t l = s == 0 ? w[j] : s == 1 ? w[j + 1] : s == 2 ? w[j + 2] : w[j + 3];
+    const uint32_t h =
+      s == 0 ? w[j + 1] : s == 1 ? w[j + 2] : s == 2 ? w[j + 3] : w[j + 4];
+    D[j] = __builtin_amdgcn_alignbyte(h, l, r);
+  }
+  D[0] = D[1] = D[2] = 0;
   return parse_header<true>(
-    [&](int off) -> uint32_t {
-      return uint32_t(off) < flen ? uint32_t(*reinterpret_cast<gbyte_ptr>(fa + off))
-                                  : 0u;
+    [&](int k) -> uint32_t {
+      return uint32_t(k) < flen ? (D[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
     },
     flen);
 }
