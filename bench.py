@@ -57,6 +57,8 @@ def parse():
                    help="torch.distributed backend for N>1 (nccl = RCCL)")
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal only: every rank uses cuda:0 (use with gloo)")
+    p.add_argument("--streams", type=int, default=1,
+                   help="independent graph branches the timed steps round-robin over")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from Python instead of replaying a "
                         "captured HIP graph of one shard rotation (16 launches); "
@@ -195,12 +197,21 @@ def main():
     graph = None
     if not args.eager:
         graph = torch.cuda.CUDAGraph()
+        side = [torch.cuda.Stream() for _ in range(args.streams)]
         with torch.cuda.graph(graph):
-            gs = torch.cuda.current_stream().cuda_stream
+            main = torch.cuda.current_stream()
+            # Steps round-robin over `streams` independent branches of the
+            # graph (batches are independent), so step i+1's waves can fill
+            # the drain of step i; each step is still one launch over one
+            # whole batch. streams=1 is a single serial chain.
+            for sd in side:
+                sd.wait_stream(main)
             for i in range(args.steps):
                 b = i % NBATCH
                 fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
-                      optr + b * NSEG * 2, NSEG, 0, gs)
+                      optr + b * NSEG * 2, NSEG, 0, side[i % len(side)].cuda_stream)
+            for sd in side:
+                main.wait_stream(sd)
         graph.replay()
         torch.cuda.synchronize()
 
@@ -263,6 +274,7 @@ def main():
             "segment_bytes": SEG,
             "parallelism": f"shard{world}",
             "launch": "graph" if graph is not None else "eager",
+            "streams": args.streams if graph is not None else 1,
         },
         "parity": parity,
         "shard_digests": shard_digests,
