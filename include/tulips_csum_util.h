@@ -18,6 +18,10 @@ extern "C" {
                                        (8/16/32) for short segments, `sps`
                                        of them in flight per subgroup; whole
                                        wave for long ones */
+#define TULIPS_CSUM_KIND_PACKED 3   /* variable only: one wave per `group`
+                                       segments (8/16/32/64), their chunks
+                                       packed end to end, `unroll` 64-chunk
+                                       windows in flight (2/4/8) */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning

@@ -20,13 +20,16 @@ from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
 
-SUB, HYB = csum.KIND_SUBGROUP, csum.KIND_HYBRID
+SUB, HYB, PCK = csum.KIND_SUBGROUP, csum.KIND_HYBRID, csum.KIND_PACKED
 # (kind, group, unroll, nontemporal bits, sps)
 GEOMETRIES = [(SUB, g, u, nt, 0) for g in (16, 32, 64) for u in (2, 4, 8) for nt in (0, 1, 3)]
 # hybrid short/long variable-length kernel, with 1/2/4 short segments in flight
 GEOMETRIES += [(HYB, 8, 4, 1, 1), (HYB, 8, 4, 1, 2), (HYB, 8, 4, 0, 4), (HYB, 8, 8, 0, 1),
                (HYB, 16, 2, 0, 1), (HYB, 16, 2, 1, 2), (HYB, 16, 2, 1, 4),
                (HYB, 16, 4, 1, 1), (HYB, 16, 4, 3, 2), (HYB, 16, 8, 1, 1), (HYB, 32, 4, 0, 1)]
+# packed kernel: `group` segments per wave, `unroll` 64-chunk windows in flight
+PACKED = [(4, 4), (6, 4), (8, 2), (8, 4), (12, 4), (16, 2), (16, 4), (16, 8), (32, 4), (32, 8), (64, 4), (64, 8)]
+GEOMETRIES += [(PCK, s, u, nt, 0) for (s, u) in PACKED for nt in (0, 1)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -161,8 +164,10 @@ def test_zipf_digest(golden, oracle, name):
                   dst=d(np.full(n, ip4(10, 1, 0, 2), np.uint32)), mode=MODE_TCP)
     geoms = [None] + [(SUB, g, 1) for g in (16, 32, 64)] + [(HYB, g, 1) for g in (8, 16, 32)]
     geoms += [(HYB, 8, 2), (HYB, 8, 4), (HYB, 16, 2)]
+    geoms += [(PCK, s_, 1, u_) for (s_, u_) in PACKED]
     for geo in geoms:
-        t = None if geo is None else csum.Tuning(kind=geo[0], group=geo[1], unroll=4,
+        t = None if geo is None else csum.Tuning(kind=geo[0], group=geo[1],
+                                                 unroll=geo[3] if len(geo) > 3 else 4,
                                                  sps=geo[2])
         out = tulips_amd.batch(arena, d(offs), d(lens), tuning=t, **kw)
         assert fnv(oracle, out) == b["fnv1a64"], geo
@@ -204,6 +209,47 @@ def test_random_vs_oracle_all_alignments(oracle):
                            nthreads=8)
         got = tulips_amd.batch(da, do, dl, seeds=ds_, src=dsrc, dst=ddst, mode=mode)
         np.testing.assert_array_equal(u16(got), exp, err_msg=hex(mode))
+
+
+@pytest.mark.parametrize("geo", PACKED)
+def test_packed_random_vs_oracle(oracle, geo):
+    """PACKED kernel: segments laid end to end in one chunk space per wave.
+    Lengths mix empty, 1..63 B, Zipf-like and up to 65,535 B; any alignment;
+    runs of empty segments at wave starts/ends; n not a multiple of the wave's
+    segment count; grid-stride (max_blocks) on and off."""
+    s_, u_ = geo
+    rng = np.random.default_rng(1000 + s_ * 10 + u_)
+    arena = rng.integers(0, 256, 2 << 20, dtype=np.uint8)
+    arena[:4096] = 0                       # all-zero segments (result 0 vs 0xffff)
+    arena[4096:8192] = 0xFF
+    n = 20000 + s_ - 3
+    lens = rng.integers(0, 3000, n).astype(np.uint16)
+    lens[rng.random(n) < 0.15] = 0
+    lens[:3 * s_] = 0                      # whole waves of empty segments
+    lens[rng.integers(0, n, 60)] = rng.integers(60000, 65536, 60)
+    lens[rng.integers(0, n, 300)] = rng.integers(1, 64, 300)
+    offs = np.array([rng.integers(0, len(arena) - int(L)) for L in lens], dtype=np.uint64)
+    zero_idx = rng.integers(0, n, 200)
+    lens[zero_idx] = np.minimum(lens[zero_idx], 2000)
+    offs[zero_idx] = rng.integers(0, 4096 - 2000, 200)
+    ff_idx = rng.integers(0, n, 200)
+    lens[ff_idx] = np.minimum(lens[ff_idx], 2000)
+    offs[ff_idx] = 4096 + rng.integers(0, 4096 - 2000, 200)
+    seeds = rng.integers(0, 65536, n, dtype=np.uint16)
+    seeds[zero_idx[:100]] = 0
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    da, do, dl = d(arena), d(offs), d(lens)
+    ds_, dsrc, ddst = d(seeds), d(src), d(dst)
+    for mode in (MODE_RAW, MODE_TCP | FLAG_COMPLEMENT):
+        exp = oracle.batch(arena, offs, lens, seeds=seeds, src=src, dst=dst, mode=mode,
+                           nthreads=8)
+        for max_blocks in (0, 5):
+            t = csum.Tuning(kind=PCK, group=s_, unroll=u_, nontemporal=1,
+                            max_blocks=max_blocks)
+            got = tulips_amd.batch(da, do, dl, seeds=ds_, src=dsrc, dst=ddst, mode=mode,
+                                   tuning=t)
+            np.testing.assert_array_equal(u16(got), exp, err_msg=f"{hex(mode)} {max_blocks}")
 
 
 @pytest.mark.parametrize("L", [0, 1, 2, 3, 15, 16, 17, 63, 64, 65, 1499, 1500, 1501, 8999,

@@ -22,4 +22,6 @@ step bench 600 python bench.py
 cat gpurun_out/bench.log | tail -1 > gpurun_out/bench_$TAG.json
 export TMPDIR=/tmp
 step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python bench.py --no-cpu-baseline --steps 320
+python tools/trace_bursts.py gpurun_out/prof_$TAG/run_kernel_trace.csv > gpurun_out/prof_$TAG/bursts_F1500.jsonl
+cat gpurun_out/prof_$TAG/bursts_F1500.jsonl
 echo "== done"

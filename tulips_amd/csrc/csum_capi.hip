@@ -165,6 +165,12 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
               (group == 16 && unroll == 4 && (spw == 1 || spw == 2)) ||
               (group == 16 && unroll == 8 && spw == 1) ||
               (group == 32 && unroll == 4 && spw == 1));
+    case TULIPS_CSUM_KIND_PACKED:
+      return variable && spw == 1 &&
+             (((group == 4 || group == 6 || group == 12) && unroll == 4) ||
+              ((group == 8) && (unroll == 2 || unroll == 4)) ||
+              ((group == 16) && (unroll == 2 || unroll == 4 || unroll == 8)) ||
+              ((group == 32 || group == 64) && (unroll == 4 || unroll == 8)));
     default:
       return false;
   }
@@ -183,8 +189,11 @@ default_tuning(uint32_t len, bool variable)
   t.block = 256;
   t.sps = 1;
   if (variable) {
-    t.kind = TULIPS_CSUM_KIND_HYBRID; // 16-lane subgroups, wave for > 1 KiB
-    t.group = 16;
+    // one wave per 8 segments, chunks packed end to end, 4 windows in
+    // flight (tools/probe_packed.py, profiles/probe_packed_r01.json: ZIPF
+    // 17.0 us vs 18.8 hybrid, 1500 B through offsets 19.9 vs 35.5)
+    t.kind = TULIPS_CSUM_KIND_PACKED;
+    t.group = 8;
     t.unroll = 4;
     return t;
   }

@@ -401,6 +401,225 @@ csum_hybrid_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
   }
 }
 
+// ---------------------------------------------------------------------------
+// PACKED variable-length kernel: one wave per S consecutive segments, whose
+// chunk lists are laid end to end in one "packed chunk space" of T chunks
+// (segment k owns packed chunks [P_k, P_k + nch_k), P = exclusive prefix of
+// nch over the wave's lanes). The wave walks that space in 64-chunk windows:
+// lane j of window b reads packed chunk b + j, so every lane of every load
+// instruction carries a useful chunk whatever the length mix (a 64 B and a
+// 9 KB segment cost 5 and 563 lane-loads), U windows are in flight per lane,
+// and no segment ever waits on another's round trip.
+//
+//   * window -> address: a scalar cursor walks the wave's non-empty segments
+//     (s_ff1 over a ballot). The window starts with the segment holding its
+//     first chunk; each segment starting inside it hands its lanes
+//     D_k = chunkbase_k - 16*P_k with one compare + 2 selects, and a lane's
+//     address is D + 16*(b + j). Uniform across lanes except at segment
+//     starts (about 1.5 per window for Zipf lengths).
+//   * per-chunk value: sum of the 8 little-endian 16-bit halves (4 x
+//     v_dot2_u32_u16 against (1,1)) — congruent to the LE dword sum mod
+//     65535, linear in the bytes, zero iff the bytes are zero, <= 0x7fff8.
+//   * per-segment sum without a segmented reduction: an inclusive wave scan
+//     of the values (u32, wrapping) gives a running prefix R over the packed
+//     space; a segment's sum is R(its last chunk) - R(previous segment's last
+//     chunk), exact because one segment's true sum is < 2^31 (4097 chunks).
+//     A second scalar cursor picks those R values out with v_readlane and
+//     parks each sum in its segment's lane with a lane-select.
+//   * boundary bytes: the bulk adds whole chunks; the bytes of the first and
+//     last chunk outside the segment are subtracted at the end from two
+//     chunk loads the segment's own lane issued with its metadata.
+// The result matches the other kernels' partial (finish(), csum_common.h).
+// ---------------------------------------------------------------------------
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Sum of the eight little-endian 16-bit halves of a chunk.
+__device__ __forceinline__ uint32_t
+half_sum(uint32_t x, uint32_t acc)
+{
+  const u16x2 one = {1, 1};
+  // (through a scalar + memcpy: __builtin_bit_cast applied directly to an
+  // ext_vector element compiled to element .x for every element here)
+  u16x2 h;
+  __builtin_memcpy(&h, &x, sizeof(h));
+  return __builtin_amdgcn_udot2(h, one, acc, false);
+}
+
+__device__ __forceinline__ uint32_t
+chunk_value(u32x4 v)
+{
+  const uint32_t x = v.x, y = v.y, z = v.z, w = v.w;
+  return half_sum(w, half_sum(z, half_sum(y, half_sum(x, 0u))));
+}
+
+// The same for the bytes [lo, hi) of a chunk only.
+__device__ __forceinline__ uint32_t
+masked_value(u32x4 v, int lo, int hi)
+{
+  u32x4 m;
+  m.x = v.x & byte_mask(lo, hi, 0);
+  m.y = v.y & byte_mask(lo, hi, 4);
+  m.z = v.z & byte_mask(lo, hi, 8);
+  m.w = v.w & byte_mask(lo, hi, 12);
+  return chunk_value(m);
+}
+
+// Inclusive u32 add-scan over the 64 lanes of a wave: DPP row shifts inside
+// each row of 16 lanes, then the row totals from lanes 15/31/47.
+__device__ __forceinline__ uint32_t
+wave_incl_scan(uint32_t x)
+{
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xf, 0xf, false));
+  const int lane = threadIdx.x & 63;
+  const uint32_t r0 = __builtin_amdgcn_readlane(x, 15);
+  const uint32_t r1 = __builtin_amdgcn_readlane(x, 31);
+  const uint32_t r2 = __builtin_amdgcn_readlane(x, 47);
+  x += lane >= 16 ? r0 : 0u;
+  x += lane >= 32 ? r1 : 0u;
+  x += lane >= 48 ? r2 : 0u;
+  return x;
+}
+
+__device__ __forceinline__ uint64_t
+readlane64(uint64_t v, uint32_t k)
+{
+  const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(v), k);
+  const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(v >> 32), k);
+  return (uint64_t(hi) << 32) | lo;
+}
+
+template<int S, int U, bool NT>
+__global__ __launch_bounds__(1024) void
+csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
+                   const uint32_t* __restrict__ src,
+                   const uint32_t* __restrict__ dst, uint16_t* __restrict__ out,
+                   uint32_t* __restrict__ bad, uint32_t n, uint32_t mode,
+                   bool nt_store)
+{
+  static_assert(S >= 1 && S <= 64, "one segment per lane at most");
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
+  const uintptr_t zero_chunk = reinterpret_cast<uintptr_t>(k_zero_chunk);
+#ifdef TULIPS_CSUM_STAMPS
+  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  for (uint32_t g0 = wave * S; g0 < n; g0 += nwaves * S) {
+    // ---- metadata: lane k < S owns segment g0 + k (coalesced loads) ------
+    const uint32_t seg = g0 + lane;
+    const bool mine = lane < uint32_t(S) && seg < n;
+    const uint32_t sk = mine ? seg : n - 1;
+    const uint32_t len = mine ? segs.length(sk) : 0u;
+    const uintptr_t sa = base + segs.off(sk);
+    const SideIn side = load_side(sk, seeds, src, dst, mode);
+    const uintptr_t a0 = sa & ~uintptr_t(15);
+    const uint32_t nch = len ? uint32_t((sa + len - a0 + 15) >> 4) : 0u;
+    const int head = int(sa - a0);
+    const int tail = nch ? int(sa + len - a0) - 16 * int(nch - 1) : 16;
+    // boundary chunks, only where bytes must be taken out (else a zero chunk)
+    const gchunk_ptr pf = reinterpret_cast<gchunk_ptr>(
+      (nch && head != 0) ? a0 : zero_chunk);
+    const gchunk_ptr pl = reinterpret_cast<gchunk_ptr>(
+      (nch && tail != 16) ? a0 + 16 * uintptr_t(nch - 1) : zero_chunk);
+    const u32x4 cfirst = load_chunk<NT>(pf);
+    const u32x4 clast = load_chunk<NT>(pl);
+    // ---- packed chunk space ------------------------------------------------
+    const uint32_t incl = wave_incl_scan(nch);
+    const uint32_t P = incl - nch;                  // first packed chunk
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t Lst = incl - 1;                  // last packed chunk
+    const uint64_t D = uint64_t(a0) - 16ull * P;    // address = D + 16*c
+    const uint64_t nonempty = __ballot(nch != 0);
+    uint64_t pend_start = nonempty, pend_end = nonempty;
+    uint64_t dcur = uint64_t(zero_chunk);           // D of the open segment
+    uint32_t run = 0;                               // R carried across windows
+    uint32_t eprev = 0;                             // R at the previous end
+    uint32_t sum = 0;                               // segment sum (lane k)
+    for (uint32_t w0 = 0; w0 < T; w0 += 64u * U) {
+      // addresses of all U windows first, then the U loads back to back (a
+      // load followed by control flow gets a vmcnt drain from hipcc)
+      uint64_t addr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t b = w0 + 64u * u;
+        // the segment holding chunk b owns the window; segments starting in
+        // [b, b + 64) take over their lanes
+        uint64_t dl = dcur;
+        while (pend_start) {
+          const uint32_t k = uint32_t(__builtin_ctzll(pend_start));
+          const uint32_t pk = __builtin_amdgcn_readlane(P, k);
+          if (pk >= b + 64u) {
+            break;
+          }
+          pend_start &= pend_start - 1;
+          const uint64_t dk = readlane64(D, k);
+          dl = lane + b >= pk ? dk : dl;
+          dcur = dk;
+        }
+        const uint32_t c = min(b + lane, T - 1u);   // past T: re-read, dropped
+        addr[u] = dl + 16ull * c;
+      }
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(addr[u]));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t b = w0 + 64u * u;
+        const uint32_t val = b + lane < T ? chunk_value(v[u]) : 0u;
+        const uint32_t r = wave_incl_scan(val) + run;
+        // segments whose last chunk is in [b, b + 64): sum = R(end) - R(prev)
+        while (pend_end) {
+          const uint32_t k = uint32_t(__builtin_ctzll(pend_end));
+          const uint32_t lk = __builtin_amdgcn_readlane(Lst, k);
+          if (lk >= b + 64u) {
+            break;
+          }
+          pend_end &= pend_end - 1;
+          const uint32_t e = __builtin_amdgcn_readlane(r, lk - b);
+          sum = lane == k ? e - eprev : sum;
+          eprev = e;
+        }
+        run = __builtin_amdgcn_readlane(r, 63);
+      }
+    }
+    // ---- boundary bytes out, finish --------------------------------------
+    const uint32_t outside =
+      masked_value(cfirst, 0, head) + masked_value(clast, tail, 16);
+    if (mine) {
+      emit_with(seg, sum - outside, sa, len, side, out, bad, mode, nt_store);
+    }
+  }
+#ifdef TULIPS_CSUM_STAMPS
+  stamp_wave(stamp0);
+#endif
+}
+
+template<int S, int U, bool NT>
+hipError_t
+launch_packed(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
+{
+  const int block = a.block ? a.block : 256;
+  const uint64_t per_block = uint64_t(block / 64) * S;
+  uint64_t blocks = (uint64_t(a.n) + per_block - 1) / per_block;
+  if (a.max_blocks && blocks > a.max_blocks) {
+    blocks = a.max_blocks;
+  }
+  if (blocks == 0) {
+    return hipSuccess;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_packed_kernel<S, U, NT>), dim3(uint32_t(blocks)),
+                     dim3(block), 0, stream, segs, a.seeds, a.src, a.dst, a.out,
+                     a.bad, a.n, a.mode, a.nt_store);
+  return hipGetLastError();
+}
+
 template<int GS, int US, int UL, int SPS, bool NT>
 hipError_t
 launch_hybrid(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
@@ -500,6 +719,28 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
            const LaunchArgs& a, hipStream_t stream)
 {
   const VarSegs segs{base, offs, lens};
+  if (a.kind == TULIPS_CSUM_KIND_PACKED) {
+    // group = segments per wave, unroll = 64-chunk windows in flight
+#define TCS_PCASE(S_, U_)                                                      \
+  if (a.group == S_ && a.unroll == U_) {                                       \
+    return a.nontemporal ? launch_packed<S_, U_, true>(segs, a, stream)        \
+                         : launch_packed<S_, U_, false>(segs, a, stream);      \
+  }
+    TCS_PCASE(4, 4)
+    TCS_PCASE(6, 4)
+    TCS_PCASE(8, 2)
+    TCS_PCASE(8, 4)
+    TCS_PCASE(12, 4)
+    TCS_PCASE(16, 2)
+    TCS_PCASE(16, 4)
+    TCS_PCASE(16, 8)
+    TCS_PCASE(32, 4)
+    TCS_PCASE(32, 8)
+    TCS_PCASE(64, 4)
+    TCS_PCASE(64, 8)
+#undef TCS_PCASE
+    return hipErrorInvalidValue;
+  }
   if (a.kind == TULIPS_CSUM_KIND_HYBRID) {
     // group = short subgroup lanes, unroll = short loads per lane,
     // spw = segments per short subgroup in flight; 8 loads/lane when long

@@ -58,7 +58,7 @@ def _check(rc: int, what: str) -> None:
     raise CsumError(rc, f"{what} [{detail}]" if detail else what)
 
 
-KIND_DEFAULT, KIND_SUBGROUP, KIND_HYBRID = 0, 1, 2
+KIND_DEFAULT, KIND_SUBGROUP, KIND_HYBRID, KIND_PACKED = 0, 1, 2, 3
 
 
 class Tuning(C.Structure):
@@ -66,8 +66,10 @@ class Tuning(C.Structure):
 
     kind SUBGROUP: `group` lanes (16/32/64) per segment; HYBRID (variable
     only): `group`-lane subgroups (8/16/32), `sps` short segments in flight
-    per subgroup, whole wave for long segments. A positive `group` with kind
-    left at DEFAULT means SUBGROUP.
+    per subgroup, whole wave for long segments; PACKED (variable only): one
+    wave per `group` segments (4..64), their chunks packed end to end,
+    `unroll` 64-chunk windows in flight. A positive `group` with kind left at
+    DEFAULT means SUBGROUP.
     """
     _fields_ = [("kind", C.c_int32), ("group", C.c_int32), ("unroll", C.c_int32),
                 ("nontemporal", C.c_int32), ("max_blocks", C.c_uint32),
