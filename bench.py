@@ -119,16 +119,23 @@ class Timer:
     def __init__(self, torch, stream, graph=True):
         self.torch, self.stream, self.graph = torch, stream, graph
 
-    def __call__(self, fn, reps):
+    def __call__(self, fn, reps, branches=1):
+        """branches > 1: launch i goes to graph branch i % branches (independent
+        launches overlap); the result is then time per launch of the pipeline."""
         t = self.torch
         a, b = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
         g = None
         if self.graph:
             g = t.cuda.CUDAGraph()
+            side = [t.cuda.Stream() for _ in range(branches)] if branches > 1 else []
             with t.cuda.graph(g):
-                cs = t.cuda.current_stream().cuda_stream
+                main = t.cuda.current_stream()
+                for sd in side:
+                    sd.wait_stream(main)
                 for i in range(reps):
-                    fn(i, cs)
+                    fn(i, side[i % branches].cuda_stream if side else main.cuda_stream)
+                for sd in side:
+                    main.wait_stream(sd)
             g.replay()                      # warm replay
         t.cuda.synchronize()
         a.record(self.stream)
@@ -147,8 +154,8 @@ def main():
     import torch
     import torch.distributed as dist
     from tulips_amd import csum
-    from tulips_amd.shard import (all_ranks_ok, gather_strings, max_over_ranks,
-                                  shard_for)
+    from tulips_amd.shard import (all_ranks_ok, gather_results, gather_strings,
+                                  max_over_ranks, shard_for)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -219,6 +226,16 @@ def main():
         graph.replay()
         torch.cuda.synchronize()
 
+    # the kernel alone, as one serial chain of the same launches (measured
+    # before the pipelined region: the figure rocprofv3 --stats averages)
+    serial_s = None
+    if graph is not None and args.streams > 1:
+        def serial(i, st):
+            b = i % NBATCH
+            fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
+                  optr + b * NSEG * 2, NSEG, 0, st)
+        serial_s = Timer(torch, stream)(serial, min(args.steps, 512))
+
     # ---- timed region ------------------------------------------------------
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -257,6 +274,26 @@ def main():
     parity = "ok" if all_ranks_ok(ok, dist, cdev) else "MISMATCH"
     shard_digests = gather_strings(digest, dist)
 
+    # exchange-inclusive figure (N>1, reported beside `value`): the K steps'
+    # results gathered to every rank — 16 batches x 65,536 x 2 B = 2 MiB per
+    # rank over RCCL — timed on its own and added to the compute time
+    exchange = None
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg0 = time.perf_counter()
+        gathered = gather_results(outs, dist, cdev)
+        torch.cuda.synchronize()
+        tg = max_over_ranks(time.perf_counter() - tg0, dist, cdev)
+        g_ok = all(fnv1a_u16(gathered[r * outs.numel():(r + 1) * outs.numel()]
+                             .cpu().numpy().view(np.uint16)) == shard_digests[r]
+                   for r in range(world)) if rank == 0 else True
+        exchange = {"op": "all_gather of the result words", "bytes_per_rank": outs.numel() * 2,
+                    "ms": round(tg * 1e3, 3),
+                    "value_exchange_inclusive": round(total_bytes / (t_max + tg) / GIB, 2),
+                    "parity": "ok" if g_ok else "MISMATCH"}
+        del gathered
+
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -282,6 +319,7 @@ def main():
         },
         "parity": parity,
         "shard_digests": shard_digests,
+        "exchange": exchange,
         "wall_s_timed": round(t_wall, 4),
     }
 
@@ -291,13 +329,7 @@ def main():
     # rocprofv3 --stats averages). With several graph branches the timed
     # region's per-launch time is shorter than any one dispatch (launches
     # overlap), so it is reported separately as "pipeline".
-    serial_s = per_launch_s
-    if graph is not None and args.streams > 1:
-        def serial(i, st):
-            b = i % NBATCH
-            fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
-                  optr + b * NSEG * 2, NSEG, 0, st)
-        serial_s = Timer(torch, stream)(serial, min(args.steps, 512))
+    serial_s = per_launch_s if serial_s is None else serial_s
     achieved = batch_bytes / serial_s / 1e9
     result["roofline"] = {
         "bound": "hbm",
@@ -328,6 +360,16 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+PIPE = 4   # graph branches for the "pipeline" figures (bench --streams default)
+
+
+def pipe_entry(nbytes, t):
+    """Rate of `PIPE` overlapped graph branches (seconds per launch t)."""
+    return {"branches": PIPE, "us_per_launch": round(t * 1e6, 2),
+            "GiBps": round(nbytes / t / GIB, 1),
+            "frac_of_peak": round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def read_traffic(workload):
@@ -369,12 +411,14 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     for i in range(4):
         f9(i, sh)
     t = timer(f9, 40)
+    tp = timer(f9, 40, branches=PIPE)
     gold = golden_digests()
     o = o9[:NSEG].cpu().numpy().view(np.uint16)
     tun = csum.default_tuning(L9)
     ex["F9000"] = {"GiBps": round(b9 / t / GIB, 1), "GBps": round(b9 / t / 1e9, 1),
                    "frac_of_peak": round(b9 / t / 1e9 / HBM_PEAK_GBS, 4),
                    "avg_launch_us": round(t * 1e6, 2),
+                   "pipeline": pipe_entry(b9, tp),
                    "geometry": f"G={tun.group},U={tun.unroll}",
                    "parity": "ok" if fnv1a_u16(o) == gold.get("F9000", {}).get("fnv1a64")
                    else "MISMATCH"}
@@ -401,10 +445,12 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     for i in range(nz):
         fz(i, sh)
     t = timer(fz, 80)
+    tp = timer(fz, 80, branches=PIPE)
     o = oz[:NSEG].cpu().numpy().view(np.uint16)
     ex["ZIPF"] = {"GiBps": round(zb / t / GIB, 1), "Mseg_per_s": round(NSEG / t / 1e6, 1),
                   "frac_of_peak": round(zb / t / 1e9 / HBM_PEAK_GBS, 4),
                   "avg_launch_us": round(t * 1e6, 2),
+                  "pipeline": pipe_entry(zb, tp),
                   "geometry": "packed: one wave per 8 segments, chunks packed end to end, "
                               "4 x 64-chunk windows in flight",
                   "parity": "ok" if fnv1a_u16(o) == gold.get("ZIPF", {}).get("fnv1a64")
@@ -476,15 +522,18 @@ def frame_extras(torch, csum, dev, timer):
     for i in range(nb):
         fgen(i, torch.cuda.current_stream().cuda_stream)
     t = timer(fgen, 64)
+    tp = timer(fgen, 64, branches=PIPE)
     ex["frames_generate_F1514"] = rate_entry(
-        alg, t, kernel="generate_kernel (wave per frame)",
-        workload="65,536 x 1514 B TCP frames per launch, 2 KiB slots, 8 bursts rotated")
+        alg, t, kernel="frame_kernel<GENERATE, 16 lanes x 6 chunks per frame>",
+        workload="65,536 x 1514 B TCP frames per launch, 2 KiB slots, 8 bursts rotated",
+        pipeline=pipe_entry(alg, tp))
     t = timer(fval, 64)
+    tp = timer(fval, 64, branches=PIPE)
     ok = bool((flags == 0x0F).all().item())
     ex["frames_validate_F1514"] = rate_entry(
-        alg, t, kernel="frame_kernel (32-lane subgroup per frame)",
+        alg, t, kernel="frame_kernel<VALIDATE, 16 lanes x 6 chunks per frame>",
         workload="same frames: generated checksums verified (flags == 0x0F)",
-        parity="ok" if ok else "MISMATCH")
+        pipeline=pipe_entry(alg, tp), parity="ok" if ok else "MISMATCH")
     del ar, v, flags
 
     # Segmentation offload: 4 batches x 1024 super-frames of 64,294 B (44 x
@@ -523,7 +572,8 @@ def frame_extras(torch, csum, dev, timer):
     sfl = csum.validate_frames(sout[:nseg * ostride], so, solen[:nseg])
     ok = bool((sfl == 0x0F).all().item()) and int(sfirst[nsf].item()) == nseg
     ex["segment_TSO_64K_mss1460"] = rate_entry(
-        moved, t, kernel="seg_count + scan + segment_kernel (wave per super-frame)",
+        moved, t, kernel="seg_prologue_small_kernel + segment_kernel<16,6> "
+                         "(16-lane subgroup per output segment)",
         workload="1024 super-frames of 64,294 B -> 45,056 segments of 1514 B per call",
         segments_per_s=round(nseg / t / 1e6, 2) * 1e6,
         parity="ok" if ok else "MISMATCH")
@@ -546,13 +596,17 @@ def frame_extras(torch, csum, dev, timer):
             0, rout.data_ptr(), st)
     frss(0, torch.cuda.current_stream().cuda_stream)
     t = timer(frss, 32)
-    j = nt // 3
-    exp = csum.toeplitz(int(sa_[j].item()) & 0xFFFFFFFF, int(da_[j].item()) & 0xFFFFFFFF,
-                        int(sp_[j].item()) & 0xFFFF, int(dp_[j].item()) & 0xFFFF, key, 0)
-    ok = (int(rout[j].item()) & 0xFFFFFFFF) == exp
+    tp = timer(frss, 32, branches=PIPE)
+    # parity: 2,048 tuples spread over the batch against the host symbol
+    js = torch.arange(0, nt, nt // 2048)
+    cols = [x.cpu().numpy() for x in (sa_[js], da_[js], sp_[js], dp_[js], rout[js])]
+    ok = all((int(cols[4][k]) & 0xFFFFFFFF) ==
+             csum.toeplitz(int(cols[0][k]) & 0xFFFFFFFF, int(cols[1][k]) & 0xFFFFFFFF,
+                           int(cols[2][k]) & 0xFFFF, int(cols[3][k]) & 0xFFFF, key, 0)
+             for k in range(len(js)))
     ex["rss_toeplitz_16M"] = rate_entry(
         nt * 16, t, kernel="rss_kernel (12x256 LDS tables)", Mtuples_per_s=round(nt / t / 1e6, 1),
-        parity="ok" if ok else "MISMATCH")
+        pipeline=pipe_entry(nt * 16, tp), parity="ok" if ok else "MISMATCH")
     return ex
 
 

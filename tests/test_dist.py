@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from tulips_amd.shard import (NBATCH, NSEG, SEG, SHARD_SEGMENTS, all_ranks_ok,
-                              gather_strings, max_over_ranks, shard_for)
+                              gather_results, gather_strings, max_over_ranks, shard_for)
 
 
 def _free_port():
@@ -44,8 +44,13 @@ def _worker(rank, world, port, q):
         ok_all = all_ranks_ok(digest == gold, dist)
         veto = all_ranks_ok(rank == 0, dist)   # rank 1 votes no
         digests = gather_strings(digest, dist)
+        import torch
+        words = torch.from_numpy(out.view(np.int16).copy()).view(torch.uint16)
+        allw = gather_results(words, dist, torch.device("cpu")).view(torch.int16).numpy()
+        gathered = [f"{orc.fnv1a_u16(allw[r * len(out):(r + 1) * len(out)].view(np.uint16)):016x}"
+                    for r in range(world)]
         q.put((rank, digest == gold, t, ok_all, veto, digests, sh.byte_offset,
-               sh.batch_offset(3)))
+               sh.batch_offset(3), gathered))
     finally:
         dist.destroy_process_group()
 
@@ -63,7 +68,8 @@ def test_two_rank_shards_match_reference_digests():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, ok, t, ok_all, veto, digests, boff, b3 in res:
+    for rank, ok, t, ok_all, veto, digests, boff, b3, gathered in res:
+        assert gathered == digests            # results all-gather, rank order
         assert ok, f"rank {rank} shard digest != reference M8 shard {rank}"
         assert t == 1.0                       # max over ranks of 0.5, 1.0
         assert ok_all and not veto

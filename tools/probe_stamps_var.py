@@ -42,7 +42,7 @@ def main():
     stamps = torch.zeros(4 * 300000, dtype=torch.int64, device=dev)
     sh = torch.cuda.current_stream().cuda_stream
     chunks = ((offs % 16) + lens + 15) // 16 * (lens > 0)
-    for s_, u_ in ((8, 4), (16, 4), (4, 4) if False else (8, 2)):
+    for s_, u_ in ((8, 4), (16, 4)):
         t = csum.Tuning(kind=csum.KIND_PACKED, group=s_, unroll=u_, nontemporal=1)
         for i in range(NB):
             lib.tulips_csum_batch_tuned(buf.data_ptr() + (i % NB) * nb, doffs.data_ptr(),
@@ -62,8 +62,14 @@ def main():
         wchunks = np.add.reduceat(chunks, np.arange(0, N, s_))[:n]
         order = np.argsort(wchunks)
         deciles = np.array_split(order, 10)
+        grid = np.arange(0, t1.max() + 0.01, 0.01)
+        alive = np.array([((t0 <= x) & (t1 > x)).sum() for x in grid])
         rep = {
             "geom": f"packed{s_}x{u_}", "waves": int(n), "span_us": round(float(t1.max()), 2),
+            "alive_max": int(alive.max()),
+            "started_by_us": [[x, int((t0 <= x).sum())] for x in (0.5, 1, 1.5, 2, 4, 6, 8, 10)],
+            "xcc_waves": np.bincount(st[:, 2].astype(np.int64) & 15, minlength=8).tolist(),
+            "cu_ids": int(len(np.unique(st[:, 3] >> 8))),
             "start_p50_p99_max": [round(float(np.percentile(t0, q)), 2) for q in (50, 99, 100)],
             "end_p50_p99_max": [round(float(np.percentile(t1, q)), 2) for q in (50, 99, 100)],
             "life_p10_p50_p90_p99_max": [round(float(np.percentile(life, q)), 2)

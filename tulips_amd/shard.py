@@ -67,3 +67,24 @@ def gather_strings(s: str, dist=None) -> list:
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, s)
     return out
+
+
+def gather_results(out, dist=None, device=None):
+    """All ranks' result words (uint16, same count per rank) at every rank, in
+    rank order: the one data-path exchange the sharded path could have
+    (an all-gather of the uint16 outputs, 2 MiB per GPU for
+    M8x1500). Under RCCL the bytes move GPU to GPU over xGMI; under gloo
+    (CPU rehearsal) through host memory. Returns a tensor on out.device."""
+    import torch
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return out.clone()
+    world = dist.get_world_size()
+    flat = out.contiguous().view(torch.uint8)      # RCCL has no 16-bit integer type
+    if device is not None and device.type == "cpu":
+        src = flat.cpu()
+        dst = torch.empty(world * src.numel(), dtype=torch.uint8)
+        dist.all_gather_into_tensor(dst, src)
+        return dst.to(out.device).view(out.dtype)
+    dst = torch.empty(world * flat.numel(), dtype=torch.uint8, device=flat.device)
+    dist.all_gather_into_tensor(dst, flat)
+    return dst.view(out.dtype)
