@@ -452,7 +452,8 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                   "avg_launch_us": round(t * 1e6, 2),
                   "pipeline": pipe_entry(zb, tp),
                   "geometry": "packed: one wave per 8 segments, chunks packed end to end, "
-                              "4 x 64-chunk windows in flight",
+                              "4 x 64-chunk windows in flight, double-buffered, "
+                              "1024-thread blocks",
                   "parity": "ok" if fnv1a_u16(o) == gold.get("ZIPF", {}).get("fnv1a64")
                   else "MISMATCH"}
     del az, oz

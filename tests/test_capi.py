@@ -165,7 +165,7 @@ def test_default_tuning():
     t = csum.default_tuning(1500)
     assert t.group in (16, 32, 64) and t.unroll in (2, 4, 8)
     t = csum.default_tuning(0, variable=True)
-    assert t.kind == csum.KIND_PACKED and t.group == 8 and t.unroll == 4
+    assert t.kind == csum.KIND_PACKED and t.group == 8 and t.unroll == 4 and t.sps == 2
     # hybrid and packed geometries are for variable-length batches only
     for kind in (csum.KIND_HYBRID, csum.KIND_PACKED):
         bad = csum.Tuning(kind=kind, group=16, unroll=4, nontemporal=1)
@@ -173,7 +173,7 @@ def test_default_tuning():
                                                       FAKE, 4, 0, C.byref(bad), None) == 1
     for kind, g, u, s in ((csum.KIND_HYBRID, 16, 3, 1), (csum.KIND_HYBRID, 16, 8, 2),
                           (csum.KIND_PACKED, 8, 8, 1), (csum.KIND_PACKED, 5, 4, 1),
-                          (csum.KIND_PACKED, 64, 2, 1), (csum.KIND_PACKED, 16, 4, 2),
+                          (csum.KIND_PACKED, 64, 2, 1), (csum.KIND_PACKED, 16, 4, 3),
                           (csum.KIND_HYBRID, 12, 4, 1), (csum.KIND_SUBGROUP, 8, 4, 0),
                           (csum.KIND_SUBGROUP, 16, 4, 2), (7, 16, 4, 0)):
         bad = csum.Tuning(kind=kind, group=g, unroll=u, nontemporal=1, sps=s)

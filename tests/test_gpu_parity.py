@@ -29,7 +29,9 @@ GEOMETRIES += [(HYB, 8, 4, 1, 1), (HYB, 8, 4, 1, 2), (HYB, 8, 4, 0, 4), (HYB, 8,
                (HYB, 16, 4, 1, 1), (HYB, 16, 4, 3, 2), (HYB, 16, 8, 1, 1), (HYB, 32, 4, 0, 1)]
 # packed kernel: `group` segments per wave, `unroll` 64-chunk windows in flight
 PACKED = [(4, 4), (6, 4), (8, 2), (8, 4), (12, 4), (16, 2), (16, 4), (16, 8), (32, 4), (32, 8), (64, 4), (64, 8)]
-GEOMETRIES += [(PCK, s, u, nt, 0) for (s, u) in PACKED for nt in (0, 1)]
+GEOMETRIES += [(PCK, s, u, nt, 1) for (s, u) in PACKED for nt in (0, 1)]
+# ... and with the double-buffered window loop (sps=2)
+GEOMETRIES += [(PCK, s, u, 1, 2) for (s, u) in PACKED]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -216,7 +218,8 @@ def test_packed_random_vs_oracle(oracle, geo):
     """PACKED kernel: segments laid end to end in one chunk space per wave.
     Lengths mix empty, 1..63 B, Zipf-like and up to 65,535 B; any alignment;
     runs of empty segments at wave starts/ends; n not a multiple of the wave's
-    segment count; grid-stride (max_blocks) on and off."""
+    segment count; grid-stride (max_blocks) on and off; single- and
+    double-buffered window loops (sps 1/2)."""
     s_, u_ = geo
     rng = np.random.default_rng(1000 + s_ * 10 + u_)
     arena = rng.integers(0, 256, 2 << 20, dtype=np.uint8)
@@ -244,12 +247,12 @@ def test_packed_random_vs_oracle(oracle, geo):
     for mode in (MODE_RAW, MODE_TCP | FLAG_COMPLEMENT):
         exp = oracle.batch(arena, offs, lens, seeds=seeds, src=src, dst=dst, mode=mode,
                            nthreads=8)
-        for max_blocks in (0, 5):
+        for max_blocks, sps in ((0, 1), (5, 1), (0, 2), (5, 2)):
             t = csum.Tuning(kind=PCK, group=s_, unroll=u_, nontemporal=1,
-                            max_blocks=max_blocks)
+                            max_blocks=max_blocks, sps=sps)
             got = tulips_amd.batch(da, do, dl, seeds=ds_, src=dsrc, dst=ddst, mode=mode,
                                    tuning=t)
-            np.testing.assert_array_equal(u16(got), exp, err_msg=f"{hex(mode)} {max_blocks}")
+            np.testing.assert_array_equal(u16(got), exp, err_msg=f"{hex(mode)} {max_blocks} {sps}")
 
 
 @pytest.mark.parametrize("L", [0, 1, 2, 3, 15, 16, 17, 63, 64, 65, 1499, 1500, 1501, 8999,

@@ -43,6 +43,14 @@ def main():
             continue
         geoms.append((key, csum.Tuning(kind=csum.KIND_PACKED, group=s, unroll=u,
                                        nontemporal=1, block=blk)))
+    # double-buffered window loop (sps=2)
+    for s, u, blk in ((4, 4, 256), (6, 4, 256), (8, 2, 256), (8, 4, 256),
+                      (8, 4, 1024), (16, 2, 256), (16, 4, 256), (32, 4, 256)):
+        key = f"packed{s}x{u}b{blk}pf"
+        if only and key not in only.split(","):
+            continue
+        geoms.append((key, csum.Tuning(kind=csum.KIND_PACKED, group=s, unroll=u,
+                                       nontemporal=1, block=blk, sps=2)))
     out = torch.empty(NB * N, dtype=torch.uint16, device=dev)
     for name, lens in shapes.items():
         offs = np.zeros(N, np.uint64)

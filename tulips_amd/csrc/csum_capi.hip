@@ -166,7 +166,7 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
               (group == 16 && unroll == 8 && spw == 1) ||
               (group == 32 && unroll == 4 && spw == 1));
     case TULIPS_CSUM_KIND_PACKED:
-      return variable && spw == 1 &&
+      return variable && (spw == 1 || spw == 2) &&
              (((group == 4 || group == 6 || group == 12) && unroll == 4) ||
               ((group == 8) && (unroll == 2 || unroll == 4)) ||
               ((group == 16) && (unroll == 2 || unroll == 4 || unroll == 8)) ||
@@ -190,11 +190,14 @@ default_tuning(uint32_t len, bool variable)
   t.sps = 1;
   if (variable) {
     // one wave per 8 segments, chunks packed end to end, 4 windows in
-    // flight (tools/probe_packed.py, profiles/probe_packed_r01.json: ZIPF
-    // 17.0 us vs 18.8 hybrid, 1500 B through offsets 19.9 vs 35.5)
+    // flight, double-buffered, 1024-thread blocks (tools/probe_packed.py,
+    // profiles/probe_packed_r01.json: ZIPF 14.1 us vs 16.8 single-buffered
+    // and 18.7 hybrid; 1500 B through offsets 19.3 vs 34.2 hybrid)
     t.kind = TULIPS_CSUM_KIND_PACKED;
     t.group = 8;
     t.unroll = 4;
+    t.sps = 2;
+    t.block = 1024;
     return t;
   }
   const uint32_t nch = len / 16 + 2;

@@ -491,7 +491,7 @@ readlane64(uint64_t v, uint32_t k)
   return (uint64_t(hi) << 32) | lo;
 }
 
-template<int S, int U, bool NT>
+template<int S, int U, bool NT, bool PF>
 __global__ __launch_bounds__(1024) void
 csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
                    const uint32_t* __restrict__ src,
@@ -539,9 +539,10 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
     uint32_t run = 0;                               // R carried across windows
     uint32_t eprev = 0;                             // R at the previous end
     uint32_t sum = 0;                               // segment sum (lane k)
-    for (uint32_t w0 = 0; w0 < T; w0 += 64u * U) {
-      // addresses of all U windows first, then the U loads back to back (a
-      // load followed by control flow gets a vmcnt drain from hipcc)
+    // U windows starting at chunk w0: all U addresses first, then the U loads
+    // back to back (a load followed by control flow gets a vmcnt drain from
+    // hipcc)
+    auto issue = [&](uint32_t w0, u32x4 (&v)[U]) {
       uint64_t addr[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -563,11 +564,12 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
         const uint32_t c = min(b + lane, T - 1u);   // past T: re-read, dropped
         addr[u] = dl + 16ull * c;
       }
-      u32x4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         v[u] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(addr[u]));
       }
+    };
+    auto consume = [&](uint32_t w0, const u32x4 (&v)[U]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t b = w0 + 64u * u;
@@ -587,6 +589,34 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
         }
         run = __builtin_amdgcn_readlane(r, 63);
       }
+    };
+    if constexpr (!PF) {
+      for (uint32_t w0 = 0; w0 < T; w0 += 64u * U) {
+        u32x4 v[U];
+        issue(w0, v);
+        consume(w0, v);
+      }
+    } else if (T != 0) {
+      // double-buffered: the next U windows are in flight while this batch is
+      // scanned, so a wave with a long chunk list (a 9 KB segment among its
+      // S) pays about half the round trips. The loop condition is
+      // wave-uniform and both edges into its header carry exactly the U loads
+      // of `cur`, so hipcc's vmcnt bookkeeping stays exact (vmcnt(U) before
+      // scanning `cur`, no drain); the last batch is scanned after the loop
+      // with nothing newer in flight.
+      u32x4 cur[U];
+      issue(0, cur);
+      uint32_t w0 = 0;
+      for (; w0 + 64u * U < T; w0 += 64u * U) {
+        u32x4 nxt[U];
+        issue(w0 + 64u * U, nxt);
+        consume(w0, cur);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cur[u] = nxt[u];
+        }
+      }
+      consume(w0, cur);
     }
     // ---- boundary bytes out, finish --------------------------------------
     const uint32_t outside =
@@ -600,7 +630,7 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
 #endif
 }
 
-template<int S, int U, bool NT>
+template<int S, int U, bool NT, bool PF>
 hipError_t
 launch_packed(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
 {
@@ -614,7 +644,7 @@ launch_packed(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
     return hipSuccess;
   }
   (void)hipGetLastError();
-  hipLaunchKernelGGL((csum_packed_kernel<S, U, NT>), dim3(uint32_t(blocks)),
+  hipLaunchKernelGGL((csum_packed_kernel<S, U, NT, PF>), dim3(uint32_t(blocks)),
                      dim3(block), 0, stream, segs, a.seeds, a.src, a.dst, a.out,
                      a.bad, a.n, a.mode, a.nt_store);
   return hipGetLastError();
@@ -720,11 +750,16 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
 {
   const VarSegs segs{base, offs, lens};
   if (a.kind == TULIPS_CSUM_KIND_PACKED) {
-    // group = segments per wave, unroll = 64-chunk windows in flight
+    // group = segments per wave, unroll = 64-chunk windows in flight,
+    // spw = 2: double-buffered (next windows in flight while scanning)
 #define TCS_PCASE(S_, U_)                                                      \
   if (a.group == S_ && a.unroll == U_) {                                       \
-    return a.nontemporal ? launch_packed<S_, U_, true>(segs, a, stream)        \
-                         : launch_packed<S_, U_, false>(segs, a, stream);      \
+    if (a.spw == 2) {                                                          \
+      return a.nontemporal ? launch_packed<S_, U_, true, true>(segs, a, stream) \
+                           : launch_packed<S_, U_, false, true>(segs, a, stream); \
+    }                                                                          \
+    return a.nontemporal ? launch_packed<S_, U_, true, false>(segs, a, stream) \
+                         : launch_packed<S_, U_, false, false>(segs, a, stream); \
   }
     TCS_PCASE(4, 4)
     TCS_PCASE(6, 4)

@@ -155,22 +155,40 @@ gather_header(uintptr_t fa, uint32_t flen, int lane, int sub0)
 // Within a subgroup that parses the same frame these are broadcast loads.
 static __device__ u32x4 k_hdr_zero_chunk;
 
-__device__ __forceinline__ Header
-load_header(uintptr_t fa, uint32_t flen)
+// load_header split in two so callers can issue the five loads together
+// with other loads and parse once they arrive.
+struct HeaderChunks
+{
+  u32x4 c[5];
+};
+
+__device__ __forceinline__ HeaderChunks
+load_header_chunks(uintptr_t fa, uint32_t flen)
 {
   const uintptr_t lo = fa & ~uintptr_t(15);
   const uintptr_t hi = flen ? (fa + flen - 1) & ~uintptr_t(15) : lo;
-  uint32_t w[20];
+  HeaderChunks hc;
 #pragma unroll
   for (int c = 0; c < 5; ++c) {
     uintptr_t q = lo + 16 * c;
     q = q > hi ? hi : q;
-    const u32x4 v = *reinterpret_cast<gchunk_ptr>(
+    hc.c[c] = *reinterpret_cast<gchunk_ptr>(
       flen ? q : reinterpret_cast<uintptr_t>(&k_hdr_zero_chunk));
-    w[4 * c + 0] = v.x;
-    w[4 * c + 1] = v.y;
-    w[4 * c + 2] = v.z;
-    w[4 * c + 3] = v.w;
+  }
+  return hc;
+}
+
+__device__ __forceinline__ Header
+parse_header_chunks(const HeaderChunks& hc, uintptr_t fa, uint32_t flen)
+{
+  const uintptr_t lo = fa & ~uintptr_t(15);
+  uint32_t w[20];
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    w[4 * c + 0] = hc.c[c].x;
+    w[4 * c + 1] = hc.c[c].y;
+    w[4 * c + 2] = hc.c[c].z;
+    w[4 * c + 3] = hc.c[c].w;
   }
   const int h0 = int(fa - lo), s = h0 >> 2;
   const uint32_t r = uint32_t(h0 & 3);
@@ -188,6 +206,12 @@ load_header(uintptr_t fa, uint32_t flen)
       return uint32_t(k) < flen ? (D[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
     },
     flen);
+}
+
+__device__ __forceinline__ Header
+load_header(uintptr_t fa, uint32_t flen)
+{
+  return parse_header_chunks(load_header_chunks(fa, flen), fa, flen);
 }
 
 __device__ __forceinline__ uint32_t

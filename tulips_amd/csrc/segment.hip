@@ -67,6 +67,23 @@ seg_info(const Header& h, uint32_t mss)
   return s;
 }
 
+// Per-frame descriptor written by the prologue (one 16-byte record per input
+// frame): everything a segment builder needs to issue its loads, so that
+// the segment kernel's chain is run start -> descriptors -> data instead of
+// run start -> prefixes -> offsets -> header -> data.
+//   x, y: frame address (lo, hi)   z: flen | hlen << 16 | seg_ok << 31
+//   w: payload | nseg << 16
+__device__ __forceinline__ u32x4
+make_desc(uintptr_t fa, uint32_t flen, const SegInfo& si)
+{
+  u32x4 d;
+  d.x = uint32_t(fa);
+  d.y = uint32_t(uint64_t(fa) >> 32);
+  d.z = (flen & 0xffffu) | (si.hlen << 16) | (si.seg_ok ? 0x80000000u : 0u);
+  d.w = (si.payload & 0xffffu) | (si.nseg << 16);
+  return d;
+}
+
 // ---- exclusive scan of segment counts -------------------------------------
 
 template<int NW>
@@ -100,14 +117,20 @@ block_inclusive_scan(uint32_t x, uint32_t* lds, uint32_t& total)
 __global__ __launch_bounds__(CB) void
 seg_count_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
                  const uint16_t* __restrict__ lens, uint32_t n, uint32_t mss,
-                 uint32_t* __restrict__ first, uint32_t* __restrict__ ws)
+                 uint32_t* __restrict__ first, uint32_t* __restrict__ ws,
+                 u32x4* __restrict__ desc)
 {
   __shared__ uint32_t lds[CB / 64];
   const uint32_t i = blockIdx.x * CB + threadIdx.x;
   uint32_t c = 0;
   if (i < n) {
     const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + offs[i];
-    c = seg_info(load_header(fa, lens[i]), mss).nseg;
+    const uint32_t flen = lens[i];
+    const SegInfo si = seg_info(load_header(fa, flen), mss);
+    c = si.nseg;
+    if (desc) {
+      desc[i] = make_desc(fa, flen, si);
+    }
   }
   uint32_t total;
   const uint32_t inc = block_inclusive_scan<CB / 64>(c, lds, total);
@@ -156,27 +179,14 @@ load_chunk(uintptr_t q)
   return *reinterpret_cast<gchunk_ptr>(q);
 }
 
-// Bytes x .. x+15 from two aligned chunk loads clamped to [lo, hi] (bytes
-// outside the frame come back unspecified; callers never use them):
-// load_win issues the loads, assemble funnel-shifts them (v_alignbyte).
+// Bytes x .. x+15 of a source: two consecutive aligned chunks a, b and the
+// offset m = x & 15 (assemble funnel-shifts them with v_alignbyte). Bytes
+// outside the frame come back unspecified; callers never use them.
 struct Win
 {
   u32x4 a, b;
   uint32_t m;
 };
-
-__device__ __forceinline__ Win
-load_win(uintptr_t x, uintptr_t lo, uintptr_t hi)
-{
-  const uintptr_t q = x & ~uintptr_t(15);
-  const uintptr_t q0 = q < lo ? lo : (q > hi ? hi : q);
-  const uintptr_t q1 = q + 16 > hi ? hi : q + 16;
-  Win w;
-  w.a = load_chunk(q0);
-  w.b = load_chunk(q1);
-  w.m = uint32_t(x & 15);
-  return w;
-}
 
 __device__ __forceinline__ u32x4
 assemble(const Win& w)
@@ -223,42 +233,60 @@ keep_bytes(u32x4 a, int k)
   return v;
 }
 
-// One input frame as a segment builder sees it.
+// One input frame as a segment builder sees it: its prologue descriptor.
 struct SegFrame
 {
   uintptr_t fa, lo, hi;
   uint32_t flen;
-  Header h;
   SegInfo si;
-  bool ip_on, l4_on;
 };
 
-// The frame's header is read by every lane of the subgroup itself
-// (load_header: broadcast chunk loads, no cross-lane traffic).
 __device__ __forceinline__ SegFrame
-seg_frame(uintptr_t fa, uint32_t flen, uint32_t mss)
+frame_of(const u32x4& d)
 {
   SegFrame F;
-  F.fa = fa;
-  F.flen = flen;
-  F.lo = fa & ~uintptr_t(15);
-  F.hi = flen ? (fa + flen - 1) & ~uintptr_t(15) : F.lo;
-  F.h = load_header(fa, flen);
-  F.si = seg_info(F.h, mss);
-  F.ip_on = F.h.ipv4;
-  F.l4_on = F.si.seg_ok || (F.h.tcp && !F.h.trunc && F.h.tcplen >= 18u);
+  F.fa = uintptr_t((uint64_t(d.y) << 32) | d.x);
+  F.flen = d.z & 0xffffu;
+  F.lo = F.fa & ~uintptr_t(15);
+  F.hi = F.flen ? (F.fa + F.flen - 1) & ~uintptr_t(15) : F.lo;
+  F.si.hlen = (d.z >> 16) & 0x7fffu;
+  F.si.seg_ok = (d.z >> 31) != 0;
+  F.si.payload = d.w & 0xffffu;
+  F.si.nseg = d.w >> 16;
   return F;
 }
 
+// The aligned chunk after each lane's (lane + 1's, the next batch slot's for
+// the subgroup's last lane): lane s hands lane s-1 its chunk, lane 0 hands
+// lane G-1 the chunk of the next batch slot.
+template<int G>
+__device__ __forceinline__ u32x4
+next_chunk(const u32x4& cur, const u32x4& nxt, int lane, int sub0)
+{
+  const u32x4 give = lane == 0 ? nxt : cur;
+  const int from = sub0 + ((lane + 1) & (G - 1));
+  u32x4 r;
+  r.x = __shfl(give.x, from, 64);
+  r.y = __shfl(give.y, from, 64);
+  r.z = __shfl(give.z, from, 64);
+  r.w = __shfl(give.w, from, 64);
+  return r;
+}
+
 // Build, checksum and store segment k of frame F as output frame j, on one
-// G-lane subgroup (lane = index in the subgroup). SU chunks per lane per
-// batch, every load of a batch issued before any is used.
+// G-lane subgroup (lane = index in the subgroup, sub0 = its first lane in the
+// wave). Output chunk c holds source bytes [x + 16c, x + 16c + 16), x = the
+// segment's source start: lane l loads ONE aligned source chunk per output
+// chunk (plus one extra for the batch) and takes the following aligned chunk
+// from lane l+1 for the funnel shift, so a batch of SU chunks per lane is
+// SU + 1 loads. The header chunks 0..6 come from one more load per lane and
+// are parsed through cross-lane shuffles; everything is issued before the
+// first use (the prologue's descriptor is all the addresses need).
 template<int G, int SU>
 __device__ __forceinline__ void
 build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* out,
-              uint64_t stride, uint16_t* __restrict__ out_lens, int lane)
+              uint64_t stride, uint16_t* __restrict__ out_lens, int lane, int sub0)
 {
-  const Header& h = F.h;
   const SegInfo& si = F.si;
   const uint32_t slice = si.seg_ok ? min(mss, si.payload - k * mss) : 0u;
   const uint32_t dlen = si.nseg == 1 ? F.flen : si.hlen + slice;
@@ -268,6 +296,39 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
     }
     return;
   }
+  const uintptr_t shift = uintptr_t(k) * mss;
+  const uintptr_t dst = reinterpret_cast<uintptr_t>(out) + uintptr_t(j) * stride;
+  const int nchunks = int((dlen + 15) >> 4);
+  const uintptr_t xs = F.fa + shift;          // source of output byte 0
+  const uintptr_t q0 = xs & ~uintptr_t(15);
+  const uint32_t m = uint32_t(xs & 15);
+  auto src_chunk = [&](int c) {               // aligned source chunk c, clamped
+    uintptr_t q = q0 + 16 * uintptr_t(c);
+    q = q < F.lo ? F.lo : (q > F.hi ? F.hi : q);
+    return load_chunk(q);
+  };
+
+  // ---- batch 0 loads: payload chunks (+1), header chunk --------------------
+  u32x4 A[SU + 1];
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    A[u] = src_chunk(lane + G * u);
+  }
+  A[SU] = src_chunk(lane == 0 ? G * SU : lane + G * (SU - 1));
+  uintptr_t hq = F.lo + 16 * uintptr_t(min(lane, 6));
+  hq = hq > F.hi ? F.hi : hq;
+  const u32x4 H = load_chunk(hq);             // frame chunk min(lane, 6)
+
+  // ---- header fields (chunks 0..4 from lanes 0..4) -------------------------
+  uint32_t FW[13];
+  header_words(H, int(F.fa - F.lo), sub0, FW);
+  const Header h = parse_header<true>(
+    [&](int b) -> uint32_t {
+      return uint32_t(b) < F.flen ? (FW[b >> 2] >> (8 * (b & 3))) & 0xffu : 0u;
+    },
+    F.flen);
+  const bool ip_on = h.ipv4;
+  const bool l4_on = si.seg_ok || (h.tcp && !h.trunc && h.tcplen >= 18u);
   const uint32_t total = si.seg_ok ? 20u + 4u * h.doff + slice : h.total;
   const uint32_t tcp_end = si.seg_ok ? 14u + total : 34u + h.tcplen;
   const uint32_t id = (h.id + k) & 0xffffu;
@@ -279,36 +340,35 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
   if (k > 0) {
     tfl &= ~TCP_CWR;
   }
-  const uintptr_t shift = uintptr_t(k) * mss;
-  const uintptr_t dst = reinterpret_cast<uintptr_t>(out) + uintptr_t(j) * stride;
-  const int nchunks = int((dlen + 15) >> 4);
+  // header window of output chunks 0..5 (segments k > 0 take their header
+  // bytes, < hlen <= 94, from the frame's own header)
+  Win hw;
+  hw.a = H;
+  hw.b = next_chunk<G>(H, H, lane, sub0);
+  hw.m = uint32_t(F.fa & 15);
+
   uint64_t ip_acc = 0, l4_acc = 0;
   u32x4 keep = {0, 0, 0, 0};
-  for (int c0 = lane; c0 < nchunks; c0 += G * SU) {
-    Win pw[SU];
+  auto consume = [&](const u32x4 (&X)[SU + 1], int c0) {
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
-      const int cb = 16 * min(c0 + G * u, nchunks - 1);
-      pw[u] = load_win(F.fa + shift + cb, F.lo, F.hi);
-    }
-    // header bytes (< hlen <= 94) of segments k > 0 come from the frame's
-    // own header: only chunks 0..5, i.e. lanes 0..5 of the first batch
-    const Win hw = load_win(F.fa + 16 * min(c0, 5), F.lo, F.hi);
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
+      Win w;
+      w.a = X[u];
+      w.b = next_chunk<G>(X[u], X[u + 1], lane, sub0);
+      w.m = m;
       const int c = c0 + G * u;
       if (c >= nchunks) {
-        break;
+        continue;   // (no break: the shuffles above need every lane)
       }
       const int cb = 16 * c;
-      u32x4 v = assemble(pw[u]);
+      u32x4 v = assemble(w);
       if (shift != 0 && uint32_t(cb) < si.hlen) {
         v = merge_bytes(assemble(hw), v, int(si.hlen) - cb);
       }
       if (uint32_t(cb + 16) > dlen) {
         v = keep_bytes(v, int(dlen) - cb);
       }
-      if (c == 1 && F.ip_on) {
+      if (c == 1 && ip_on) {
         if (si.seg_ok) {
           v.x = (total >> 8) | ((total & 0xffu) << 8) | ((id >> 8) << 16) |
                 ((id & 0xffu) << 24);
@@ -321,13 +381,13 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
         v.z = (v.z & 0xffff0000u) | ((seq >> 8) & 0xffu) | ((seq & 0xffu) << 8);
         v.w = (v.w & 0x00ffffffu) | (tfl << 24);
       }
-      if (c == 3 && F.l4_on) {
+      if (c == 3 && l4_on) {
         v.x &= 0x0000ffffu; // chksum = 0
       }
-      if (F.ip_on && cb < 34) {
+      if (ip_on && cb < 34) {
         ip_acc += masked_hsum(v, max(14 - cb, 0), min(34 - cb, 16));
       }
-      if (F.l4_on && cb + 16 > 34 && uint32_t(cb) < tcp_end) {
+      if (l4_on && cb + 16 > 34 && uint32_t(cb) < tcp_end) {
         l4_acc += masked_hsum(v, max(34 - cb, 0), min(int(tcp_end) - cb, 16));
       }
       if (c == 1 || c == 3) {
@@ -336,17 +396,28 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
         *reinterpret_cast<gchunk_wptr>(dst + cb) = v;
       }
     }
+  };
+  consume(A, lane);
+  // further batches: jumbo segments only (> G*SU chunks); uniform per subgroup
+  for (int b0 = G * SU; b0 < nchunks; b0 += G * SU) {
+    u32x4 X[SU + 1];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      X[u] = src_chunk(b0 + lane + G * u);
+    }
+    X[SU] = src_chunk(lane == 0 ? b0 + G * SU : b0 + lane + G * (SU - 1));
+    consume(X, b0 + lane);
   }
   const uint32_t ip = sub_sum<G>(fold64(ip_acc));
   const uint32_t l4 = sub_sum<G>(fold64(l4_acc));
   if (lane == 1 && nchunks > 1) {
-    if (F.ip_on) {
+    if (ip_on) {
       keep.z |= ~finish(ip, false, MODE_INET, 0, 0, 0, 20) & 0xffffu;
     }
     *reinterpret_cast<gchunk_wptr>(dst + 16) = keep;
   }
   if (lane == 3 && nchunks > 3) {
-    if (F.l4_on) {
+    if (l4_on) {
       const uint32_t r = finish(l4, false, MODE_TCP, 0, h.src, h.dst, total - 20u);
       keep.x |= (~r & 0xffffu) << 16;
     }
@@ -391,7 +462,7 @@ __global__ __launch_bounds__(1024) void
 seg_prologue_small_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
                           const uint16_t* __restrict__ lens, uint32_t n, uint32_t mss,
                           uint32_t* __restrict__ first, uint32_t capacity,
-                          uint32_t* __restrict__ runs)
+                          uint32_t* __restrict__ runs, u32x4* __restrict__ desc)
 {
   __shared__ uint32_t lds[16];
   uint32_t carry = 0;
@@ -400,7 +471,12 @@ seg_prologue_small_kernel(const uint8_t* base, const uint64_t* __restrict__ offs
     uint32_t c = 0;
     if (i < n) {
       const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + offs[i];
-      c = seg_info(load_header(fa, lens[i]), mss).nseg;
+      const uint32_t flen = lens[i];
+      const SegInfo si = seg_info(load_header(fa, flen), mss);
+      c = si.nseg;
+      if (desc) {
+        desc[i] = make_desc(fa, flen, si);
+      }
     }
     uint32_t tile;
     const uint32_t a = carry + block_inclusive_scan<16>(c, lds, tile) - c;
@@ -422,8 +498,7 @@ seg_prologue_small_kernel(const uint8_t* base, const uint64_t* __restrict__ offs
 // super-frames at MSS 1460 is 45,056 independent segments.
 template<int G, int SU>
 __global__ __launch_bounds__(256) void
-segment_kernel(const uint8_t* in, const uint64_t* __restrict__ offs,
-               const uint16_t* __restrict__ lens, uint32_t mss,
+segment_kernel(const u32x4* __restrict__ desc, uint32_t mss,
                const uint32_t* __restrict__ first, uint32_t n,
                const uint32_t* __restrict__ runs, uint8_t* out, uint64_t stride,
                uint32_t capacity, uint16_t* __restrict__ out_lens)
@@ -431,6 +506,7 @@ segment_kernel(const uint8_t* in, const uint64_t* __restrict__ offs,
   constexpr uint32_t S = 256 / G;
   constexpr uint32_t L = RUN + S + 1; // frames [runs[jb/RUN], ...] that can hold jb..jb+S-1
   __shared__ uint32_t pre[L];
+  __shared__ u32x4 dsc[L];
   const int lane = threadIdx.x & (G - 1);
   const uint32_t sub = threadIdx.x / G;
   const uint32_t total = min(first[n], capacity);
@@ -438,6 +514,7 @@ segment_kernel(const uint8_t* in, const uint64_t* __restrict__ offs,
     const uint32_t ir = runs[jb / RUN];
     if (threadIdx.x < L) {
       pre[threadIdx.x] = first[min(ir + threadIdx.x, n)];
+      dsc[threadIdx.x] = desc[min(ir + threadIdx.x, n - 1)];
     }
     __syncthreads();
     const uint32_t j = jb + sub;
@@ -447,17 +524,16 @@ segment_kernel(const uint8_t* in, const uint64_t* __restrict__ offs,
       while (pre[f + 1] <= j) {
         ++f;
       }
-      const uint32_t i = ir + f;
-      const SegFrame F =
-        seg_frame(reinterpret_cast<uintptr_t>(in) + offs[i], lens[i], mss);
-      build_segment<G, SU>(F, j - pre[f], j, mss, out, stride, out_lens, lane);
+      build_segment<G, SU>(frame_of(dsc[f]), j - pre[f], j, mss, out, stride, out_lens,
+                           lane, int(threadIdx.x & 63) & ~(G - 1));
     }
     __syncthreads();
   }
 }
 
-// Per-device workspace: the scan's block totals (MAX_FRAMES / CB words) and
-// the run starts (one word per RUN output segments). Made on first use
+// Per-device workspace: the scan's block totals (MAX_FRAMES / CB words), the
+// run starts (one word per RUN output segments) and the frame descriptors
+// (16 bytes per input frame). Made on first use
 // and grown when a call's capacity needs a longer map; a call that grows it
 // cannot be captured in a HIP graph (warm it up outside the capture).
 struct Workspace
@@ -465,12 +541,15 @@ struct Workspace
   uint32_t* blocks = nullptr;
   uint32_t* runs = nullptr;
   uint64_t nruns = 0;
+  u32x4* desc = nullptr;
+  uint64_t ndesc = 0;
 };
 std::mutex g_ws_mutex;
 Workspace g_ws[64];
 
 hipError_t
-workspace(uint32_t capacity, uint32_t** blocks, uint32_t** runs)
+workspace(uint32_t capacity, uint32_t n, uint32_t** blocks, uint32_t** runs,
+          u32x4** desc)
 {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -505,8 +584,23 @@ workspace(uint32_t capacity, uint32_t** blocks, uint32_t** runs)
     w.runs = p;
     w.nruns = want;
   }
+  if (capacity && uint64_t(n) > w.ndesc) {
+    const uint64_t want = n < 65536 ? 65536 : uint64_t(n);
+    u32x4* p = nullptr;
+    e = hipMalloc(reinterpret_cast<void**>(&p), sizeof(u32x4) * want);
+    if (e != hipSuccess) {
+      return e;
+    }
+    if (w.desc) {
+      (void)hipDeviceSynchronize(); // the old array may still be in use
+      (void)hipFree(w.desc);
+    }
+    w.desc = p;
+    w.ndesc = want;
+  }
   *blocks = w.blocks;
   *runs = w.runs;
+  *desc = w.desc;
   return hipSuccess;
 }
 
@@ -538,7 +632,8 @@ tulips_csum_segment_frames(const uint8_t* in_base, const uint64_t* in_offsets,
   }
   uint32_t* ws = nullptr;
   uint32_t* runs = nullptr;
-  hipError_t e = workspace(out_capacity, &ws, &runs);
+  u32x4* desc = nullptr;
+  hipError_t e = workspace(out_capacity, n, &ws, &runs, &desc);
   if (e != hipSuccess) {
     return e == hipErrorOutOfMemory ? TULIPS_STATUS_NO_MORE_RESOURCES
                                     : TULIPS_STATUS_HARDWARE_ERROR;
@@ -548,10 +643,11 @@ tulips_csum_segment_frames(const uint8_t* in_base, const uint64_t* in_offsets,
   if (n <= SMALL_N) {
     hipLaunchKernelGGL(seg_prologue_small_kernel, dim3(1), dim3(1024), 0, st, in_base,
                        in_offsets, in_lengths, n, mss, out_first, out_capacity,
-                       out_capacity ? runs : nullptr);
+                       out_capacity ? runs : nullptr, out_capacity ? desc : nullptr);
   } else {
     hipLaunchKernelGGL(seg_count_kernel, dim3(nb), dim3(CB), 0, st, in_base,
-                       in_offsets, in_lengths, n, mss, out_first, ws);
+                       in_offsets, in_lengths, n, mss, out_first, ws,
+                       out_capacity ? desc : nullptr);
     hipLaunchKernelGGL(seg_scan_blocks_kernel, dim3(1), dim3(1024), 0, st, ws, nb,
                        out_first + n);
     hipLaunchKernelGGL(seg_add_kernel, dim3(nb), dim3(CB), 0, st, n, out_first, ws);
@@ -568,13 +664,13 @@ tulips_csum_segment_frames(const uint8_t* in_base, const uint64_t* in_offsets,
     const uint64_t want = (uint64_t(out_capacity) + per_block - 1) / per_block;
     const uint32_t blocks = uint32_t(want > 65535 ? 65535 : want);
     if (small) {
-      hipLaunchKernelGGL((segment_kernel<16, 6>), dim3(blocks), dim3(256), 0, st, in_base,
-                         in_offsets, in_lengths, mss, out_first, n, runs, out_base,
-                         out_stride, out_capacity, out_lengths);
+      hipLaunchKernelGGL((segment_kernel<16, 6>), dim3(blocks), dim3(256), 0, st, desc,
+                         mss, out_first, n, runs, out_base, out_stride, out_capacity,
+                         out_lengths);
     } else {
-      hipLaunchKernelGGL((segment_kernel<64, 6>), dim3(blocks), dim3(256), 0, st, in_base,
-                         in_offsets, in_lengths, mss, out_first, n, runs, out_base,
-                         out_stride, out_capacity, out_lengths);
+      hipLaunchKernelGGL((segment_kernel<64, 6>), dim3(blocks), dim3(256), 0, st, desc,
+                         mss, out_first, n, runs, out_base, out_stride, out_capacity,
+                         out_lengths);
     }
   }
   e = hipGetLastError();
