@@ -420,6 +420,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                    "avg_launch_us": round(t * 1e6, 2),
                    "pipeline": pipe_entry(b9, tp),
                    "geometry": f"G={tun.group},U={tun.unroll}",
+                   "traffic": read_traffic("F9000"),
                    "parity": "ok" if fnv1a_u16(o) == gold.get("F9000", {}).get("fnv1a64")
                    else "MISMATCH"}
     del a9, o9
@@ -454,6 +455,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                   "geometry": "packed: one wave per 8 segments, chunks packed end to end, "
                               "4 x 64-chunk windows in flight, double-buffered, "
                               "1024-thread blocks",
+                  "traffic": read_traffic("ZIPF"),
                   "parity": "ok" if fnv1a_u16(o) == gold.get("ZIPF", {}).get("fnv1a64")
                   else "MISMATCH"}
     del az, oz
@@ -527,14 +529,15 @@ def frame_extras(torch, csum, dev, timer):
     ex["frames_generate_F1514"] = rate_entry(
         alg, t, kernel="frame_kernel<GENERATE, 16 lanes x 6 chunks per frame>",
         workload="65,536 x 1514 B TCP frames per launch, 2 KiB slots, 8 bursts rotated",
-        pipeline=pipe_entry(alg, tp))
+        pipeline=pipe_entry(alg, tp), traffic=read_traffic("frames_generate_F1514"))
     t = timer(fval, 64)
     tp = timer(fval, 64, branches=PIPE)
     ok = bool((flags == 0x0F).all().item())
     ex["frames_validate_F1514"] = rate_entry(
         alg, t, kernel="frame_kernel<VALIDATE, 16 lanes x 6 chunks per frame>",
         workload="same frames: generated checksums verified (flags == 0x0F)",
-        pipeline=pipe_entry(alg, tp), parity="ok" if ok else "MISMATCH")
+        pipeline=pipe_entry(alg, tp), parity="ok" if ok else "MISMATCH",
+        traffic=read_traffic("frames_validate_F1514"))
     del ar, v, flags
 
     # Segmentation offload: 4 batches x 1024 super-frames of 64,294 B (44 x
@@ -577,6 +580,7 @@ def frame_extras(torch, csum, dev, timer):
                          "(16-lane subgroup per output segment)",
         workload="1024 super-frames of 64,294 B -> 45,056 segments of 1514 B per call",
         segments_per_s=round(nseg / t / 1e6, 2) * 1e6,
+        traffic=read_traffic("segment_TSO_64K_mss1460"),
         parity="ok" if ok else "MISMATCH")
     del sa, sv, sout
 
@@ -607,7 +611,8 @@ def frame_extras(torch, csum, dev, timer):
              for k in range(len(js)))
     ex["rss_toeplitz_16M"] = rate_entry(
         nt * 16, t, kernel="rss_kernel (12x256 LDS tables)", Mtuples_per_s=round(nt / t / 1e6, 1),
-        pipeline=pipe_entry(nt * 16, tp), parity="ok" if ok else "MISMATCH")
+        pipeline=pipe_entry(nt * 16, tp), parity="ok" if ok else "MISMATCH",
+        traffic=read_traffic("rss_toeplitz_16M"))
     return ex
 
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output into profiles/ (run here, after a GPU session).
 
-  python tools/pmc_traffic.py gpurun_out/prof_r01 profiles r01
+  python tools/pmc_traffic.py gpurun_out/prof_<tag> profiles <tag>
+(after TAG=<tag> tools/gpu_check.sh on the GPU box)
 
 Reads <prof>/stats/run_kernel_stats.csv and the separate --pmc passes
 (<prof>/pmc_fetch, pmc_write, pmc_rdreq), and writes
@@ -25,9 +26,19 @@ from collections import defaultdict
 WORKLOADS = {
     "csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>": "F1500",
     "csum_kernel<64, 8, true, tulips_amd::(anonymous namespace)::FixedSegs>": "F9000",
-    "csum_hybrid_kernel<16, 4, 8, true>": "ZIPF",
+    "csum_packed_kernel<8, 4, true, true>": "ZIPF",
+    "frame_kernel<false, 16, 6, true>": "frames_validate_F1514",
+    "frame_kernel<true, 16, 6, true>": "frames_generate_F1514",
+    "segment_kernel<16, 6>": "segment_TSO_64K_mss1460",
+    "rss_kernel": "rss_toeplitz_16M",
 }
-ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673}
+# algorithmic bytes per launch (bench.py): segment bytes; frame bytes; bytes
+# read + written by segmentation (super-frames in, segments out); RSS 12 B in
+# + 4 B out per tuple
+ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673,
+              "frames_validate_F1514": 65536 * 1514, "frames_generate_F1514": 65536 * 1514,
+              "segment_TSO_64K_mss1460": 1024 * 64294 + 45056 * 1514,
+              "rss_toeplitz_16M": (1 << 24) * 16}
 
 
 def label(name):

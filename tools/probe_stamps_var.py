@@ -42,8 +42,9 @@ def main():
     stamps = torch.zeros(4 * 300000, dtype=torch.int64, device=dev)
     sh = torch.cuda.current_stream().cuda_stream
     chunks = ((offs % 16) + lens + 15) // 16 * (lens > 0)
-    for s_, u_ in ((8, 4), (16, 4)):
-        t = csum.Tuning(kind=csum.KIND_PACKED, group=s_, unroll=u_, nontemporal=1)
+    for s_, u_, sps, blk in ((8, 4, 1, 256), (8, 4, 2, 256), (8, 4, 2, 1024)):
+        t = csum.Tuning(kind=csum.KIND_PACKED, group=s_, unroll=u_, nontemporal=1, sps=sps,
+                        block=blk)
         for i in range(NB):
             lib.tulips_csum_batch_tuned(buf.data_ptr() + (i % NB) * nb, doffs.data_ptr(),
                                         dlens.data_ptr(), None, None, None, out.data_ptr(),
@@ -65,7 +66,7 @@ def main():
         grid = np.arange(0, t1.max() + 0.01, 0.01)
         alive = np.array([((t0 <= x) & (t1 > x)).sum() for x in grid])
         rep = {
-            "geom": f"packed{s_}x{u_}", "waves": int(n), "span_us": round(float(t1.max()), 2),
+            "geom": f"packed{s_}x{u_}b{blk}" + ("pf" if sps == 2 else ""), "waves": int(n), "span_us": round(float(t1.max()), 2),
             "alive_max": int(alive.max()),
             "started_by_us": [[x, int((t0 <= x).sum())] for x in (0.5, 1, 1.5, 2, 4, 6, 8, 10)],
             "xcc_waves": np.bincount(st[:, 2].astype(np.int64) & 15, minlength=8).tolist(),

@@ -155,8 +155,9 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
 {
   switch (kind) {
     case TULIPS_CSUM_KIND_SUBGROUP:
-      return spw == 1 && (group == 16 || group == 32 || group == 64) &&
-             (unroll == 2 || unroll == 4 || unroll == 8);
+      return spw == 1 && (((group == 16 || group == 32 || group == 64) &&
+                           (unroll == 2 || unroll == 4 || unroll == 8)) ||
+                          (group == 16 && unroll == 6) || (group == 32 && unroll == 3));
     case TULIPS_CSUM_KIND_HYBRID:
       return variable &&
              ((group == 8 && unroll == 4 && (spw == 1 || spw == 2 || spw == 4)) ||

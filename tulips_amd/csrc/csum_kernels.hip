@@ -701,8 +701,10 @@ dispatch(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
   }
   TCS_CASE(16, 2)
   TCS_CASE(16, 4)
+  TCS_CASE(16, 6)
   TCS_CASE(16, 8)
   TCS_CASE(32, 2)
+  TCS_CASE(32, 3)
   TCS_CASE(32, 4)
   TCS_CASE(32, 8)
   TCS_CASE(64, 2)
