@@ -232,6 +232,12 @@ int tulips_csum_generate_frames(uint8_t* base, const uint64_t* offsets,
  * is not written (length 0), nor is any j >= out_capacity. With
  * out_capacity == 0 only out_first is computed (to size the output).
  * n <= 2^24, 1 <= mss <= 65535. Input frames are not modified.
+ *
+ * The library keeps a device workspace per (device, stream), made or grown
+ * on a call that needs more room; calls on one stream run in order, calls
+ * on different streams may overlap. A call inside a stream capture must not
+ * need that (returns InvalidArgument): make one call of the same or larger
+ * size on that stream before capturing.
  */
 int tulips_csum_segment_frames(const uint8_t* in_base,
                                const uint64_t* in_offsets,

@@ -191,14 +191,16 @@ default_tuning(uint32_t len, bool variable)
   t.sps = 1;
   if (variable) {
     // one wave per 8 segments, chunks packed end to end, 4 windows in
-    // flight, double-buffered, 1024-thread blocks (tools/probe_packed.py,
-    // profiles/probe_packed_r01.json: ZIPF 14.1 us vs 16.8 single-buffered
-    // and 18.7 hybrid; 1500 B through offsets 19.3 vs 34.2 hybrid)
+    // flight, double-buffered (tools/probe_packed.py,
+    // profiles/probe_packed_r01.json: ZIPF 14.8 us vs 16.8 single-buffered
+    // and 18.7 hybrid; 1500 B through offsets 19.1 vs 34.2 hybrid).
+    // 256-thread blocks: 1024-thread blocks are 0.6 us faster alone but
+    // cannot share CUs with a concurrent launch (overlapped bursts: 21 us
+    // per launch vs 10)
     t.kind = TULIPS_CSUM_KIND_PACKED;
     t.group = 8;
     t.unroll = 4;
     t.sps = 2;
-    t.block = 1024;
     return t;
   }
   const uint32_t nch = len / 16 + 2;

@@ -33,7 +33,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
 #include <mutex>
+#include <utility>
 
 #include "../../include/tulips_csum.h"
 #include "csum_common.h"
@@ -531,11 +533,13 @@ segment_kernel(const u32x4* __restrict__ desc, uint32_t mss,
   }
 }
 
-// Per-device workspace: the scan's block totals (MAX_FRAMES / CB words), the
-// run starts (one word per RUN output segments) and the frame descriptors
-// (16 bytes per input frame). Made on first use
-// and grown when a call's capacity needs a longer map; a call that grows it
-// cannot be captured in a HIP graph (warm it up outside the capture).
+// Workspace per (device, stream): the scan's block totals (MAX_FRAMES / CB
+// words), the run starts (one word per RUN output segments) and the frame
+// descriptors (16 bytes per input frame). Calls on one stream run in order,
+// so they can share one; calls on different streams may overlap, so each
+// stream gets its own. Made on first use and grown when a call's capacity
+// needs a longer map; a call that grows it cannot be captured in a HIP graph
+// (warm it up outside the capture).
 struct Workspace
 {
   uint32_t* blocks = nullptr;
@@ -545,22 +549,29 @@ struct Workspace
   uint64_t ndesc = 0;
 };
 std::mutex g_ws_mutex;
-Workspace g_ws[64];
+std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
 
 hipError_t
-workspace(uint32_t capacity, uint32_t n, uint32_t** blocks, uint32_t** runs,
-          u32x4** desc)
+workspace(hipStream_t stream, uint32_t capacity, uint32_t n, uint32_t** blocks,
+          uint32_t** runs, u32x4** desc)
 {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) {
     return e;
   }
-  if (dev < 0 || dev >= 64) {
-    return hipErrorInvalidDevice;
-  }
+  // making or growing a workspace (hipMalloc, a stream sync) cannot happen
+  // inside a stream capture: such a call fails with InvalidArgument
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(stream, &cs);
+  const bool capturing = cs != hipStreamCaptureStatusNone;
   std::lock_guard<std::mutex> g(g_ws_mutex);
-  Workspace& w = g_ws[dev];
+  Workspace& w = g_ws[std::make_pair(dev, stream)];
+  const uint64_t need = (uint64_t(capacity) + RUN - 1) / RUN;
+  if (capturing &&
+      (!w.blocks || need > w.nruns || (capacity && uint64_t(n) > w.ndesc))) {
+    return hipErrorStreamCaptureUnsupported;
+  }
   if (!w.blocks) {
     e = hipMalloc(reinterpret_cast<void**>(&w.blocks),
                   sizeof(uint32_t) * (MAX_FRAMES / CB));
@@ -569,7 +580,6 @@ workspace(uint32_t capacity, uint32_t n, uint32_t** blocks, uint32_t** runs,
       return e;
     }
   }
-  const uint64_t need = (uint64_t(capacity) + RUN - 1) / RUN;
   if (need > w.nruns) {
     const uint64_t want = need < 65536 ? 65536 : need;
     uint32_t* p = nullptr;
@@ -578,7 +588,7 @@ workspace(uint32_t capacity, uint32_t n, uint32_t** blocks, uint32_t** runs,
       return e;
     }
     if (w.runs) {
-      (void)hipDeviceSynchronize(); // the old array may still be in use
+      (void)hipStreamSynchronize(stream); // the old array may still be in use
       (void)hipFree(w.runs);
     }
     w.runs = p;
@@ -592,7 +602,7 @@ workspace(uint32_t capacity, uint32_t n, uint32_t** blocks, uint32_t** runs,
       return e;
     }
     if (w.desc) {
-      (void)hipDeviceSynchronize(); // the old array may still be in use
+      (void)hipStreamSynchronize(stream); // the old array may still be in use
       (void)hipFree(w.desc);
     }
     w.desc = p;
@@ -633,10 +643,11 @@ tulips_csum_segment_frames(const uint8_t* in_base, const uint64_t* in_offsets,
   uint32_t* ws = nullptr;
   uint32_t* runs = nullptr;
   u32x4* desc = nullptr;
-  hipError_t e = workspace(out_capacity, n, &ws, &runs, &desc);
+  hipError_t e = workspace(st, out_capacity, n, &ws, &runs, &desc);
   if (e != hipSuccess) {
-    return e == hipErrorOutOfMemory ? TULIPS_STATUS_NO_MORE_RESOURCES
-                                    : TULIPS_STATUS_HARDWARE_ERROR;
+    return e == hipErrorOutOfMemory                ? TULIPS_STATUS_NO_MORE_RESOURCES
+           : e == hipErrorStreamCaptureUnsupported ? TULIPS_STATUS_INVALID_ARGUMENT
+                                                   : TULIPS_STATUS_HARDWARE_ERROR;
   }
   const uint32_t nb = (n + CB - 1) / CB;
   (void)hipGetLastError();
