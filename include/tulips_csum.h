@@ -124,7 +124,8 @@ int tulips_csum_verify(const uint8_t* base, const uint64_t* offsets,
 typedef struct tulips_csum_ctx tulips_csum_ctx;
 
 /* A context owns a stream, pinned staging and device buffers sized for
- * `chunk_bytes` of segment bytes per pipeline stage (0 = 64 MiB). */
+ * `chunk_bytes` of segment bytes per pipeline stage (0 = 16 MiB; three
+ * stages), and a pool of threads for the staging copy. */
 int tulips_csum_ctx_create(int device, uint64_t chunk_bytes,
                            tulips_csum_ctx** ctx);
 int tulips_csum_ctx_destroy(tulips_csum_ctx* ctx);

@@ -6,8 +6,9 @@
 // a reused read buffer for npipe, include/tulips/transport/npipe/Device.h:103)
 // and are checksummed per frame on the CPU. Here a batch is cut into chunks
 // of <= chunk_bytes; each chunk goes host -> pinned staging -> HBM -> kernel
-// -> results back, on two pipeline slots with their own streams so that
-// packing chunk k+1 on the CPU overlaps the copy and kernel of chunk k.
+// -> results back, on NSLOTS pipeline slots with their own streams so that
+// packing the next chunks on the CPU (a pool of PACK_THREADS threads owned by
+// the context) overlaps the copies and kernels of the previous ones.
 //
 // When the caller's arena is already pinned (hipHostMalloc/hipHostRegister,
 // as a registered NIC ring would be) and a chunk's segments lie in a compact
@@ -17,6 +18,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -30,9 +34,83 @@ using namespace tulips_amd;
 
 namespace {
 
-constexpr uint64_t DEFAULT_CHUNK = 64ull << 20;
+// 16 MiB chunks on 3 slots: the first chunk's pack and the last chunk's
+// kernel + D2H are the only unoverlapped steps
+constexpr uint64_t DEFAULT_CHUNK = 16ull << 20;
 constexpr uint32_t MAX_SEGS_PER_CHUNK = 1u << 20;
-constexpr int PACK_THREADS = 4;
+constexpr int NSLOTS = 3;
+constexpr int PACK_THREADS = 8;
+
+// Persistent workers for the staging copy (a thread per pack would cost
+// tens of microseconds per chunk to create). run(f) calls f(0..PACK_THREADS-1)
+// once each, part 0 on the calling thread, and returns when all are done.
+class PackPool
+{
+public:
+  PackPool()
+  {
+    for (int t = 1; t < PACK_THREADS; ++t) {
+      threads_.emplace_back([this, t] { worker(t); });
+    }
+  }
+  ~PackPool()
+  {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) {
+      t.join();
+    }
+  }
+  void run(const std::function<void(int)>& f)
+  {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      work_ = &f;
+      pending_ = PACK_THREADS - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return pending_ == 0; });
+    work_ = nullptr;
+  }
+
+private:
+  void worker(int id)
+  {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) {
+          return;
+        }
+        seen = gen_;
+        f = work_;
+      }
+      (*f)(id);
+      {
+        std::lock_guard<std::mutex> g(m_);
+        if (--pending_ == 0) {
+          done_.notify_one();
+        }
+      }
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* work_ = nullptr;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
 
 struct Slot
 {
@@ -85,7 +163,8 @@ struct tulips_csum_ctx
 {
   int device = 0;
   uint64_t chunk = DEFAULT_CHUNK;
-  Slot slots[2];
+  Slot slots[NSLOTS];
+  PackPool pool;
 };
 
 namespace {
@@ -187,9 +266,10 @@ retire(Slot& s, const Job& job)
   return e;
 }
 
-// Copy segments [i0, i1) into the slot's pinned staging, back to back.
+// Copy segments [i0, i1) into the slot's pinned staging, back to back,
+// split over the context's pack threads by segment count.
 void
-pack(Slot& s, const uint8_t* base, const uint64_t* offsets,
+pack(PackPool& pool, Slot& s, const uint8_t* base, const uint64_t* offsets,
      const uint16_t* lengths, uint32_t i0, uint32_t i1)
 {
   auto copy_range = [&](uint32_t a, uint32_t b) {
@@ -198,20 +278,15 @@ pack(Slot& s, const uint8_t* base, const uint64_t* offsets,
     }
   };
   const uint64_t total = s.h_offs[i1 - 1 - i0] + lengths[i1 - 1];
-  if (total < (8ull << 20) || i1 - i0 < 64) {
+  if (total < (1ull << 20) || i1 - i0 < 64) {
     copy_range(i0, i1);
     return;
   }
-  std::thread ts[PACK_THREADS];
   const uint32_t cnt = i1 - i0;
-  for (int t = 0; t < PACK_THREADS; ++t) {
-    const uint32_t a = i0 + uint32_t(uint64_t(cnt) * t / PACK_THREADS);
-    const uint32_t b = i0 + uint32_t(uint64_t(cnt) * (t + 1) / PACK_THREADS);
-    ts[t] = std::thread(copy_range, a, b);
-  }
-  for (auto& t : ts) {
-    t.join();
-  }
+  pool.run([&](int t) {
+    copy_range(i0 + uint32_t(uint64_t(cnt) * t / PACK_THREADS),
+               i0 + uint32_t(uint64_t(cnt) * (t + 1) / PACK_THREADS));
+  });
 }
 
 } // namespace
@@ -241,7 +316,12 @@ tulips_csum_ctx_create(int device, uint64_t chunk_bytes, tulips_csum_ctx** ctx)
   if ((e = hipSetDevice(device)) != hipSuccess) {
     return status_of(e);
   }
-  auto* c = new (std::nothrow) tulips_csum_ctx();
+  tulips_csum_ctx* c = nullptr;
+  try {
+    c = new tulips_csum_ctx(); // starts the pack threads
+  } catch (...) {
+    c = nullptr;
+  }
   if (!c) {
     (void)hipSetDevice(prev);
     return TULIPS_STATUS_NO_MORE_RESOURCES;
@@ -325,7 +405,7 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
       hsrc = base + lo;
       hbytes = hi - lo;
     } else {
-      pack(s, base, offsets, lengths, i, j);
+      pack(ctx->pool, s, base, offsets, lengths, i, j);
       hsrc = s.h_bytes;
       hbytes = bytes;
     }
@@ -376,10 +456,12 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
       a.bad = nullptr;
       a.n = cnt;
       a.mode = job.mode;
-      a.kind = TULIPS_CSUM_KIND_HYBRID; // the variable-length default
-      a.group = 16;
-      a.spw = 1;
+      // the variable-length default geometry (csum_capi.hip default_tuning)
+      a.kind = TULIPS_CSUM_KIND_PACKED;
+      a.group = 8;
       a.unroll = 4;
+      a.spw = 2;
+      a.block = 256;
       a.nontemporal = true;
       a.max_blocks = 0;
       TCS_Q(launch_var(dbase, s.d_offs, s.d_lens, a, st));
@@ -392,7 +474,7 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
     s.i0 = i;
     s.i1 = j;
     i = j;
-    slot ^= 1;
+    slot = (slot + 1) % NSLOTS;
   }
   for (auto& s : ctx->slots) {
     const hipError_t r = retire(s, job);
