@@ -23,15 +23,19 @@ import sys
 from collections import defaultdict
 
 # kernel name fragment -> workload label (bench.py default geometries)
-WORKLOADS = {
-    "csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>": "F1500",
-    "csum_kernel<64, 8, true, tulips_amd::(anonymous namespace)::FixedSegs>": "F9000",
-    "csum_packed_kernel<8, 4, true, true>": "ZIPF",
-    "frame_kernel<false, 16, 6, true>": "frames_validate_F1514",
-    "frame_kernel<true, 16, 6, true>": "frames_generate_F1514",
-    "segment_kernel<16, 6>": "segment_TSO_64K_mss1460",
-    "rss_kernel": "rss_toeplitz_16M",
-}
+# (kernel name fragment, grid size or None, workload label): bench.py's
+# default geometries. The ZIPF kernel is also what the host path launches
+# per staging chunk, so ZIPF is told apart by its grid (65,536 segments /
+# 8 per wave = 8,192 waves = 524,288 threads).
+WORKLOADS = [
+    ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
+    ("csum_kernel<64, 8, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
+    ("csum_packed_kernel<8, 4, true, true>", 524288, "ZIPF"),
+    ("frame_kernel<false, 16, 6, true>", None, "frames_validate_F1514"),
+    ("frame_kernel<true, 16, 6, true>", None, "frames_generate_F1514"),
+    ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
+    ("rss_kernel", None, "rss_toeplitz_16M"),
+]
 # algorithmic bytes per launch (bench.py): segment bytes; frame bytes; bytes
 # read + written by segmentation (super-frames in, segments out); RSS 12 B in
 # + 4 B out per tuple
@@ -41,9 +45,9 @@ ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673,
               "rss_toeplitz_16M": (1 << 24) * 16}
 
 
-def label(name):
-    for frag, wl in WORKLOADS.items():
-        if frag in name:
+def label(name, grid):
+    for frag, g, wl in WORKLOADS:
+        if frag in name and (g is None or int(grid) == g):
             return wl
     return None
 
@@ -54,7 +58,7 @@ def counters(path):
         return per
     with open(path) as f:
         for r in csv.DictReader(f):
-            wl = label(r["Kernel_Name"])
+            wl = label(r["Kernel_Name"], r.get("Grid_Size", 0))
             if wl:
                 per[wl][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return per
