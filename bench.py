@@ -617,7 +617,7 @@ def frame_extras(torch, csum, dev, timer):
                            int(cols[2][k]) & 0xFFFF, int(cols[3][k]) & 0xFFFF, key, 0)
              for k in range(len(js)))
     ex["rss_toeplitz_16M"] = rate_entry(
-        nt * 16, t, kernel="rss_kernel (12x256 LDS tables)", Mtuples_per_s=round(nt / t / 1e6, 1),
+        nt * 16, t, kernel="rss_kernel<VEC> (4 byte + 16 nibble LDS tables, 4 tuples per thread)", Mtuples_per_s=round(nt / t / 1e6, 1),
         pipeline=pipe_entry(nt * 16, tp), parity="ok" if ok else "MISMATCH",
         traffic=read_traffic("rss_toeplitz_16M"))
     return ex

@@ -124,3 +124,29 @@ def test_gpu_batch_large_vs_host():
         exp = csum.toeplitz(int(arrs["saddr"][j]), int(arrs["daddr"][j]),
                             int(arrs["sport"][j]), int(arrs["dport"][j]), key, 0x5A5A5A5A)
         assert int(got[j]) == exp, j
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,shift", [(1, 0), (3, 0), (4097, 0), (4099, 1), (10001, 2)])
+def test_gpu_batch_tails_and_alignment(n, shift):
+    """The 4-tuples-per-thread path (aligned arrays, n / 4 vector groups plus
+    an n % 4 tail) and the one-tuple path (arrays not 16-B aligned: views
+    starting `shift` elements in), against the host path."""
+    torch = pytest.importorskip("torch")
+    from tulips_amd import csum
+    rng = np.random.default_rng(n + shift)
+    m = n + shift
+    arrs = dict(saddr=rng.integers(0, 2**32, m, dtype=np.uint64).astype(np.uint32),
+                daddr=rng.integers(0, 2**32, m, dtype=np.uint64).astype(np.uint32),
+                sport=rng.integers(0, 65536, m, dtype=np.uint16),
+                dport=rng.integers(0, 65536, m, dtype=np.uint16))
+    key = rng.integers(0, 256, 52, dtype=np.uint8).tobytes()
+    t = {k: torch.from_numpy(v).to("cuda:0")[shift:] for k, v in arrs.items()}
+    out = csum.rss_batch(t["saddr"], t["daddr"], t["sport"], t["dport"], key, 0x1234567)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    for j in range(n):
+        exp = csum.toeplitz(int(arrs["saddr"][shift + j]), int(arrs["daddr"][shift + j]),
+                            int(arrs["sport"][shift + j]), int(arrs["dport"][shift + j]),
+                            key, 0x1234567)
+        assert int(got[j]) == exp, j

@@ -13,7 +13,7 @@
 // already-shifted first byte (Utils.cpp:123-125) and matters for keys shorter
 // than 16 bytes — and the GPU only evaluates
 //   h = init ^ XOR_b T_b[tuple byte b],   T_b[v] = XOR of the windows of v's bits
-// with the 12 x 256 tables built in LDS by each workgroup (12 KiB).
+// with lookup tables built in LDS by each workgroup (rss_kernel).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -81,8 +81,76 @@ rss_host(const RssWindows& w, uint32_t saddr, uint32_t daddr, uint16_t sport,
   return h;
 }
 
-// One workgroup: build T[12][256] in LDS, then hash a grid-stride share of
-// the tuples (structure of arrays, coalesced).
+// One workgroup builds its lookup tables in LDS, then hashes a grid-stride
+// share of the tuples (structure of arrays). The hash is
+//   h = init ^ XOR over tuple bytes b of T_b[byte b]
+// and a lookup costs LDS cycles: a 256-entry table read at 32 random
+// addresses per lane group conflicts ~3.5-way (about 7 cycles per wave
+// instruction instead of 2), while a 16-entry table spans 16 banks and never
+// conflicts but needs two lookups per byte and twice the VALU to form the
+// indices. The 4 port bytes use byte tables, the 8 address bytes nibble
+// tables: LDS 4 x ~7 + 16 x 2 = 60 cycles and ~36 VALU per 64 tuples, where
+// 12 byte lookups cost ~84 LDS cycles (the kernel was LDS-bound).
+//   TB[k][v]: byte tables for tuple bytes 8 + k (k = 0..3), v = 0..255
+//   TN[p][v]: nibble tables for tuple bits 4p..4p+3 (p = 0..15, MSB first)
+struct RssTables
+{
+  uint32_t TB[4][256];
+  uint32_t TN[16][16];
+};
+
+__device__ __forceinline__ void
+build_tables(const RssWindows& win, RssTables& t)
+{
+  for (int e = threadIdx.x; e < 4 * 256; e += blockDim.x) {
+    const int k = e >> 8, v = e & 255;
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x ^= (v & (0x80 >> j)) ? win.w[8 * (8 + k) + j] : 0u;
+    }
+    t.TB[k][v] = x;
+  }
+  for (int e = threadIdx.x; e < 16 * 16; e += blockDim.x) {
+    const int p = e >> 4, v = e & 15;
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x ^= (v & (0x8 >> j)) ? win.w[4 * p + j] : 0u;
+    }
+    t.TN[p][v] = x;
+  }
+}
+
+// Tuple bytes 4a..4a+3 are the little-endian bytes of word x (the reference
+// copies the address words' memory, Utils.cpp:101-104): nibble j of x (bits
+// 4j..4j+3) is the low (j even) or high (j odd) nibble of byte 4a + j/2.
+__device__ __forceinline__ uint32_t
+hash_word(const RssTables& t, uint32_t x, int a)
+{
+  uint32_t h = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = 2 * (4 * a + (j >> 1)) + ((j & 1) ? 0 : 1);
+    h ^= t.TN[p][(x >> (4 * j)) & 15u];
+  }
+  return h;
+}
+
+__device__ __forceinline__ uint32_t
+rss_one(const RssTables& t, uint32_t s, uint32_t d, uint32_t sp, uint32_t dp, uint32_t init)
+{
+  return init ^ hash_word(t, s, 0) ^ hash_word(t, d, 1) ^ t.TB[0][(sp >> 8) & 0xffu] ^
+         t.TB[1][sp & 0xffu] ^ t.TB[2][(dp >> 8) & 0xffu] ^ t.TB[3][dp & 0xffu];
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// VEC: 4 tuples per thread (16-B address / result vectors, 8-B port
+// vectors; the arrays are 16-B / 8-B aligned, n / 4 groups), then the n % 4
+// tail one tuple per thread. Otherwise one tuple per thread throughout.
+template<bool VEC>
 __global__ __launch_bounds__(256) void
 rss_kernel(RssWindows win, const uint32_t* __restrict__ saddr,
            const uint32_t* __restrict__ daddr,
@@ -90,31 +158,29 @@ rss_kernel(RssWindows win, const uint32_t* __restrict__ saddr,
            const uint16_t* __restrict__ dport, uint32_t* __restrict__ out,
            uint32_t n, uint32_t init)
 {
-  __shared__ uint32_t T[12][256];
-  for (int e = threadIdx.x; e < 12 * 256; e += blockDim.x) {
-    const int b = e >> 8, v = e & 255;
-    uint32_t x = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (v & (0x80 >> j)) {
-        x ^= win.w[8 * b + j];
-      }
-    }
-    T[b][v] = x;
-  }
+  __shared__ RssTables t;
+  build_tables(win, t);
   __syncthreads();
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += gridDim.x * blockDim.x) {
-    const uint32_t s = saddr[i], d = daddr[i];
-    const uint32_t sp = sport[i], dp = dport[i];
-    uint32_t h = init;
-    h ^= T[0][s & 0xff] ^ T[1][(s >> 8) & 0xff] ^ T[2][(s >> 16) & 0xff] ^
-         T[3][s >> 24];
-    h ^= T[4][d & 0xff] ^ T[5][(d >> 8) & 0xff] ^ T[6][(d >> 16) & 0xff] ^
-         T[7][d >> 24];
-    h ^= T[8][(sp >> 8) & 0xff] ^ T[9][sp & 0xff] ^ T[10][(dp >> 8) & 0xff] ^
-         T[11][dp & 0xff];
-    out[i] = h;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  uint32_t i0 = 0;
+  if constexpr (VEC) {
+    const uint32_t n4 = n / 4;
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < n4; g += stride) {
+      const u32x4 s = reinterpret_cast<const u32x4*>(saddr)[g];
+      const u32x4 d = reinterpret_cast<const u32x4*>(daddr)[g];
+      const u32x2 sp = reinterpret_cast<const u32x2*>(sport)[g];
+      const u32x2 dp = reinterpret_cast<const u32x2*>(dport)[g];
+      u32x4 h;
+      h.x = rss_one(t, s.x, d.x, sp.x & 0xffffu, dp.x & 0xffffu, init);
+      h.y = rss_one(t, s.y, d.y, sp.x >> 16, dp.x >> 16, init);
+      h.z = rss_one(t, s.z, d.z, sp.y & 0xffffu, dp.y & 0xffffu, init);
+      h.w = rss_one(t, s.w, d.w, sp.y >> 16, dp.y >> 16, init);
+      reinterpret_cast<u32x4*>(out)[g] = h;
+    }
+    i0 = 4 * n4;
+  }
+  for (uint32_t i = i0 + blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    out[i] = rss_one(t, saddr[i], daddr[i], sport[i], dport[i], init);
   }
 }
 
@@ -172,14 +238,25 @@ tulips_rss_toeplitz_batch(const uint32_t* saddr, const uint32_t* daddr,
       !rss_windows(key, key_len, w)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
-  uint64_t blocks = (uint64_t(n) + 255) / 256;
+  const bool vec = ((reinterpret_cast<uintptr_t>(saddr) | reinterpret_cast<uintptr_t>(daddr) |
+                     reinterpret_cast<uintptr_t>(out)) & 15) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(sport) | reinterpret_cast<uintptr_t>(dport)) &
+                    7) == 0;
+  const uint64_t per_thread = vec ? 4 : 1;
+  uint64_t blocks = (uint64_t(n) + 256 * per_thread - 1) / (256 * per_thread);
   if (blocks > 2048) {
     blocks = 2048; // 8 per CU; each builds its LDS tables once
   }
   (void)hipGetLastError();
-  hipLaunchKernelGGL(rss_kernel, dim3(uint32_t(blocks)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), w, saddr, daddr, sport,
-                     dport, out, n, init);
+  if (vec) {
+    hipLaunchKernelGGL(rss_kernel<true>, dim3(uint32_t(blocks)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), w, saddr, daddr, sport, dport, out,
+                       n, init);
+  } else {
+    hipLaunchKernelGGL(rss_kernel<false>, dim3(uint32_t(blocks)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), w, saddr, daddr, sport, dport, out,
+                       n, init);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
 }
