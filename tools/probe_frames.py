@@ -32,9 +32,25 @@ def main():
     flags = torch.empty(nb * nf, dtype=torch.uint8, device=dev)
     burst = nf * slot
     alg = nf * flen
-    ft = csum.lib.tulips_csum_frames_tuned
+    lib = csum.lib
+    if os.environ.get("PROBE_LIB"):
+        # a diagnostic build (e.g. tools/libcsum_nostore.so); the frames are
+        # sealed by the product library first so validation still checks
+        import ctypes as C
+        for i in range(nb):
+            assert csum.lib.tulips_csum_generate_frames(ar.data_ptr() + i * burst,
+                                                         offs.data_ptr(), lens.data_ptr(), nf,
+                                                         None, stream.cuda_stream) == 0
+        torch.cuda.synchronize()
+        lib = C.CDLL(os.path.join(ROOT, os.environ["PROBE_LIB"]))
+        for name, (res, argt) in csum._SIGNATURES.items():
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, argt
+    ft = lib.tulips_csum_frames_tuned
     results = []
     geos = [(16, 4), (16, 6), (16, 8), (8, 8), (8, 16), (32, 4), (64, 2)]
+    if os.environ.get("PROBE_GEOS"):
+        geos = [tuple(int(v) for v in g.split("x")) for g in os.environ["PROBE_GEOS"].split(",")]
     caps = [int(x) for x in os.environ.get("PROBE_CAPS", "0").split(",")]
     blocks = [int(x) for x in os.environ.get("PROBE_BLOCKS", "256").split(",")]
     configs = [(gu, c, b, nt) for gu in geos for c in caps for b in blocks for nt in (1, 0)]
