@@ -628,7 +628,7 @@ def cpu_baseline(arena, batch_bytes, seconds):
     compiled with -O3 -mssse3), else the C restatement, on this box's cores,
     over the first F1500 batch of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from oracle import Oracle, Reference  # noqa: E402 (cpu_baseline leg only)
+    from oracle import REF_CLANG_SO, Oracle, Reference  # noqa: E402 (cpu_baseline leg only)
     if Reference.available():
         impl, kind = Reference(), "reference"
     else:
@@ -640,7 +640,7 @@ def cpu_baseline(arena, batch_bytes, seconds):
         ncpu = os.cpu_count() or 1
     threads = max(1, min(16, ncpu))
 
-    def rate(nt):
+    def rate(nt, impl=impl):
         impl.batch(host, stride=SEG, fixed_len=SEG, n=NSEG, nthreads=nt)
         reps, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < seconds:
@@ -650,11 +650,20 @@ def cpu_baseline(arena, batch_bytes, seconds):
 
     r1, n1 = rate(1)
     rN, nN = rate(threads)
-    return {"value": round(rN, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "value_1core": round(r1, 3),
-            "sample": f"F1500 batch 0 (65,536 x 1500 B = 98.3 MB) copied to host; "
-                      f"{nN} passes on {threads} pinned threads + {n1} passes on 1 "
-                      f"thread, ~{seconds:.1f} s wall each; g++ -O3 -mssse3"}
+    res = {"value": round(rN, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+           "value_1core": round(r1, 3),
+           "sample": f"F1500 batch 0 (65,536 x 1500 B = 98.3 MB) copied to host; "
+                     f"{nN} passes on {threads} pinned threads + {n1} passes on 1 "
+                     f"thread, ~{seconds:.1f} s wall each; g++ -O3 -mssse3"}
+    if kind == "reference" and Reference.available(REF_CLANG_SO):
+        # the same reference sources built with clang, the compiler the
+        # reference's CMake prefers (CMakeLists.txt:20-21)
+        clang = Reference(REF_CLANG_SO)
+        c1, _ = rate(1, clang)
+        cN, _ = rate(threads, clang)
+        res["clang"] = {"value": round(cN, 3), "value_1core": round(c1, 3),
+                        "build": "clang++ (ROCm LLVM) -O3 -mssse3"}
+    return res
 
 
 if __name__ == "__main__":

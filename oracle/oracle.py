@@ -6,8 +6,9 @@ ctypes bindings for the CPU checkers:
   (``oracle/csum_oracle.c``) of the reference checksum path plus the golden
   data generators of SURVEY.md §8c.
 * ``Reference`` -> ``oracle/_ref/libtulips_ref.so``: the reference's own
-  ``src/stack`` sources compiled by ``oracle/Makefile`` (present only where
-  it was built; it travels to the GPU box as a prebuilt ``.so``).
+  ``src/stack`` sources compiled by ``oracle/Makefile`` with g++ (present
+  only where it was built; it travels to the GPU box as a prebuilt ``.so``),
+  or ``libtulips_ref_clang.so``, the same sources built with clang.
 
 Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
 ``cpu_baseline`` leg may import this module, and only as the checker.
@@ -23,6 +24,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libtulips_ref.so")
+REF_CLANG_SO = os.path.join(HERE, "_ref", "libtulips_ref_clang.so")  # same sources, clang
 
 MODE_RAW, MODE_INET, MODE_TCP = 0, 1, 2
 FLAG_COMPLEMENT = 0x100

@@ -8,7 +8,7 @@ where it is present (oracle/_ref/libtulips_ref.so).
 import numpy as np
 import pytest
 
-from oracle import (MODE_INET, MODE_RAW, MODE_TCP, FLAG_COMPLEMENT, Reference,
+from oracle import (MODE_INET, MODE_RAW, MODE_TCP, FLAG_COMPLEMENT, REF_CLANG_SO, Reference,
                     fixed_offsets, ip4, packed_offsets)
 
 
@@ -140,3 +140,19 @@ def test_live_reference_fuzz(oracle):
         d = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
         s = int(rng.integers(0, 65536))
         assert oracle.checksum(s, d) == ref.checksum(s, d)
+
+
+@pytest.mark.skipif(not Reference.available(REF_CLANG_SO), reason="clang build of oracle/_ref absent")
+def test_clang_reference_build_matches_golden(golden):
+    """The clang build of the reference (bench.py's second CPU baseline) gives
+    the reference's results: every known answer and the F1500 digest."""
+    from oracle import Oracle
+    ref, orc = Reference(REF_CLANG_SO), Oracle()
+    for c in golden.kat():
+        if c["fn"] == "checksum":
+            d = golden.kat_data(c, orc)
+            assert ref.checksum(c["seed"], d) == c["expect"], c
+    arena = orc.splitmix_bytes(65536 * 1500)
+    out = ref.batch(arena, stride=1500, fixed_len=1500, n=65536, nthreads=8)
+    gold = golden.digests()["batches"]["F1500"]["fnv1a64"]
+    assert f"{orc.fnv1a_u16(out):016x}" == gold
