@@ -181,3 +181,18 @@ def test_default_tuning():
                                                 0, C.byref(bad), None) == 1
     with pytest.raises(csum.InvalidArgument):
         csum.default_tuning(70000)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: the package without its built .so refuses to import."""
+    import shutil
+    import subprocess
+    import sys
+    pkg = tmp_path / "tulips_amd"
+    pkg.mkdir()
+    for f in ("__init__.py", "csum.py", "shard.py"):
+        shutil.copy(os.path.join(ROOT, "tulips_amd", f), pkg / f)
+    r = subprocess.run([sys.executable, "-c", "import tulips_amd"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "no CPU fallback" in r.stderr
