@@ -15,7 +15,7 @@ HDRS = tulips_amd/csrc/csum_common.h tulips_amd/csrc/csum_launch.h \
        include/tulips_csum.h include/tulips_csum_util.h
 OBJS = $(patsubst tulips_amd/csrc/%.hip,build/%.o,$(SRCS))
 
-.PHONY: all lib oracle clean asm
+.PHONY: all lib oracle clean asm stamps xcd_ab
 
 all: lib oracle
 
@@ -37,6 +37,14 @@ stamps: tools/libcsum_stamps.so
 
 tools/libcsum_stamps.so: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DTULIPS_CSUM_STAMPS -shared -o $@ $(SRCS)
+
+# Diagnostic A/B builds of the XCD cluster size (tools/ab_xcd.sh). Never
+# loaded by the product.
+XCD_AB = 1 2 4 8 32 1024
+xcd_ab: $(foreach c,$(XCD_AB),tools/libcsum_xcd$(c).so)
+
+tools/libcsum_xcd%.so: $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DTULIPS_XCD_CLUSTER=$* -shared -o $@ $(SRCS)
 
 # Device assembly + resource usage of the kernels (for inspection).
 asm:

@@ -98,4 +98,29 @@ TCS_HD uint32_t finish(uint32_t le_partial, bool start_odd, uint32_t mode,
   return r;
 }
 
+#if defined(__HIPCC__)
+#ifndef TULIPS_XCD_CLUSTER
+#define TULIPS_XCD_CLUSTER 8
+#endif
+// Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+// one; MI355X_MICROARCH.md, "Workgroup dispatch, XCD placement"), each with
+// its own L2. Consecutive blocks take consecutive segments, and segments
+// that meet inside a 128-byte line both fetch it. Runs of C consecutive
+// logical blocks are therefore kept on one XCD, while the runs themselves
+// stay dealt over the 8 XCDs (so the chip still streams one address window
+// at a time): hardware block b = 8g + x maps to logical block
+// (g / C) * 8C + x * C + g % C. Blocks of a last, incomplete group of 8C map
+// to themselves. A bijection on [0, nb): results never depend on placement.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
+{
+  constexpr uint32_t C = TULIPS_XCD_CLUSTER;
+  const uint32_t full = (nb / (8u * C)) * (8u * C);
+  if (C <= 1 || b >= full) {
+    return b;
+  }
+  const uint32_t x = b & 7u, g = b >> 3;
+  return (g / C) * (8u * C) + x * C + g % C;
+}
+#endif
+
 }

@@ -227,7 +227,7 @@ csum_kernel(Segs segs, const uint16_t* __restrict__ seeds,
   const int lane = threadIdx.x & (G - 1);
   const uint32_t groups_per_block = blockDim.x / G;
   const uint32_t nsub = gridDim.x * groups_per_block;
-  uint32_t seg = blockIdx.x * groups_per_block + threadIdx.x / G;
+  uint32_t seg = xcd_block(blockIdx.x, gridDim.x) * groups_per_block + threadIdx.x / G;
 #ifdef TULIPS_CSUM_STAMPS
   const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -315,7 +315,7 @@ csum_hybrid_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
   const int lane64 = threadIdx.x & 63;
   const int lane = lane64 & (GS - 1);
   const int sub = lane64 / GS;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t wave = (xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
   const uintptr_t zero_chunk = reinterpret_cast<uintptr_t>(k_zero_chunk);
@@ -501,7 +501,7 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
 {
   static_assert(S >= 1 && S <= 64, "one segment per lane at most");
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t wave = (xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
   const uintptr_t zero_chunk = reinterpret_cast<uintptr_t>(k_zero_chunk);
