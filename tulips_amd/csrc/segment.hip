@@ -512,7 +512,7 @@ segment_kernel(const u32x4* __restrict__ desc, uint32_t mss,
   const int lane = threadIdx.x & (G - 1);
   const uint32_t sub = threadIdx.x / G;
   const uint32_t total = min(first[n], capacity);
-  for (uint32_t jb = blockIdx.x * S; jb < total; jb += gridDim.x * S) {
+  for (uint32_t jb = xcd_block(blockIdx.x, gridDim.x) * S; jb < total; jb += gridDim.x * S) {
     const uint32_t ir = runs[jb / RUN];
     if (threadIdx.x < L) {
       pre[threadIdx.x] = first[min(ir + threadIdx.x, n)];
