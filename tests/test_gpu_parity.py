@@ -23,6 +23,7 @@ DEV = "cuda:0"
 SUB, HYB, PCK = csum.KIND_SUBGROUP, csum.KIND_HYBRID, csum.KIND_PACKED
 # (kind, group, unroll, nontemporal bits, sps)
 GEOMETRIES = [(SUB, g, u, nt, 0) for g in (16, 32, 64) for u in (2, 4, 8) for nt in (0, 1, 3)]
+GEOMETRIES += [(SUB, g, u, 1, 0) for (g, u) in ((16, 6), (32, 3), (64, 9), (64, 12))]
 # hybrid short/long variable-length kernel, with 1/2/4 short segments in flight
 GEOMETRIES += [(HYB, 8, 4, 1, 1), (HYB, 8, 4, 1, 2), (HYB, 8, 4, 0, 4), (HYB, 8, 8, 0, 1),
                (HYB, 16, 2, 0, 1), (HYB, 16, 2, 1, 2), (HYB, 16, 2, 1, 4),

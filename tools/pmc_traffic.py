@@ -29,7 +29,7 @@ from collections import defaultdict
 # 8 per wave = 8,192 waves = 524,288 threads).
 WORKLOADS = [
     ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
-    ("csum_kernel<64, 8, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
+    ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
     ("csum_packed_kernel<8, 4, true, true>", 524288, "ZIPF"),
     ("frame_kernel<false, 16, 6, true>", None, "frames_validate_F1514"),
     ("frame_kernel<true, 16, 6, true>", None, "frames_generate_F1514"),

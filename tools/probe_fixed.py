@@ -26,7 +26,7 @@ def main():
              (32, 3, 512), (16, 6, 1024), (64, 2, 256)]
     for L, nb in ((1500, 16), (9000, 3)):
         if L == 9000:
-            geoms = [(64, 8, 256), (64, 4, 256), (32, 8, 256), (64, 8, 512)]
+            geoms = [(64, 8, 256), (64, 9, 256), (64, 12, 256), (64, 4, 256), (64, 9, 512)]
         bb = N * L
         buf = torch.empty(nb * bb + 256, dtype=torch.uint8, device=dev)
         csum.fill_splitmix(buf, nb * bb)
