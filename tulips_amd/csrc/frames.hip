@@ -63,7 +63,7 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
   const int sub0 = lane64 - lane; // first lane of this subgroup
   const uint32_t per_block = blockDim.x / FG;
   const uint32_t nsub = gridDim.x * per_block;
-  uint32_t f = blockIdx.x * per_block + threadIdx.x / FG;
+  uint32_t f = xcd_block(blockIdx.x, gridDim.x) * per_block + threadIdx.x / FG;
   if (f >= n) {
     return;
   }
