@@ -275,13 +275,47 @@ next_chunk(const u32x4& cur, const u32x4& nxt, int lane, int sub0)
   return r;
 }
 
+// The dword after each lane's chunk: lane l + 1's first dword, the next batch
+// slot's for the subgroup's last lane (lane 0 hands it nxt).
+template<int G>
+__device__ __forceinline__ uint32_t
+next_dword(uint32_t cur, uint32_t nxt, int lane, int sub0)
+{
+  const uint32_t give = lane == 0 ? nxt : cur;
+  if constexpr (G == 16) {
+    // a 16-lane subgroup is one DPP row: row_ror:15 hands lane l the value of
+    // lane (l + 1) mod 16 in one VALU move
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(give), 0x12F, 0xF, 0xF, false));
+  } else {
+    return __shfl(give, sub0 + ((lane + 1) & (G - 1)), 64);
+  }
+}
+
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef const __attribute__((address_space(1))) u32x4_a4* gdw4_ptr;
+
+// A payload chunk whose dwords start past the frame's last aligned chunk is
+// loaded from that chunk instead (reads never leave the 16-byte chunks the
+// frame touches), sel dwords early: move its dwords down. Dwords that would
+// come from beyond that chunk lie past the frame and are never used.
+__device__ __forceinline__ void
+realign(u32x4& d, uint32_t sel)
+{
+  if (sel != 0) {
+    const u32x4 e = d;
+    d.x = sel == 1 ? e.y : (sel == 2 ? e.z : e.w);
+    d.y = sel == 1 ? e.z : e.w;
+    d.z = e.w;
+  }
+}
+
 // Build, checksum and store segment k of frame F as output frame j, on one
 // G-lane subgroup (lane = index in the subgroup, sub0 = its first lane in the
 // wave). Output chunk c holds source bytes [x + 16c, x + 16c + 16), x = the
-// segment's source start: lane l loads ONE aligned source chunk per output
-// chunk (plus one extra for the batch) and takes the following aligned chunk
-// from lane l+1 for the funnel shift, so a batch of SU chunks per lane is
-// SU + 1 loads. The header chunks 0..6 come from one more load per lane and
+// segment's source start: lane l loads the 4 source dwords of each of its
+// output chunks (one dword-aligned 16-byte load) plus one extra for the batch,
+// and takes the fifth dword from lane l+1 for the funnel shift, so a batch of
+// SU chunks per lane is SU + 1 loads. The header chunks 0..6 come from one more load per lane and
 // are parsed through cross-lane shuffles; everything is issued before the
 // first use (the prologue's descriptor is all the addresses need).
 template<int G, int SU>
@@ -289,6 +323,7 @@ __device__ __forceinline__ void
 build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* out,
               uint64_t stride, uint16_t* __restrict__ out_lens, int lane, int sub0)
 {
+  static_assert(G >= 8, "batch slots u > 0 must lie past every header byte");
   const SegInfo& si = F.si;
   const uint32_t slice = si.seg_ok ? min(mss, si.payload - k * mss) : 0u;
   const uint32_t dlen = si.nseg == 1 ? F.flen : si.hlen + slice;
@@ -302,24 +337,36 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
   const uintptr_t dst = reinterpret_cast<uintptr_t>(out) + uintptr_t(j) * stride;
   const int nchunks = int((dlen + 15) >> 4);
   const uintptr_t xs = F.fa + shift;          // source of output byte 0
-  const uintptr_t q0 = xs & ~uintptr_t(15);
-  const uint32_t m = uint32_t(xs & 15);
-  auto src_chunk = [&](int c) {               // aligned source chunk c, clamped
-    uintptr_t q = q0 + 16 * uintptr_t(c);
-    q = q < F.lo ? F.lo : (q > F.hi ? F.hi : q);
-    return load_chunk(q);
+  // Output chunk c is source bytes [xs + 16c, +16): dwords p0 + 16c .. + 20
+  // funnel-shifted by r bytes. Each lane loads the 4 dwords of its chunk at
+  // their (4-byte aligned) address and takes the fifth from lane + 1.
+  const uintptr_t p0 = xs & ~uintptr_t(3);
+  const uint32_t r = uint32_t(xs & 3);
+  auto src_chunk = [&](int c, uint32_t& sel) { // clamped to the last chunk
+    const uintptr_t p = p0 + 16 * uintptr_t(c);
+    const uintptr_t q = p > F.hi ? F.hi : p;   // p >= xs & ~3 >= F.lo
+    sel = uint32_t(p - q) >> 2;
+    return u32x4(*reinterpret_cast<gdw4_ptr>(q));
   };
 
   // ---- batch 0 loads: payload chunks (+1), header chunk --------------------
-  u32x4 A[SU + 1];
+  u32x4 X[SU + 1];
+  uint32_t XS[SU + 1];
+  auto load_batch = [&](int b0) {
 #pragma unroll
-  for (int u = 0; u < SU; ++u) {
-    A[u] = src_chunk(lane + G * u);
-  }
-  A[SU] = src_chunk(lane == 0 ? G * SU : lane + G * (SU - 1));
+    for (int u = 0; u < SU; ++u) {
+      X[u] = src_chunk(b0 + lane + G * u, XS[u]);
+    }
+    X[SU] = src_chunk(lane == 0 ? b0 + G * SU : b0 + lane + G * (SU - 1), XS[SU]);
+  };
   uintptr_t hq = F.lo + 16 * uintptr_t(min(lane, 6));
   hq = hq > F.hi ? F.hi : hq;
-  const u32x4 H = load_chunk(hq);             // frame chunk min(lane, 6)
+  const u32x4 H = load_chunk(hq);             // frame chunk min(lane, 6), first
+  load_batch(0);
+  // every load of the batch is in flight before the header waits for H
+  // (left alone, the scheduler trades that overlap for registers); H is
+  // issued first, so that wait leaves the payload loads outstanding
+  __builtin_amdgcn_sched_barrier(0);
 
   // ---- header fields (chunks 0..4 from lanes 0..4) -------------------------
   uint32_t FW[13];
@@ -351,19 +398,37 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
 
   uint64_t ip_acc = 0, l4_acc = 0;
   u32x4 keep = {0, 0, 0, 0};
-  auto consume = [&](const u32x4 (&X)[SU + 1], int c0) {
+  // first: batch 0, whose slot u = 0 holds output chunks c = lane < G, the
+  // only ones that can touch a header byte (hlen <= 94 < 16 * 16 <= 16 * G);
+  // every other slot is plain payload.
+  auto consume = [&](int c0, bool first) {
+    realign(X[0], XS[0]);
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
-      Win w;
-      w.a = X[u];
-      w.b = next_chunk<G>(X[u], X[u + 1], lane, sub0);
-      w.m = m;
+      realign(X[u + 1], XS[u + 1]);
+      const uint32_t d4 = next_dword<G>(X[u].x, X[u + 1].x, lane, sub0);
       const int c = c0 + G * u;
       if (c >= nchunks) {
         continue;   // (no break: the shuffles above need every lane)
       }
       const int cb = 16 * c;
-      u32x4 v = assemble(w);
+      const u32x4 a = X[u];
+      u32x4 v;
+      v.x = __builtin_amdgcn_alignbyte(a.y, a.x, r);
+      v.y = __builtin_amdgcn_alignbyte(a.z, a.y, r);
+      v.z = __builtin_amdgcn_alignbyte(a.w, a.z, r);
+      v.w = __builtin_amdgcn_alignbyte(d4, a.w, r);
+      if (!(first && u == 0)) {
+        if (uint32_t(cb + 16) > dlen) {
+          v = keep_bytes(v, int(dlen) - cb);
+        }
+        if (l4_on && uint32_t(cb) < tcp_end) {
+          l4_acc += uint32_t(cb + 16) <= tcp_end ? hsum(v)
+                                                  : masked_hsum(v, 0, int(tcp_end) - cb);
+        }
+        *reinterpret_cast<gchunk_wptr>(dst + cb) = v;
+        continue;
+      }
       if (shift != 0 && uint32_t(cb) < si.hlen) {
         v = merge_bytes(assemble(hw), v, int(si.hlen) - cb);
       }
@@ -399,16 +464,14 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
       }
     }
   };
-  consume(A, lane);
   // further batches: jumbo segments only (> G*SU chunks); uniform per subgroup
-  for (int b0 = G * SU; b0 < nchunks; b0 += G * SU) {
-    u32x4 X[SU + 1];
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      X[u] = src_chunk(b0 + lane + G * u);
+  for (int b0 = 0;;) {
+    consume(b0 + lane, b0 == 0);
+    b0 += G * SU;
+    if (b0 >= nchunks) {
+      break;
     }
-    X[SU] = src_chunk(lane == 0 ? b0 + G * SU : b0 + lane + G * (SU - 1));
-    consume(X, b0 + lane);
+    load_batch(b0);
   }
   const uint32_t ip = sub_sum<G>(fold64(ip_acc));
   const uint32_t l4 = sub_sum<G>(fold64(l4_acc));
@@ -526,8 +589,13 @@ segment_kernel(const u32x4* __restrict__ desc, uint32_t mss,
       while (pre[f + 1] <= j) {
         ++f;
       }
+      // (opaque per iteration: keeps LLVM from hoisting ~30 lane-derived
+      // values out of this loop, which nearly always runs once, into VGPRs
+      // that stay live across the whole segment build)
+      int l = lane;
+      asm volatile("" : "+v"(l));
       build_segment<G, SU>(frame_of(dsc[f]), j - pre[f], j, mss, out, stride, out_lens,
-                           lane, int(threadIdx.x & 63) & ~(G - 1));
+                           l, int(threadIdx.x & 63) & ~(G - 1));
     }
     __syncthreads();
   }
