@@ -15,7 +15,7 @@ d = json.load(open(f"gpurun_out/ab_c{C}.json")); e = d["extras"]
 r = lambda k: (e[k]["avg_launch_us"], e[k].get("pipeline", {}).get("us_per_launch"))
 print(f"C={C:>5} F1500 {d['roofline']['avg_launch_us']} {d['roofline']['pipeline']['us_per_launch']}"
       f" F9000 {r('F9000')} ZIPF {r('ZIPF')} seg {r('segment_TSO_64K_mss1460')}"
-      f" val {r('frames_validate_F1514')} gen {r('frames_generate_F1514')}"
+      f" val {r('frames_validate_F1514')} gen {r('frames_generate_F1514')} rss {r('rss_toeplitz_16M')}"
       f" e2e {e['e2e_host_F1500']['pinned']['GiBps']} {e['e2e_host_F1500']['pageable']['GiBps']}")
 PY
 done
