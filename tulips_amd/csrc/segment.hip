@@ -475,8 +475,8 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
       if (l4_on && cb + 16 > 34 && uint32_t(cb) < tcp_end) {
         l4_acc += masked_hsum(v, max(34 - cb, 0), min(int(tcp_end) - cb, 16));
       }
-      if (c == 1 || c == 3) {
-        keep = v;
+      if (c < 4) {
+        keep = v;   // line 0 (chunks 0..3) is stored whole after the sums
       } else {
         store_chunk(dst + cb, v);
       }
@@ -493,18 +493,18 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
   }
   const uint32_t ip = sub_sum<G>(fold64(ip_acc));
   const uint32_t l4 = sub_sum<G>(fold64(l4_acc));
-  if (lane == 1 && nchunks > 1) {
-    if (ip_on) {
+  // lanes 0..3 write the first 64 bytes in one instruction: nontemporal
+  // stores are not merged in L2, and separate stores of chunks 1 and 3 wrote
+  // that line to HBM three times
+  if (lane < 4 && lane < nchunks) {
+    if (lane == 1 && ip_on) {
       keep.z |= ~finish(ip, false, MODE_INET, 0, 0, 0, 20) & 0xffffu;
     }
-    store_chunk(dst + 16, keep);
-  }
-  if (lane == 3 && nchunks > 3) {
-    if (l4_on) {
+    if (lane == 3 && l4_on) {
       const uint32_t r = finish(l4, false, MODE_TCP, 0, h.src, h.dst, total - 20u);
       keep.x |= (~r & 0xffffu) << 16;
     }
-    store_chunk(dst + 48, keep);
+    store_chunk(dst + 16 * uintptr_t(lane), keep);
   }
   if (lane == 0) {
     out_lens[j] = uint16_t(dlen);
