@@ -34,7 +34,10 @@ typedef struct tulips_csum_tuning
   int32_t block;       /* threads per workgroup: 256, 512 or 1024; 0 = default */
   int32_t sps;         /* HYBRID: short segments per subgroup issued together
                           (1, 2, 4); PACKED: 1 = one batch of windows at a
-                          time, 2 = double-buffered; 0 = default */
+                          time, 2 = double-buffered, 3 = double-buffered with
+                          the next group's metadata prefetched (grid-stride;
+                          pays with max_blocks below one group per wave);
+                          0 = default */
 } tulips_csum_tuning;
 
 /* The geometry tulips_csum_batch_fixed / tulips_csum_batch would pick. */

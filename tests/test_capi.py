@@ -173,7 +173,7 @@ def test_default_tuning():
                                                       FAKE, 4, 0, C.byref(bad), None) == 1
     for kind, g, u, s in ((csum.KIND_HYBRID, 16, 3, 1), (csum.KIND_HYBRID, 16, 8, 2),
                           (csum.KIND_PACKED, 8, 8, 1), (csum.KIND_PACKED, 5, 4, 1),
-                          (csum.KIND_PACKED, 64, 2, 1), (csum.KIND_PACKED, 16, 4, 3),
+                          (csum.KIND_PACKED, 64, 2, 1), (csum.KIND_PACKED, 16, 4, 5),
                           (csum.KIND_HYBRID, 12, 4, 1), (csum.KIND_SUBGROUP, 8, 4, 0),
                           (csum.KIND_SUBGROUP, 16, 4, 2), (7, 16, 4, 0)):
         bad = csum.Tuning(kind=kind, group=g, unroll=u, nontemporal=1, sps=s)

@@ -33,6 +33,8 @@ PACKED = [(4, 4), (6, 4), (8, 2), (8, 4), (12, 4), (16, 2), (16, 4), (16, 8), (3
 GEOMETRIES += [(PCK, s, u, nt, 1) for (s, u) in PACKED for nt in (0, 1)]
 # ... and with the double-buffered window loop (sps=2)
 GEOMETRIES += [(PCK, s, u, 1, 2) for (s, u) in PACKED]
+# ... and with the next group's metadata prefetched (sps=3)
+GEOMETRIES += [(PCK, s, u, 1, 3) for (s, u) in PACKED]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -220,7 +222,8 @@ def test_packed_random_vs_oracle(oracle, geo):
     Lengths mix empty, 1..63 B, Zipf-like and up to 65,535 B; any alignment;
     runs of empty segments at wave starts/ends; n not a multiple of the wave's
     segment count; grid-stride (max_blocks) on and off; single- and
-    double-buffered window loops (sps 1/2)."""
+    double-buffered window loops (sps 1/2), the latter with the next
+    group's metadata prefetched (sps 3, several groups per wave when capped)."""
     s_, u_ = geo
     rng = np.random.default_rng(1000 + s_ * 10 + u_)
     arena = rng.integers(0, 256, 2 << 20, dtype=np.uint8)
@@ -248,7 +251,7 @@ def test_packed_random_vs_oracle(oracle, geo):
     for mode in (MODE_RAW, MODE_TCP | FLAG_COMPLEMENT):
         exp = oracle.batch(arena, offs, lens, seeds=seeds, src=src, dst=dst, mode=mode,
                            nthreads=8)
-        for max_blocks, sps in ((0, 1), (5, 1), (0, 2), (5, 2)):
+        for max_blocks, sps in ((0, 1), (5, 1), (0, 2), (5, 2), (0, 3), (5, 3), (37, 3)):
             t = csum.Tuning(kind=PCK, group=s_, unroll=u_, nontemporal=1,
                             max_blocks=max_blocks, sps=sps)
             got = tulips_amd.batch(da, do, dl, seeds=ds_, src=dsrc, dst=ddst, mode=mode,

@@ -168,7 +168,7 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
               (group == 16 && unroll == 8 && spw == 1) ||
               (group == 32 && unroll == 4 && spw == 1));
     case TULIPS_CSUM_KIND_PACKED:
-      return variable && (spw == 1 || spw == 2) &&
+      return variable && (spw == 1 || spw == 2 || spw == 3) &&
              (((group == 4 || group == 6 || group == 12) && unroll == 4) ||
               ((group == 8) && (unroll == 2 || unroll == 4)) ||
               ((group == 16) && (unroll == 2 || unroll == 4 || unroll == 8)) ||

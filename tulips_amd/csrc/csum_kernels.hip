@@ -491,7 +491,19 @@ readlane64(uint64_t v, uint32_t k)
   return (uint64_t(hi) << 32) | lo;
 }
 
-template<int S, int U, bool NT, bool PF>
+// Metadata of one segment (lane k < S of a wave owns segment g0 + k).
+struct SegMeta
+{
+  uint32_t len;
+  uint64_t off;
+  SideIn side;
+};
+
+// PF: 0 = one batch of U windows at a time, 1 = double-buffered windows,
+// 2 = double-buffered + the NEXT group's metadata loaded while this group's
+// first windows are in flight (grid-stride waves; pays once a wave owns more
+// than one group, i.e. with a capped grid).
+template<int S, int U, bool NT, int PF>
 __global__ __launch_bounds__(1024) void
 csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
                    const uint32_t* __restrict__ src,
@@ -508,14 +520,32 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
 #ifdef TULIPS_CSUM_STAMPS
   const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  for (uint32_t g0 = wave * S; g0 < n; g0 += nwaves * S) {
-    // ---- metadata: lane k < S owns segment g0 + k (coalesced loads) ------
+  // metadata: lane k < S owns segment g + k (coalesced loads; lanes past n
+  // re-read segment n - 1 and drop it)
+  auto load_meta = [&](uint32_t g) {
+    const uint32_t sg = g + lane;
+    const bool own = lane < uint32_t(S) && sg < n;
+    const uint32_t sk = own ? sg : n - 1;
+    SegMeta m;
+    m.len = own ? segs.length(sk) : 0u;
+    m.off = segs.off(sk);
+    m.side = load_side(sk, seeds, src, dst, mode);
+    return m;
+  };
+  const uint32_t gstride = nwaves * S;
+  SegMeta meta;
+  if constexpr (PF == 2) {
+    meta = load_meta(wave * S);
+  }
+  for (uint32_t g0 = wave * S; g0 < n; g0 += gstride) {
+    if constexpr (PF != 2) {
+      meta = load_meta(g0);
+    }
     const uint32_t seg = g0 + lane;
     const bool mine = lane < uint32_t(S) && seg < n;
-    const uint32_t sk = mine ? seg : n - 1;
-    const uint32_t len = mine ? segs.length(sk) : 0u;
-    const uintptr_t sa = base + segs.off(sk);
-    const SideIn side = load_side(sk, seeds, src, dst, mode);
+    const uint32_t len = meta.len;
+    const uintptr_t sa = base + meta.off;
+    const SideIn side = meta.side;
     const uintptr_t a0 = sa & ~uintptr_t(15);
     const uint32_t nch = len ? uint32_t((sa + len - a0 + 15) >> 4) : 0u;
     const int head = int(sa - a0);
@@ -590,7 +620,8 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
         run = __builtin_amdgcn_readlane(r, 63);
       }
     };
-    if constexpr (!PF) {
+    SegMeta next;
+    if constexpr (PF == 0) {
       for (uint32_t w0 = 0; w0 < T; w0 += 64u * U) {
         u32x4 v[U];
         issue(w0, v);
@@ -606,6 +637,10 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
       // with nothing newer in flight.
       u32x4 cur[U];
       issue(0, cur);
+      if constexpr (PF == 2) {
+        // behind the first windows: arrives while they are scanned
+        next = load_meta(g0 + gstride);
+      }
       uint32_t w0 = 0;
       for (; w0 + 64u * U < T; w0 += 64u * U) {
         u32x4 nxt[U];
@@ -617,6 +652,8 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
         }
       }
       consume(w0, cur);
+    } else if constexpr (PF == 2) {
+      next = load_meta(g0 + gstride);
     }
     // ---- boundary bytes out, finish --------------------------------------
     const uint32_t outside =
@@ -624,13 +661,16 @@ csum_packed_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
     if (mine) {
       emit_with(seg, sum - outside, sa, len, side, out, bad, mode, nt_store);
     }
+    if constexpr (PF == 2) {
+      meta = next;
+    }
   }
 #ifdef TULIPS_CSUM_STAMPS
   stamp_wave(stamp0);
 #endif
 }
 
-template<int S, int U, bool NT, bool PF>
+template<int S, int U, bool NT, int PF>
 hipError_t
 launch_packed(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
 {
@@ -758,12 +798,16 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
     // spw = 2: double-buffered (next windows in flight while scanning)
 #define TCS_PCASE(S_, U_)                                                      \
   if (a.group == S_ && a.unroll == U_) {                                       \
-    if (a.spw == 2) {                                                          \
-      return a.nontemporal ? launch_packed<S_, U_, true, true>(segs, a, stream) \
-                           : launch_packed<S_, U_, false, true>(segs, a, stream); \
+    if (a.spw == 3) {                                                          \
+      return a.nontemporal ? launch_packed<S_, U_, true, 2>(segs, a, stream)   \
+                           : launch_packed<S_, U_, false, 2>(segs, a, stream); \
     }                                                                          \
-    return a.nontemporal ? launch_packed<S_, U_, true, false>(segs, a, stream) \
-                         : launch_packed<S_, U_, false, false>(segs, a, stream); \
+    if (a.spw == 2) {                                                          \
+      return a.nontemporal ? launch_packed<S_, U_, true, 1>(segs, a, stream)   \
+                           : launch_packed<S_, U_, false, 1>(segs, a, stream); \
+    }                                                                          \
+    return a.nontemporal ? launch_packed<S_, U_, true, 0>(segs, a, stream)     \
+                         : launch_packed<S_, U_, false, 0>(segs, a, stream);   \
   }
     TCS_PCASE(4, 4)
     TCS_PCASE(6, 4)

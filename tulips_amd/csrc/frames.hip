@@ -52,8 +52,20 @@ using namespace frame;
 // (4 frames per wave, 96 chunks = a 1514 B frame in one batch, nt loads), is
 // the best of tools/probe_frames.py's sweep on 1514 B frames
 // (profiles/probe_frames_r01.json).
+// Minimum waves per SIMD the register allocator must leave room for
+// (0 = no bound; diagnostic A/B builds override them). Generation: 94 -> 80
+// VGPRs, 5 -> 6 waves/SIMD, no spill; 3 alternations on one box
+// (profiles/ab_r01.txt): 21.2-22.0 -> 20.8-21.4 us serial, 19.4-19.7 ->
+// 18.7-19.0 us on 4 branches. Validation at 7 waves spills 12 B and is slower.
+#ifndef TULIPS_FRAME_VAL_WAVES
+#define TULIPS_FRAME_VAL_WAVES 0
+#endif
+#ifndef TULIPS_FRAME_GEN_WAVES
+#define TULIPS_FRAME_GEN_WAVES 6
+#endif
+
 template<bool GENERATE, int FG, int FU, bool NT>
-__global__ __launch_bounds__(1024) void
+__global__ __launch_bounds__(1024, GENERATE ? TULIPS_FRAME_GEN_WAVES : TULIPS_FRAME_VAL_WAVES) void
 frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ counters)
