@@ -30,7 +30,7 @@ from collections import defaultdict
 WORKLOADS = [
     ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
     ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
-    ("csum_packed_kernel<8, 4, true, true>", 524288, "ZIPF"),
+    ("csum_packed_kernel<8, 4, true, 1>", 524288, "ZIPF"),  # PF = 1: double-buffered
     ("frame_kernel<false, 16, 6, true>", None, "frames_validate_F1514"),
     ("frame_kernel<true, 16, 6, true>", None, "frames_generate_F1514"),
     ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
