@@ -191,6 +191,9 @@ int tulips_rss_toeplitz_batch(const uint32_t* saddr, const uint32_t* daddr,
  * NULL) and, when `counters` (device uint32[4], may be NULL) is given, zeroes
  * it and counts { IPv4 frames, bad IP checksums, TCP frames, TCP frames
  * without L4_CSUM_OK }. At least one of flags / counters is required.
+ * Counting uses a small per-(device, stream) workspace made on the stream's
+ * first counting call; made inside a stream capture, that call returns
+ * InvalidArgument (count once on the stream before capturing).
  */
 int tulips_csum_validate_frames(const uint8_t* base, const uint64_t* offsets,
                                 const uint16_t* lengths, uint32_t n,

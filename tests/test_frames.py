@@ -135,6 +135,38 @@ def test_gpu_fixture():
 
 
 @pytest.mark.gpu
+def test_gpu_counters_repeat_streams_and_grid_caps():
+    """Counters are summed per block into per-stream shards and finalised
+    after the launch: back-to-back calls on one stream (the shards must come
+    back zeroed), two streams at once, and capped grids (many frames per
+    block) all give the oracle's totals."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    exp = counters_of(fx["expect"])
+    a, o, l = _dev(fx["arena"], fx["offsets"].astype(np.int64), fx["lengths"].view(np.int16))
+    n = len(fx["offsets"])
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    cnts = [torch.full((4,), -1, dtype=torch.int32, device="cuda:0") for _ in range(6)]
+    torch.cuda.synchronize()
+    for k, c in enumerate(cnts):
+        st = (s1 if k % 2 else s2).cuda_stream
+        assert csum.lib.tulips_csum_validate_frames(a.data_ptr(), o.data_ptr(), l.data_ptr(),
+                                                    n, None, c.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    for c in cnts:
+        np.testing.assert_array_equal(c.cpu().numpy().view(np.uint32), exp)
+    st = torch.cuda.current_stream().cuda_stream
+    for cap, blk in ((1, 256), (3, 1024), (40, 256), (0, 512)):
+        t = csum.Tuning(group=16, unroll=6, nontemporal=1, max_blocks=cap, block=blk)
+        c = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
+        assert csum.lib.tulips_csum_frames_tuned(0, a.data_ptr(), o.data_ptr(), l.data_ptr(),
+                                                 n, None, c.data_ptr(), t, st) == 0
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(c.cpu().numpy().view(np.uint32), exp, err_msg=f"{cap} {blk}")
+
+
+@pytest.mark.gpu
 def test_gpu_counters_only():
     import torch
     from tulips_amd import csum

@@ -461,9 +461,6 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
                            hipMemcpyHostToDevice, st));
     }
     if (job.frames) {
-      if (job.counters) {
-        TCS_Q(hipMemsetAsync(s.d_cnt, 0, 16, st));
-      }
       TCS_Q(launch_frames(dbase, s.d_offs, s.d_lens, cnt,
                           reinterpret_cast<uint8_t*>(s.d_out),
                           job.counters ? s.d_cnt : nullptr, st));
