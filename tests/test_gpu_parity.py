@@ -309,6 +309,42 @@ def test_generate_then_verify_roundtrip_and_corruption(oracle):
     np.testing.assert_array_equal(o, exp)
 
 
+def test_verify_all_bad_repeat_and_two_streams(oracle):
+    """The bad count is added per block into per-stream counter shards and
+    summed by a finalize launch: an all-bad burst (random bytes) counts every
+    segment, back-to-back calls on one stream each see zeroed shards, calls
+    on two streams keep separate shards, and n = 0 writes 0."""
+    rng = np.random.default_rng(7)
+    n, L = 65536, 1500
+    arena = d(rng.integers(0, 256, n * L, dtype=np.uint8))
+    offs = d(fixed_offsets(n, L))
+    lens = d(np.full(n, L, np.uint16))
+    exp = oracle.batch(h(arena), fixed_offsets(n, L), np.full(n, L, np.uint16),
+                       mode=MODE_INET, nthreads=8)
+    want = int(np.count_nonzero(exp != 0xFFFF))
+    assert want > n - 10
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    cnts = [torch.full((1,), -1, dtype=torch.int32, device=DEV) for _ in range(6)]
+    torch.cuda.synchronize()
+    for k, c in enumerate(cnts):
+        st = (s1 if k % 2 else s2).cuda_stream
+        sub = n if k < 4 else 1000 * k
+        assert csum.lib.tulips_csum_verify(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                           None, None, None, c.data_ptr(), sub,
+                                           MODE_INET, st) == 0
+    torch.cuda.synchronize()
+    got = [int(h(c)[0]) for c in cnts]
+    assert got[:4] == [want] * 4
+    assert got[4] == int(np.count_nonzero(exp[:4000] != 0xFFFF))
+    assert got[5] == int(np.count_nonzero(exp[:5000] != 0xFFFF))
+    c = torch.full((1,), -1, dtype=torch.int32, device=DEV)
+    assert csum.lib.tulips_csum_verify(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                       None, None, None, c.data_ptr(), 0, MODE_INET,
+                                       torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert int(h(c)[0]) == 0
+
+
 def test_ipv4_headers_batch(oracle):
     rng = np.random.default_rng(4)
     n = 10000

@@ -344,13 +344,20 @@ tulips_csum_verify(const uint8_t* base, const uint64_t* offsets,
   if (!bad_count || (m != TULIPS_CSUM_INET && m != TULIPS_CSUM_TCP)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
-  const hipError_t e = hipMemsetAsync(bad_count, 0, sizeof(uint32_t),
-                                      static_cast<hipStream_t>(stream));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  uint32_t* shards = nullptr;
+  hipError_t e = counter_shards(st, &shards);
   if (e != hipSuccess) {
-    return status_of(e);
+    return e == hipErrorStreamCaptureUnsupported ? TULIPS_STATUS_INVALID_ARGUMENT
+                                                 : status_of(e);
   }
-  return batch_var(base, offsets, lengths, nullptr, src, dst, out, bad_count,
-                   n, mode, nullptr, stream);
+  const int rc = batch_var(base, offsets, lengths, nullptr, src, dst, out, shards,
+                           n, mode, nullptr, stream);
+  if (rc != TULIPS_STATUS_OK) {
+    return rc;
+  }
+  // bad_count = the shards' sum (0 for n == 0), shards zeroed again
+  return status_of(launch_counters_finalize(shards, bad_count, 1, st));
 }
 
 int

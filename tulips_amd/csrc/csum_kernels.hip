@@ -283,7 +283,9 @@ emit_with(uint32_t seg, uint32_t part, uintptr_t sa, uint32_t len, SideIn in,
     }
   }
   if (bad && (r ^ ((mode & FLAG_COMPLEMENT) ? 0u : 0xffffu)) != 0) {
-    atomicAdd(bad, 1u);
+    // this block's counter shard (csum_launch.h): a verify of an all-bad
+    // burst otherwise serialises one same-address atomic per wave
+    atomicAdd(bad + CNT_LINE * (blockIdx.x % CNT_SHARDS), 1u);
   }
 }
 

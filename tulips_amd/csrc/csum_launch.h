@@ -13,7 +13,8 @@ struct LaunchArgs
   const uint32_t* src;   // TCP only
   const uint32_t* dst;   // TCP only
   uint16_t* out;         // nullable when only counting
-  uint32_t* bad;         // nullable: count of results != 0xffff
+  uint32_t* bad;         // nullable: counter shards (counter_shards) that
+                         // results != 0xffff are counted into
   uint32_t n;
   uint32_t mode;
   int kind;              // TULIPS_CSUM_KIND_* (never DEFAULT here)
@@ -25,6 +26,17 @@ struct LaunchArgs
   int block;             // threads per workgroup: 256, 512, 1024 (0 = 256)
   int spw;               // hybrid: short segments per subgroup in flight
 };
+
+// Counter shards (frames.hip): CNT_SHARDS zeroed 128-B lines per (device,
+// stream), counter k of a block's shard at shards[CNT_LINE * shard + k].
+// Kernels add per-block totals to their shard; launch_counters_finalize
+// writes the sums of counters 0..nout-1 to `out` and zeroes the shards again.
+// Spreading the adds keeps same-address device atomics (~11 ns each,
+// serialised) off the critical path.
+constexpr uint32_t CNT_SHARDS = 32, CNT_LINE = 32;
+hipError_t counter_shards(hipStream_t stream, uint32_t** out);
+hipError_t launch_counters_finalize(uint32_t* shards, uint32_t* out, uint32_t nout,
+                                    hipStream_t stream);
 
 hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,
                         const LaunchArgs& a, hipStream_t stream);

@@ -40,8 +40,6 @@ namespace {
 
 using namespace frame;
 
-// Counter shards: CNT_SHARDS lines of 128 B, counters in the first 4 words.
-constexpr uint32_t CNT_SHARDS = 32, CNT_LINE = 32;
 
 // One G-lane subgroup per frame (two frames per wave), frames taken in
 // grid-stride order. The whole frame is loaded (load_frame) as soon as its
@@ -181,7 +179,8 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
 // call on this stream (atomic exchange: read and cleared where the adds
 // landed).
 __global__ __launch_bounds__(64) void
-frame_counters_finalize(uint32_t* __restrict__ shards, uint32_t* __restrict__ counters)
+frame_counters_finalize(uint32_t* __restrict__ shards, uint32_t* __restrict__ counters,
+                        uint32_t nout)
 {
   // lane l takes counter l & 3 of shards l >> 2 and (l >> 2) + 16: all 128
   // exchanges in flight at once, then a sum over the lanes of each counter
@@ -194,7 +193,7 @@ frame_counters_finalize(uint32_t* __restrict__ shards, uint32_t* __restrict__ co
   for (int m = 4; m < 64; m <<= 1) {
     sum += __shfl_xor(sum, m);
   }
-  if (l < 4) {
+  if (l < nout) {
     counters[k] = sum;
   }
 }
@@ -259,14 +258,14 @@ frame_geometry_ok(int group, int unroll, uint32_t block)
 }
 
 namespace {
+std::mutex g_cnt_mutex;
+std::map<std::pair<int, hipStream_t>, uint32_t*> g_cnt;
+} // namespace
 
 // Zeroed counter shards per (device, stream): calls on one stream run in
 // order and leave them zeroed; calls on different streams may overlap, so
 // each stream gets its own. Made on first use, which cannot happen inside a
 // stream capture (warm the stream up outside it).
-std::mutex g_cnt_mutex;
-std::map<std::pair<int, hipStream_t>, uint32_t*> g_cnt;
-
 hipError_t
 counter_shards(hipStream_t stream, uint32_t** out)
 {
@@ -298,7 +297,14 @@ counter_shards(hipStream_t stream, uint32_t** out)
   return hipSuccess;
 }
 
-} // namespace
+hipError_t
+launch_counters_finalize(uint32_t* shards, uint32_t* out, uint32_t nout,
+                         hipStream_t stream)
+{
+  hipLaunchKernelGGL(frame_counters_finalize, dim3(1), dim3(64), 0, stream, shards,
+                     out, nout);
+  return hipGetLastError();
+}
 
 // counters (device uint32[4], may be null) are overwritten with this call's
 // totals, in stream order.
@@ -322,9 +328,7 @@ launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
   if (e != hipSuccess || !counters) {
     return e;
   }
-  hipLaunchKernelGGL(frame_counters_finalize, dim3(1), dim3(64), 0, stream, shards,
-                     counters);
-  return hipGetLastError();
+  return launch_counters_finalize(shards, counters, 4, stream);
 }
 
 hipError_t
