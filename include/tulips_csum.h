@@ -188,12 +188,13 @@ int tulips_rss_toeplitz_batch(const uint32_t* saddr, const uint32_t* daddr,
 /*
  * Frame i is base[offsets[i] .. offsets[i] + lengths[i]) (device pointers;
  * a frame is read only within its length). Writes flags[i] (uint8, may be
- * NULL) and, when `counters` (device uint32[4], may be NULL) is given, zeroes
- * it and counts { IPv4 frames, bad IP checksums, TCP frames, TCP frames
- * without L4_CSUM_OK }. At least one of flags / counters is required.
- * Counting uses a small per-(device, stream) workspace made on the stream's
- * first counting call; made inside a stream capture, that call returns
- * InvalidArgument (count once on the stream before capturing).
+ * NULL) and, when `counters` (device uint32[4], may be NULL) is given,
+ * overwrites it with this call's counts { IPv4 frames, bad IP checksums, TCP
+ * frames, TCP frames without L4_CSUM_OK } (zeros for n == 0). At least one of
+ * flags / counters is required for n > 0. Counting uses the per-stream state
+ * below, made on the stream's first counting call; made inside a stream
+ * capture, that call returns InvalidArgument (count once on the stream before
+ * capturing).
  */
 int tulips_csum_validate_frames(const uint8_t* base, const uint64_t* offsets,
                                 const uint16_t* lengths, uint32_t n,
@@ -257,6 +258,24 @@ int tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
                                      const uint64_t* offsets,
                                      const uint16_t* lengths, uint32_t n,
                                      uint8_t* flags, uint32_t* counters);
+
+/* ---- per-stream state ---------------------------------------------------- */
+/*
+ * Counting calls (tulips_csum_verify, tulips_csum_validate_frames with
+ * counters) and tulips_csum_segment_frames keep a small device workspace per
+ * (device, stream), on the stream's own device. A call holds the stream's lock
+ * from its first launch to its last, so host threads sharing a stream (e.g.
+ * the NULL stream) never interleave their launch sequences. A counting call
+ * captured in a HIP graph gets counter shards of its own, owned by the graph
+ * (up to 16 per stream; count once on the stream before capturing).
+ *
+ * tulips_csum_release_stream waits for `stream` and frees everything the
+ * library holds for it, including shards owned by graphs captured on it
+ * (destroy those graphs first). Call it before hipStreamDestroy; it must not
+ * race calls on the same stream. Later calls on the stream start afresh.
+ * tulips_csum_ctx_destroy releases the context's own streams.
+ */
+int tulips_csum_release_stream(void* stream);
 
 /* ---- misc ---------------------------------------------------------------- */
 

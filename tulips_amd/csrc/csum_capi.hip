@@ -7,6 +7,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -14,6 +16,7 @@
 #include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
+#include "stream_state.h"
 
 using namespace tulips_amd;
 
@@ -345,19 +348,32 @@ tulips_csum_verify(const uint8_t* base, const uint64_t* offsets,
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  uint32_t* shards = nullptr;
-  hipError_t e = counter_shards(st, &shards);
+  if (n && (!base || !offsets || !lengths || !mode_ok(mode, src, dst))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  std::shared_ptr<StreamState> ss;
+  hipError_t e = stream_state(st, &ss);
   if (e != hipSuccess) {
+    return status_of(e);
+  }
+  // count kernel + finalize queued as one sequence (stream_state.h)
+  const bool capturing = stream_capturing(st);
+  std::lock_guard<std::mutex> g(ss->call);
+  uint32_t* shards = nullptr;
+  if ((e = call_shards(*ss, capturing, &shards)) != hipSuccess) {
     return e == hipErrorStreamCaptureUnsupported ? TULIPS_STATUS_INVALID_ARGUMENT
                                                  : status_of(e);
   }
-  const int rc = batch_var(base, offsets, lengths, nullptr, src, dst, out, shards,
-                           n, mode, nullptr, stream);
-  if (rc != TULIPS_STATUS_OK) {
-    return rc;
+  int rc = batch_var(base, offsets, lengths, nullptr, src, dst, out, shards, n, mode,
+                     nullptr, stream);
+  if (rc == TULIPS_STATUS_OK) {
+    // bad_count = the shards' sum (0 for n == 0), shards zeroed again
+    rc = status_of(launch_counters_finalize(shards, bad_count, 1, st));
   }
-  // bad_count = the shards' sum (0 for n == 0), shards zeroed again
-  return status_of(launch_counters_finalize(shards, bad_count, 1, st));
+  if (rc != TULIPS_STATUS_OK && !capturing) {
+    drop_shards(*ss, shards);
+  }
+  return rc;
 }
 
 int

@@ -217,6 +217,7 @@ free_slot(Slot& s)
     (void)hipEventDestroy(s.done);
   }
   if (s.stream) {
+    (void)tulips_csum_release_stream(s.stream); // counter shards of the slot
     (void)hipStreamDestroy(s.stream);
   }
   s = Slot();

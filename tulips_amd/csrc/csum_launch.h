@@ -13,7 +13,7 @@ struct LaunchArgs
   const uint32_t* src;   // TCP only
   const uint32_t* dst;   // TCP only
   uint16_t* out;         // nullable when only counting
-  uint32_t* bad;         // nullable: counter shards (counter_shards) that
+  uint32_t* bad;         // nullable: counter shards (stream_state.h) that
                          // results != 0xffff are counted into
   uint32_t n;
   uint32_t mode;
@@ -27,14 +27,14 @@ struct LaunchArgs
   int spw;               // hybrid: short segments per subgroup in flight
 };
 
-// Counter shards (frames.hip): CNT_SHARDS zeroed 128-B lines per (device,
+// Counter shards: CNT_SHARDS zeroed 128-B lines per (device,
 // stream), counter k of a block's shard at shards[CNT_LINE * shard + k].
 // Kernels add per-block totals to their shard; launch_counters_finalize
 // writes the sums of counters 0..nout-1 to `out` and zeroes the shards again.
 // Spreading the adds keeps same-address device atomics (~11 ns each,
 // serialised) off the critical path.
+// The shards come from the stream's state (stream_state.h call_shards).
 constexpr uint32_t CNT_SHARDS = 32, CNT_LINE = 32;
-hipError_t counter_shards(hipStream_t stream, uint32_t** out);
 hipError_t launch_counters_finalize(uint32_t* shards, uint32_t* out, uint32_t nout,
                                     hipStream_t stream);
 

@@ -25,15 +25,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <map>
+#include <memory>
 #include <mutex>
-#include <utility>
 
 #include "../../include/tulips_csum.h"
 #include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
 #include "frame_common.h"
+#include "stream_state.h"
 
 namespace tulips_amd {
 namespace {
@@ -257,46 +257,6 @@ frame_geometry_ok(int group, int unroll, uint32_t block)
   return geo && (block == 0 || block == 256 || block == 512 || block == 1024);
 }
 
-namespace {
-std::mutex g_cnt_mutex;
-std::map<std::pair<int, hipStream_t>, uint32_t*> g_cnt;
-} // namespace
-
-// Zeroed counter shards per (device, stream): calls on one stream run in
-// order and leave them zeroed; calls on different streams may overlap, so
-// each stream gets its own. Made on first use, which cannot happen inside a
-// stream capture (warm the stream up outside it).
-hipError_t
-counter_shards(hipStream_t stream, uint32_t** out)
-{
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) {
-    return e;
-  }
-  std::lock_guard<std::mutex> g(g_cnt_mutex);
-  uint32_t*& p = g_cnt[std::make_pair(dev, stream)];
-  if (!p) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(stream, &cs);
-    if (cs != hipStreamCaptureStatusNone) {
-      return hipErrorStreamCaptureUnsupported;
-    }
-    const size_t bytes = sizeof(uint32_t) * CNT_LINE * CNT_SHARDS;
-    uint32_t* q = nullptr;
-    if ((e = hipMalloc(reinterpret_cast<void**>(&q), bytes)) != hipSuccess) {
-      return e;
-    }
-    if ((e = hipMemsetAsync(q, 0, bytes, stream)) != hipSuccess) {
-      (void)hipFree(q);
-      return e;
-    }
-    p = q;
-  }
-  *out = p;
-  return hipSuccess;
-}
-
 hipError_t
 launch_counters_finalize(uint32_t* shards, uint32_t* out, uint32_t nout,
                          hipStream_t stream)
@@ -307,28 +267,41 @@ launch_counters_finalize(uint32_t* shards, uint32_t* out, uint32_t nout,
 }
 
 // counters (device uint32[4], may be null) are overwritten with this call's
-// totals, in stream order.
+// totals, in stream order (zeroed for n == 0). The count kernel and the
+// finalize are queued under the stream's call mutex (stream_state.h).
 hipError_t
 launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
               uint32_t n, uint8_t* flags, uint32_t* counters, hipStream_t stream,
               const FrameLaunch& fl)
 {
   if (n == 0) {
-    return hipSuccess;
+    return counters ? hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), stream)
+                    : hipSuccess;
   }
-  uint32_t* shards = nullptr;
-  if (counters) {
-    const hipError_t e = counter_shards(stream, &shards);
-    if (e != hipSuccess) {
-      return e;
-    }
+  if (!counters) {
+    return dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n, flags, nullptr,
+                           fl, stream);
   }
-  const hipError_t e = dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n,
-                                       flags, shards, fl, stream);
-  if (e != hipSuccess || !counters) {
+  std::shared_ptr<StreamState> ss;
+  hipError_t e = stream_state(stream, &ss);
+  if (e != hipSuccess) {
     return e;
   }
-  return launch_counters_finalize(shards, counters, 4, stream);
+  const bool capturing = stream_capturing(stream);
+  std::lock_guard<std::mutex> g(ss->call);
+  uint32_t* shards = nullptr;
+  if ((e = call_shards(*ss, capturing, &shards)) != hipSuccess) {
+    return e;
+  }
+  e = dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n, flags, shards, fl,
+                      stream);
+  if (e == hipSuccess) {
+    e = launch_counters_finalize(shards, counters, 4, stream);
+  }
+  if (e != hipSuccess && !capturing) {
+    drop_shards(*ss, shards);
+  }
+  return e;
 }
 
 hipError_t
@@ -349,7 +322,11 @@ tulips_csum_validate_frames(const uint8_t* base, const uint64_t* offsets,
                             uint32_t* counters, void* stream)
 {
   if (n == 0) {
-    return TULIPS_STATUS_OK;
+    // counters are still this call's totals (zero), like tulips_csum_verify
+    return !counters || hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t),
+                                       static_cast<hipStream_t>(stream)) == hipSuccess
+             ? TULIPS_STATUS_OK
+             : TULIPS_STATUS_HARDWARE_ERROR;
   }
   if (!base || !offsets || !lengths || (!flags && !counters)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
@@ -389,10 +366,10 @@ tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
                                      uint32_t(tuning->block < 0 ? 0 : tuning->block))) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
-  if (n == 0) {
+  if (n == 0 && !(op == 0 && counters)) {
     return TULIPS_STATUS_OK;
   }
-  if (!base || !offsets || !lengths || (op == 0 && !flags && !counters)) {
+  if (n && (!base || !offsets || !lengths || (op == 0 && !flags && !counters))) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   tulips_amd::FrameLaunch fl;

@@ -33,13 +33,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <map>
+#include <memory>
 #include <mutex>
-#include <utility>
 
 #include "../../include/tulips_csum.h"
 #include "csum_common.h"
 #include "frame_common.h"
+#include "stream_state.h"
 
 namespace tulips_amd {
 namespace {
@@ -619,84 +619,63 @@ segment_kernel(const u32x4* __restrict__ desc, uint32_t mss,
   }
 }
 
-// Workspace per (device, stream): the scan's block totals (MAX_FRAMES / CB
-// words), the run starts (one word per RUN output segments) and the frame
-// descriptors (16 bytes per input frame). Calls on one stream run in order,
-// so they can share one; calls on different streams may overlap, so each
-// stream gets its own. Made on first use and grown when a call's capacity
-// needs a longer map; a call that grows it cannot be captured in a HIP graph
-// (warm it up outside the capture).
-struct Workspace
-{
-  uint32_t* blocks = nullptr;
-  uint32_t* runs = nullptr;
-  uint64_t nruns = 0;
-  u32x4* desc = nullptr;
-  uint64_t ndesc = 0;
-};
-std::mutex g_ws_mutex;
-std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
-
+// Workspace per (device, stream) (stream_state.h): the scan's block totals
+// (MAX_FRAMES / CB words), the run starts (one word per RUN output segments)
+// and the frame descriptors (16 bytes per input frame). Calls on one stream
+// run in order, so they can share one; calls on different streams may
+// overlap, so each stream gets its own. Made on first use and grown when a
+// call's capacity needs a longer map; a call that grows it cannot be captured
+// in a HIP graph (warm it up outside the capture). The caller holds the
+// stream's call mutex.
 hipError_t
-workspace(hipStream_t stream, uint32_t capacity, uint32_t n, uint32_t** blocks,
-          uint32_t** runs, u32x4** desc)
+workspace(StreamState& w, bool capturing, uint32_t capacity, uint32_t n,
+          uint32_t** blocks, uint32_t** runs, u32x4** desc)
 {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) {
-    return e;
-  }
-  // making or growing a workspace (hipMalloc, a stream sync) cannot happen
-  // inside a stream capture: such a call fails with InvalidArgument
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  (void)hipStreamIsCapturing(stream, &cs);
-  const bool capturing = cs != hipStreamCaptureStatusNone;
-  std::lock_guard<std::mutex> g(g_ws_mutex);
-  Workspace& w = g_ws[std::make_pair(dev, stream)];
   const uint64_t need = (uint64_t(capacity) + RUN - 1) / RUN;
   if (capturing &&
-      (!w.blocks || need > w.nruns || (capacity && uint64_t(n) > w.ndesc))) {
+      (!w.seg_blocks || need > w.seg_nruns || (capacity && uint64_t(n) > w.seg_ndesc))) {
     return hipErrorStreamCaptureUnsupported;
   }
-  if (!w.blocks) {
-    e = hipMalloc(reinterpret_cast<void**>(&w.blocks),
-                  sizeof(uint32_t) * (MAX_FRAMES / CB));
+  hipError_t e;
+  if (!w.seg_blocks) {
+    void* p = nullptr;
+    e = device_malloc(w.device, &p, sizeof(uint32_t) * (MAX_FRAMES / CB));
     if (e != hipSuccess) {
-      w.blocks = nullptr;
       return e;
     }
+    w.seg_blocks = static_cast<uint32_t*>(p);
   }
-  if (need > w.nruns) {
+  if (need > w.seg_nruns) {
     const uint64_t want = need < 65536 ? 65536 : need;
-    uint32_t* p = nullptr;
-    e = hipMalloc(reinterpret_cast<void**>(&p), sizeof(uint32_t) * want);
+    void* p = nullptr;
+    e = device_malloc(w.device, &p, sizeof(uint32_t) * want);
     if (e != hipSuccess) {
       return e;
     }
-    if (w.runs) {
-      (void)hipStreamSynchronize(stream); // the old array may still be in use
-      (void)hipFree(w.runs);
+    if (w.seg_runs) {
+      (void)hipStreamSynchronize(w.stream); // the old array may still be in use
+      (void)hipFree(w.seg_runs);
     }
-    w.runs = p;
-    w.nruns = want;
+    w.seg_runs = static_cast<uint32_t*>(p);
+    w.seg_nruns = want;
   }
-  if (capacity && uint64_t(n) > w.ndesc) {
+  if (capacity && uint64_t(n) > w.seg_ndesc) {
     const uint64_t want = n < 65536 ? 65536 : uint64_t(n);
-    u32x4* p = nullptr;
-    e = hipMalloc(reinterpret_cast<void**>(&p), sizeof(u32x4) * want);
+    void* p = nullptr;
+    e = device_malloc(w.device, &p, sizeof(u32x4) * want);
     if (e != hipSuccess) {
       return e;
     }
-    if (w.desc) {
-      (void)hipStreamSynchronize(stream); // the old array may still be in use
-      (void)hipFree(w.desc);
+    if (w.seg_desc) {
+      (void)hipStreamSynchronize(w.stream); // the old array may still be in use
+      (void)hipFree(w.seg_desc);
     }
-    w.desc = p;
-    w.ndesc = want;
+    w.seg_desc = p;
+    w.seg_ndesc = want;
   }
-  *blocks = w.blocks;
-  *runs = w.runs;
-  *desc = w.desc;
+  *blocks = w.seg_blocks;
+  *runs = w.seg_runs;
+  *desc = static_cast<u32x4*>(w.seg_desc);
   return hipSuccess;
 }
 
@@ -726,10 +705,18 @@ tulips_csum_segment_frames(const uint8_t* in_base, const uint64_t* in_offsets,
                         out_stride < 16 || (out_stride & 15)))) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
+  std::shared_ptr<StreamState> ss;
+  hipError_t e = stream_state(st, &ss);
+  if (e != hipSuccess) {
+    return TULIPS_STATUS_HARDWARE_ERROR;
+  }
+  // the prologue and the segment kernel share the stream's workspace: queue
+  // them as one sequence (stream_state.h)
+  std::lock_guard<std::mutex> g(ss->call);
   uint32_t* ws = nullptr;
   uint32_t* runs = nullptr;
   u32x4* desc = nullptr;
-  hipError_t e = workspace(st, out_capacity, n, &ws, &runs, &desc);
+  e = workspace(*ss, stream_capturing(st), out_capacity, n, &ws, &runs, &desc);
   if (e != hipSuccess) {
     return e == hipErrorOutOfMemory                ? TULIPS_STATUS_NO_MORE_RESOURCES
            : e == hipErrorStreamCaptureUnsupported ? TULIPS_STATUS_INVALID_ARGUMENT

@@ -1,0 +1,73 @@
+// stream_state.h — the library's per-(device, stream) state: counter shards
+// for the counting calls (verify, counted frame validation) and the
+// segmentation workspace.
+//
+// Rules (include/tulips_csum.h):
+//  * A call that uses the state holds the stream's `call` mutex from its
+//    first launch through its last, so two host threads issuing counting or
+//    segmentation calls on the same stream (e.g. the legacy NULL stream) get
+//    their launches queued as whole sequences, never interleaved.
+//  * The device is the stream's own (hipStreamGetDevice), not the calling
+//    thread's current device; state is allocated on that device.
+//  * A counting call captured in a HIP graph gets shards of its own (taken
+//    from a spare set made with the stream's direct shards), owned by the
+//    graph from then on, so replays never share shards with direct calls on
+//    the capture stream. A capture cannot allocate: count once on the stream
+//    before capturing (spares are made then), at most SPARE_SHARDS captured
+//    counting calls per stream until tulips_csum_release_stream.
+//  * tulips_csum_release_stream frees everything a stream holds, including
+//    the shards owned by graphs captured on it (destroy those graphs first).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace tulips_amd {
+
+struct StreamState
+{
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex call; // held across one call's launch sequence
+
+  // counter shards (csum_launch.h CNT_SHARDS x CNT_LINE words each)
+  uint32_t* shards = nullptr;          // direct (uncaptured) calls
+  std::vector<uint32_t*> spare;        // for captured calls, made with `shards`
+  std::vector<uint32_t*> graph_owned;  // handed to captured calls
+  std::vector<uint32_t*> retired;      // dropped after a failed launch
+
+  // segmentation workspace (segment.hip)
+  uint32_t* seg_blocks = nullptr;
+  uint32_t* seg_runs = nullptr;
+  uint64_t seg_nruns = 0;
+  void* seg_desc = nullptr; // 16 B per input frame
+  uint64_t seg_ndesc = 0;
+};
+
+constexpr int SPARE_SHARDS = 16;
+
+// The state of `stream` (created on first use). The returned pointer stays
+// valid while held even if the stream is released meanwhile.
+hipError_t stream_state(hipStream_t stream, std::shared_ptr<StreamState>* out);
+
+// Whether `stream` is capturing (a stream that cannot be queried counts as
+// not capturing; the launches will report the error).
+bool stream_capturing(hipStream_t stream);
+
+// Counter shards for one counting call on `s` (caller holds s.call):
+// the stream's direct shards, or, inside a capture, a spare set the graph
+// keeps. hipErrorStreamCaptureUnsupported when a capture finds no spare.
+hipError_t call_shards(StreamState& s, bool capturing, uint32_t** out);
+
+// After a failed launch in a direct counting call: the shards may hold
+// partial sums, so the stream gets fresh zeroed ones on its next call.
+void drop_shards(StreamState& s, uint32_t* shards);
+
+// hipMalloc on `device` (restores the caller's current device).
+hipError_t device_malloc(int device, void** p, size_t bytes);
+
+} // namespace tulips_amd

@@ -1,0 +1,194 @@
+// stream_state.hip — per-(device, stream) state registry (stream_state.h)
+// and tulips_csum_release_stream.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "../../include/tulips_csum.h"
+#include "csum_launch.h"
+#include "stream_state.h"
+
+namespace tulips_amd {
+namespace {
+
+std::mutex g_mutex;
+std::map<std::pair<int, hipStream_t>, std::shared_ptr<StreamState>> g_states;
+
+constexpr size_t SHARD_BYTES = sizeof(uint32_t) * CNT_LINE * CNT_SHARDS;
+
+hipError_t
+stream_device(hipStream_t stream, int* dev)
+{
+  hipDevice_t d = 0;
+  hipError_t e = hipStreamGetDevice(stream, &d);
+  if (e != hipSuccess) {
+    return e;
+  }
+  *dev = int(d);
+  return hipSuccess;
+}
+
+void
+free_on(int device, const std::vector<void*>& ps)
+{
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(device);
+  for (void* p : ps) {
+    if (p) {
+      (void)hipFree(p);
+    }
+  }
+  (void)hipSetDevice(prev);
+}
+
+} // namespace
+
+hipError_t
+device_malloc(int device, void** p, size_t bytes)
+{
+  int prev = 0;
+  hipError_t e = hipGetDevice(&prev);
+  if (e != hipSuccess) {
+    return e;
+  }
+  if (prev != device && (e = hipSetDevice(device)) != hipSuccess) {
+    return e;
+  }
+  *p = nullptr;
+  e = hipMalloc(p, bytes);
+  if (prev != device) {
+    (void)hipSetDevice(prev);
+  }
+  return e;
+}
+
+hipError_t
+stream_state(hipStream_t stream, std::shared_ptr<StreamState>* out)
+{
+  int dev = 0;
+  const hipError_t e = stream_device(stream, &dev);
+  if (e != hipSuccess) {
+    return e;
+  }
+  std::lock_guard<std::mutex> g(g_mutex);
+  std::shared_ptr<StreamState>& s = g_states[std::make_pair(dev, stream)];
+  if (!s) {
+    s = std::make_shared<StreamState>();
+    s->device = dev;
+    s->stream = stream;
+  }
+  *out = s;
+  return hipSuccess;
+}
+
+bool
+stream_capturing(hipStream_t stream)
+{
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return cs != hipStreamCaptureStatusNone;
+}
+
+hipError_t
+call_shards(StreamState& s, bool capturing, uint32_t** out)
+{
+  if (!s.shards) {
+    if (capturing) {
+      return hipErrorStreamCaptureUnsupported;
+    }
+    // direct shards plus the spares captured calls will take, one
+    // allocation each, zeroed in stream order before any kernel uses them
+    std::vector<uint32_t*> made;
+    hipError_t e = hipSuccess;
+    for (int k = 0; k <= SPARE_SHARDS && e == hipSuccess; ++k) {
+      void* p = nullptr;
+      if ((e = device_malloc(s.device, &p, SHARD_BYTES)) == hipSuccess) {
+        made.push_back(static_cast<uint32_t*>(p));
+        e = hipMemsetAsync(p, 0, SHARD_BYTES, s.stream);
+      }
+    }
+    if (e != hipSuccess) {
+      free_on(s.device, std::vector<void*>(made.begin(), made.end()));
+      return e;
+    }
+    s.shards = made[0];
+    s.spare.assign(made.begin() + 1, made.end());
+  }
+  if (!capturing) {
+    *out = s.shards;
+    return hipSuccess;
+  }
+  if (s.spare.empty()) {
+    return hipErrorStreamCaptureUnsupported;
+  }
+  *out = s.spare.back();
+  s.spare.pop_back();
+  s.graph_owned.push_back(*out);
+  return hipSuccess;
+}
+
+void
+drop_shards(StreamState& s, uint32_t* shards)
+{
+  if (shards == s.shards) {
+    s.retired.push_back(s.shards);
+    s.shards = nullptr; // the next call makes fresh ones (and fresh spares)
+  }
+}
+
+} // namespace tulips_amd
+
+extern "C" int
+tulips_csum_release_stream(void* stream)
+{
+  using namespace tulips_amd;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<std::shared_ptr<StreamState>> gone;
+  {
+    std::lock_guard<std::mutex> g(g_mutex);
+    for (auto it = g_states.begin(); it != g_states.end();) {
+      if (it->first.second == st) {
+        gone.push_back(it->second);
+        it = g_states.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  for (auto& s : gone) {
+    std::lock_guard<std::mutex> g(s->call); // no call of this stream in flight
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(s->device);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipGetLastError();
+    }
+    (void)hipSetDevice(prev);
+    std::vector<void*> ps;
+    ps.push_back(s->shards);
+    for (auto* p : s->spare) ps.push_back(p);
+    for (auto* p : s->graph_owned) ps.push_back(p);
+    for (auto* p : s->retired) ps.push_back(p);
+    ps.push_back(s->seg_blocks);
+    ps.push_back(s->seg_runs);
+    ps.push_back(s->seg_desc);
+    free_on(s->device, ps);
+    s->shards = nullptr;
+    s->spare.clear();
+    s->graph_owned.clear();
+    s->retired.clear();
+    s->seg_blocks = s->seg_runs = nullptr;
+    s->seg_desc = nullptr;
+    s->seg_nruns = s->seg_ndesc = 0;
+  }
+  return TULIPS_STATUS_OK;
+}

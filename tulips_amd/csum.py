@@ -133,6 +133,7 @@ _SIGNATURES = {
                                            C.POINTER(Tuning), _vp]),
     "tulips_csum_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
                                                    _vp]),
+    "tulips_csum_release_stream": (C.c_int, [_vp]),
 }
 
 # include/tulips_csum.h TULIPS_FRAME_* (per-frame validation flags)
@@ -519,6 +520,12 @@ def segment_frames(arena, offsets, lengths, mss: int, *, stride: int = 2048,
                                           _addr(first), st),
            "tulips_csum_segment_frames")
     return out, out_lengths, first
+
+
+def release_stream(stream) -> None:
+    """Free the library's per-stream state (counter shards, segmentation
+    workspace) after waiting for `stream` (include/tulips_csum.h)."""
+    _check(lib.tulips_csum_release_stream(_stream(stream)), "release_stream")
 
 
 def version() -> str:
