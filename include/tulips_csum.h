@@ -259,6 +259,29 @@ int tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
                                      const uint16_t* lengths, uint32_t n,
                                      uint8_t* flags, uint32_t* counters);
 
+/* In-place checksum generation for host-resident frames (what a transport's
+ * send path would offload, src/transport/ofed/Device.cpp:756): the frames
+ * travel through the context's pinned pipeline, the GPU computes both fields
+ * as tulips_csum_generate_frames does, and only the 4 field bytes per frame
+ * are written back into `base`. `flags` (host, n bytes) may be NULL. */
+int tulips_csum_generate_frames_host(tulips_csum_ctx* ctx, uint8_t* base,
+                                     const uint64_t* offsets,
+                                     const uint16_t* lengths, uint32_t n,
+                                     uint8_t* flags);
+
+/* Segmentation offload of host-resident super-frames (the TSO request of
+ * src/transport/ofed/Device.cpp:688-772), semantics as
+ * tulips_csum_segment_frames with host arrays: out_base (host) receives
+ * segment j at out_base + j * out_stride for j < out_capacity, out_lengths
+ * (host) its length, out_first (host, n + 1 entries) the exclusive prefix of
+ * the per-frame segment counts. Blocks until the outputs are written. */
+int tulips_csum_segment_frames_host(tulips_csum_ctx* ctx, const uint8_t* in_base,
+                                    const uint64_t* in_offsets,
+                                    const uint16_t* in_lengths, uint32_t n,
+                                    uint32_t mss, uint8_t* out_base,
+                                    uint64_t out_stride, uint32_t out_capacity,
+                                    uint16_t* out_lengths, uint32_t* out_first);
+
 /* ---- per-stream state ---------------------------------------------------- */
 /*
  * Counting calls (tulips_csum_verify, tulips_csum_validate_frames with

@@ -27,10 +27,28 @@
  * only for the process() call, so each frame is copied into the staging
  * arena there; forwarded frames point into the arena and are valid for the
  * duration of the downstream process() call.
+ *
+ * Transmit side (Config::tx) — what a stack built with
+ * TULIPS_HAS_HW_CHECKSUM expects of the NIC (IBV_SEND_IP_CSUM,
+ * src/transport/ofed/Device.cpp:756): committed frames are staged, and at a
+ * burst boundary (tx_burst frames), at the next poll()/wait(), or on
+ * flushTransmit(), their IPv4 and TCP checksums are generated on the GPU in
+ * one batch (tulips_csum_generate_frames_host) and the frames are committed
+ * to the inner device in order. With Config::tso the decorator also plays
+ * the NIC's TSO (TULIPS_HAS_HW_TSO, src/transport/ofed/Device.cpp:688-772):
+ * mss() advertises `tso`-byte send buffers, which prepare() hands out from
+ * its own pool, and a committed frame longer than the inner device's buffer
+ * is cut on the GPU (tulips_csum_segment_frames_host) into frames of the
+ * commit's MSS (0 or too large: the largest that fits the inner buffer, as
+ * the OFED device adjusts it) with both checksums generated; the pieces are
+ * copied into inner buffers and committed in order. The stack's sent()
+ * callback for such a frame comes once all its pieces are sent.
  */
 
 #include <tulips/transport/Device.h>
 #include <cstdint>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 struct tulips_csum_ctx;
@@ -49,23 +67,45 @@ public:
     uint64_t bad_ip = 0;     // dropped: IPv4 header checksum
     uint64_t bad_l4 = 0;     // dropped: TCP checksum / truncation
     uint64_t batches = 0;    // GPU launches
+    uint64_t tx_frames = 0;  // committed by the stack (tx)
+    uint64_t tx_segments = 0; // frames committed to the inner device (tx)
+    uint64_t tx_batches = 0; // GPU batches on the transmit side
   };
 
   static constexpr uint32_t DEFAULT_BURST = 1024;
+
+  struct Config
+  {
+    int gpu = 0;
+    uint32_t burst = DEFAULT_BURST; // receive: frames per GPU batch
+    uint16_t hints = 0;             // VALIDATE_* set up front
+    bool tx = false;                // transmit: checksums generated on the GPU
+    uint32_t tx_burst = 64;         // transmit: frames per GPU batch
+    uint32_t tso = 0;               // > 0: TSO with send buffers of this size
+  };
 
   static Ref allocate(system::Logger& log, transport::Device::Ref device,
                       const int gpu = 0, const uint32_t burst = DEFAULT_BURST,
                       const uint16_t hints = 0)
   {
-    return std::make_unique<Device>(log, std::move(device), gpu, burst, hints);
+    Config c;
+    c.gpu = gpu;
+    c.burst = burst;
+    c.hints = hints;
+    return std::make_unique<Device>(log, std::move(device), c);
+  }
+
+  static Ref allocate(system::Logger& log, transport::Device::Ref device,
+                      Config const& config)
+  {
+    return std::make_unique<Device>(log, std::move(device), config);
   }
 
   /*
    * Throws std::runtime_error when the GPU context cannot be created (no
    * device, no libtulips_csum): there is no CPU fallback.
    */
-  Device(system::Logger& log, transport::Device::Ref device, const int gpu,
-         const uint32_t burst, const uint16_t hints);
+  Device(system::Logger& log, transport::Device::Ref device, Config const& config);
   ~Device() override;
 
   /*
@@ -99,7 +139,7 @@ public:
   Status wait(Processor& proc, const uint64_t ns) override;
 
   uint32_t mtu() const override { return m_device->mtu(); }
-  uint32_t mss() const override { return m_device->mss(); }
+  uint32_t mss() const override { return m_tso ? m_tso : m_device->mss(); }
 
   uint8_t receiveBufferLengthLog2() const override
   {
@@ -116,18 +156,16 @@ public:
     return m_device->identify(buf);
   }
 
-  Status prepare(uint8_t*& buf) override { return m_device->prepare(buf); }
-
+  Status prepare(uint8_t*& buf) override;
   Status commit(const uint16_t len, uint8_t* const buf,
-                const uint16_t mss = 0) override
-  {
-    return m_device->commit(len, buf, mss);
-  }
+                const uint16_t mss = 0) override;
+  Status release(uint8_t* const buf) override;
 
-  Status release(uint8_t* const buf) override
-  {
-    return m_device->release(buf);
-  }
+  /*
+   * Generate (and segment) the staged transmit burst on the GPU now and
+   * commit it to the inner device. No-op without Config::tx.
+   */
+  Status flushTransmit();
 
   Statistics const& statistics() const { return m_stats; }
 
@@ -139,6 +177,14 @@ private:
 
   Status drain();
   Status flush();
+  Status commitPiece(const uint8_t* data, uint16_t len, uint8_t* own, uint16_t mss);
+
+  struct Pending
+  {
+    uint8_t* buf;
+    uint16_t len;
+    uint16_t mss;
+  };
 
   transport::Device::Ref m_device;
   Processor* m_proc;
@@ -153,6 +199,21 @@ private:
   std::vector<uint8_t> m_flags;
   Status m_error;
   Statistics m_stats;
+  // transmit
+  bool m_tx;
+  uint32_t m_tx_burst;
+  uint32_t m_tso;
+  std::vector<Pending> m_pending;
+  std::unordered_set<uint8_t*> m_own;        // our TSO send buffers
+  std::vector<uint8_t*> m_free;              // ... not handed out
+  std::unordered_map<uint8_t*, uint8_t*> m_piece_of; // inner buf -> our buf
+  std::unordered_map<uint8_t*, std::pair<uint32_t, uint16_t>> m_inflight;
+  std::vector<uint64_t> m_tx_offsets;
+  std::vector<uint16_t> m_tx_lengths;
+  std::vector<uint8_t> m_tx_flags;
+  std::vector<uint8_t> m_seg_out;
+  std::vector<uint16_t> m_seg_lengths;
+  std::vector<uint32_t> m_seg_first;
 };
 
 }

@@ -72,7 +72,10 @@ gpucsum_run(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
         return -3;
       }
     }
-    transport::gpucsum::Device dev(log, std::move(rx), 0, burst, hints);
+    transport::gpucsum::Device::Config cfg;
+    cfg.burst = burst;
+    cfg.hints = hints;
+    transport::gpucsum::Device dev(log, std::move(rx), cfg);
     Recorder rec;
     Status s = Status::Ok;
     for (uint64_t it = 0; it <= uint64_t(n) + 2; ++it) {
@@ -106,6 +109,85 @@ gpucsum_run(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
     return 0;
   } catch (std::exception const& e) {
     fprintf(stderr, "gpucsum_run: %s\n", e.what());
+    return -1;
+  }
+}
+
+// Transmit side: the stack's frames (arena/offs/lens, checksum fields as the
+// sender left them) are prepared on and committed to a gpucsum::Device with
+// Config::tx (and Config::tso = `tso` if non-zero) over a list::Device whose
+// buffers hold `wire_mtu` bytes; `mss` is the commit's MSS. The frames that
+// reach the wire (the peer's read list) are copied out back to back into
+// `out` (capacity `out_cap` bytes) with their lengths in out_lens (at most
+// `out_n`). stats = { tx_frames, tx_segments, tx_batches, sent callbacks for
+// the stack's buffers, buffers released }. Returns the number of wire frames
+// or < 0 on failure.
+extern "C" int64_t
+gpucsum_tx_run(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
+               uint32_t n, uint16_t mss, uint32_t tx_burst, uint32_t tso,
+               uint32_t wire_mtu, uint8_t* out, uint64_t out_cap, uint16_t* out_lens,
+               uint32_t out_n, uint64_t* stats)
+{
+  try {
+    system::ConsoleLogger log(system::Logger::Level::Error);
+    transport::list::Device::List a2b, b2a;
+    stack::ethernet::Address mac(0x02, 0, 0, 0, 0, 1);
+    auto inner = transport::list::Device::allocate(log, mac, wire_mtu, b2a, a2b);
+    transport::gpucsum::Device::Config cfg;
+    cfg.tx = true;
+    cfg.tx_burst = tx_burst;
+    cfg.tso = tso;
+    transport::gpucsum::Device dev(log, std::move(inner), cfg);
+    std::vector<uint8_t*> bufs;
+    for (uint32_t i = 0; i < n; ++i) {
+      uint8_t* buf = nullptr;
+      if (dev.prepare(buf) != Status::Ok) {
+        return -3;
+      }
+      memcpy(buf, arena + offs[i], lens[i]);
+      bufs.push_back(buf);
+      if (dev.commit(lens[i], buf, mss) != Status::Ok) {
+        return -4;
+      }
+    }
+    if (dev.flushTransmit() != Status::Ok) {
+      return -5;
+    }
+    // the list device reports its committed buffers as sent on the next
+    // poll; the stack (here: the recorder) then releases them
+    Recorder rec;
+    Status s = dev.poll(rec);
+    if (s != Status::Ok && s != Status::NoDataAvailable) {
+      return -6;
+    }
+    uint64_t released = 0;
+    for (uint8_t* b : bufs) {
+      if (dev.release(b) == Status::Ok) {
+        released += 1;
+      }
+    }
+    uint64_t at = 0;
+    int64_t k = 0;
+    for (auto* p : a2b) {
+      if (uint32_t(k) >= out_n || at + p->len > out_cap) {
+        return -7;
+      }
+      memcpy(out + at, p->data, p->len);
+      out_lens[k++] = uint16_t(p->len);
+      at += p->len;
+    }
+    for (auto* p : a2b) {
+      transport::list::Device::Packet::release(p);
+    }
+    auto const& st = dev.statistics();
+    stats[0] = st.tx_frames;
+    stats[1] = st.tx_segments;
+    stats[2] = st.tx_batches;
+    stats[3] = rec.sent_count;
+    stats[4] = released;
+    return k;
+  } catch (std::exception const& e) {
+    fprintf(stderr, "gpucsum_tx_run: %s\n", e.what());
     return -1;
   }
 }

@@ -70,6 +70,10 @@ def test_host_cxx_symbols_match_reference_kat(golden, oracle):
     a5.restype, a5.argtypes = C.c_uint16, [u8p]
     a6 = getattr(lib, "_ZN6tulips5stack6icmpv48checksumEPKh")
     a6.restype, a6.argtypes = C.c_uint16, [u8p]
+    # tcpv4::Processor::checksum (private static): Address const& -> pointer
+    a2 = getattr(lib, "_ZN6tulips5stack5tcpv49Processor8checksumERKNS0_4ipv47AddressES6_tPKh")
+    a2.restype = C.c_uint16
+    a2.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint16, u8p]
 
     def buf(d):
         b = (C.c_uint8 * max(1, len(d))).from_buffer_copy(d or b"\0")
@@ -79,6 +83,7 @@ def test_host_cxx_symbols_match_reference_kat(golden, oracle):
         p, keep = buf(data)
         return f(*args[:-1], p, *args[-1:]) if args else f(p)
 
+    seen_tcp = False
     for c in golden.kat():
         d = golden.kat_data(c, oracle)
         p, _k = buf(d)
@@ -88,6 +93,11 @@ def test_host_cxx_symbols_match_reference_kat(golden, oracle):
             assert a5(p) == c["expect"], c
         elif c["fn"] == "icmpv4":
             assert a6(p) == c["expect"], c
+        elif c["fn"] == "tcp":
+            src, dst = C.c_uint32(c["src"]), C.c_uint32(c["dst"])
+            assert a2(C.byref(src), C.byref(dst), len(d), p) == c["expect"], c
+            seen_tcp = True
+    assert seen_tcp
 
 
 def test_host_scalar_fuzz_vs_oracle(oracle):

@@ -1,0 +1,171 @@
+"""The drop-in at the reference's own call sites.
+
+integration/Makefile (target `dropin`) compiles the reference's unmodified
+src/stack + src/system + src/api + src/transport/list sources three times —
+the gate variants of CMakeLists.txt:46-47,151-163:
+
+  default  stack verifies (tcpv4/Processor.cpp:121-131, ipv4/Processor.cpp:
+           94-103) and generates (tcpv4/Send.cpp:434-455, ipv4/Producer.cpp:
+           79-82, icmpv4/Request.cpp:54-55) itself
+  nocheck  -DTULIPS_DISABLE_CHECKSUM_CHECK: receive checks left to the device
+  offload  + -DTULIPS_HAS_HW_CHECKSUM: generation left to the device too
+
+removes the reference's own checksum definitions from the objects
+(integration/strip_checksums.sh) and links integration/test/dropin_harness.cpp
+against libtulips_csum.so first. The harness mirrors tests/api/one_client.cpp
+(client + server over list devices) and tests/icmp/basic.cpp (ICMP echo),
+flips a payload bit in 5 data frames on the wire and expects each to be
+dropped, counted and recovered by retransmission.
+
+default runs on the CPU (only the host scalar drop-ins are involved); the
+gated variants need the GPU (the gpucsum decorator validates / generates).
+"""
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, "integration", "_build", "dropin")
+SYMS = {
+    "utils::checksum": "_ZN6tulips5stack5utils8checksumEtPKht",
+    "ipv4::checksum": "_ZN6tulips5stack4ipv48checksumEPKh",
+    "icmpv4::checksum": "_ZN6tulips5stack6icmpv48checksumEPKh",
+    "tcpv4::Processor::checksum":
+        "_ZN6tulips5stack5tcpv49Processor8checksumERKNS0_4ipv47AddressES6_tPKh",
+}
+
+
+def harness(variant):
+    return os.path.join(BUILD, variant, "dropin_harness")
+
+
+needs_build = pytest.mark.skipif(not os.path.exists(harness("default")),
+                                 reason="integration/_build/dropin not built (no reference tree)")
+
+
+def run(variant, *args, env=None, timeout=120):
+    e = dict(os.environ)
+    e.update(env or {})
+    p = subprocess.run([harness(variant), *args], capture_output=True, text=True,
+                       timeout=timeout, env=e)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    return p.returncode, json.loads(lines[-1])
+
+
+def check_exchange(r, flipped=5, replies="messages"):
+    assert r["connected"] and r["data_ok"], r
+    assert r["bytes"] == r["want_bytes"] and r["undelivered"] == 0, r
+    # the server answers every delivery (one per segment: with TSO a message
+    # arrives as several)
+    if replies == "messages":
+        assert r["replies"] == r["messages"], r
+    assert r["reply_bytes"] == 32 * r["replies"], r
+    assert r["flipped"] == flipped, r
+    assert r["cli_tcp"]["rexmit"] >= flipped, r
+    assert r["icmp_ok"], r
+    assert r["other_status"] == 0, r
+    assert r["ok"], r
+
+
+@needs_build
+def test_reference_definitions_removed_from_the_stack():
+    """Every variant's stack object set lost its own checksum definitions;
+    the library that replaces them defines all four."""
+    for v in ("default", "nocheck", "offload"):
+        txt = open(os.path.join(BUILD, v, "stripped.txt")).read()
+        for name, sym in SYMS.items():
+            assert re.search(rf"^(stripped|weakened|absent)\s+{re.escape(sym)}\b", txt, re.M), (v, name)
+        nm = subprocess.run(["nm", "-D", "--defined-only",
+                             os.path.join(BUILD, v, "libtulips_stack_dropin.so")],
+                            capture_output=True, text=True, check=True).stdout
+        for name in ("utils::checksum", "ipv4::checksum", "icmpv4::checksum"):
+            assert not re.search(rf" [TtWw] {re.escape(SYMS[name])}$", nm, re.M), (v, name)
+    lib = subprocess.run(["nm", "-D", "--defined-only",
+                          os.path.join(ROOT, "tulips_amd", "libtulips_csum.so")],
+                         capture_output=True, text=True, check=True).stdout
+    for sym in SYMS.values():
+        assert re.search(rf" T {re.escape(sym)}$", lib, re.M), sym
+
+
+@needs_build
+def test_default_gates_exchange_and_bindings(tmp_path):
+    """Stack-side checks and generation through libtulips_csum.so's host
+    drop-ins: the exchange completes with no checksum error, the 5 corrupted
+    frames are dropped by the stack's own verify site (chkerr, CorruptedData)
+    and retransmitted, ICMP echo works, and the dynamic linker binds the
+    stack's checksum references to libtulips_csum.so."""
+    rc, r = run("default", env={"LD_DEBUG": "bindings",
+                                "LD_DEBUG_OUTPUT": str(tmp_path / "ld")})
+    assert rc == 0
+    check_exchange(r)
+    assert r["stack_checks"] and r["stack_generates"]
+    assert r["srv_tcp"]["chkerr"] == 5 and r["srv_tcp"]["drop"] == 5, r
+    assert r["corrupted_status"] == 5, r
+    assert r["cli_tcp"]["chkerr"] == 0 and r["srv_ip"]["chkerr"] == 0 and r["cli_ip"]["chkerr"] == 0
+    for name in SYMS:
+        assert r["symbols"][name] == "libtulips_csum.so", (name, r["symbols"])
+    log = "".join(open(tmp_path / f).read() for f in os.listdir(tmp_path))
+    for name in ("ipv4::checksum", "icmpv4::checksum", "tcpv4::Processor::checksum"):
+        pat = (r"binding file \S*libtulips_stack_dropin\.so \[0\] to \S*libtulips_csum\.so "
+               rf"\[0\]: normal symbol `{re.escape(SYMS[name])}'")
+        assert re.search(pat, log), name
+        assert not re.search(r"to \S*libtulips_stack_dropin\.so \[0\]: normal symbol "
+                             rf"`{re.escape(SYMS[name])}'", log), name
+
+
+@needs_build
+def test_default_gates_clean_exchange():
+    rc, r = run("default", "--corrupt", "0", "--messages", "300")
+    assert rc == 0
+    check_exchange(r, flipped=0)
+    assert r["srv_tcp"]["chkerr"] == 0 and r["srv_tcp"]["drop"] == 0, r
+    assert r["cli_tcp"]["rexmit"] == 0
+
+
+@pytest.mark.gpu
+@needs_build
+@pytest.mark.parametrize("burst", [1, 64])
+def test_nocheck_gates_with_gpu_validation(burst):
+    """TULIPS_DISABLE_CHECKSUM_CHECK: the stack checks nothing and hints
+    VALIDATE_IP_CSUM / VALIDATE_L4_CSUM (src/api/Client.cpp:39-41); the gpucsum
+    decorator validates every received frame on the GPU and drops the 5
+    corrupted ones (bad_l4), which the client then retransmits."""
+    rc, r = run("nocheck", "--gpucsum", "--burst", str(burst))
+    assert rc == 0, r
+    check_exchange(r)
+    assert not r["stack_checks"] and r["stack_generates"]
+    assert r["srv_tcp"]["chkerr"] == 0
+    sd = r["server_decorator"]
+    assert sd["bad_l4"] == 5 and sd["bad_ip"] == 0, sd
+    assert sd["forwarded"] == sd["frames"] - 5 and sd["batches"] > 0, sd
+    assert r["client_decorator"]["bad_l4"] == 0
+
+
+@pytest.mark.gpu
+@needs_build
+@pytest.mark.parametrize("tso", [0, 65535])
+def test_offload_gates_gpu_generates_and_validates(tso):
+    """TULIPS_HAS_HW_CHECKSUM + TULIPS_DISABLE_CHECKSUM_CHECK: the stack
+    neither generates nor verifies (a2/a5 are compiled out); the decorators
+    generate every IPv4/TCP checksum on the GPU before frames reach the wire
+    and validate on receipt. With TSO the client's stack builds super-frames
+    (up to 16 KB messages) that the decorator cuts on the GPU."""
+    args = ["--gpucsum", "--tx"]
+    if tso:
+        args += ["--tso", str(tso), "--max", "16000", "--messages", "120"]
+    rc, r = run("offload", *args)
+    assert rc == 0, json.dumps(r)
+    check_exchange(r, replies=None if tso else "messages")
+    assert not r["stack_checks"] and not r["stack_generates"]
+    cd, sd = r["client_decorator"], r["server_decorator"]
+    assert sd["bad_l4"] == 5 and sd["bad_ip"] == 0, sd
+    assert cd["bad_l4"] == 0 and cd["bad_ip"] == 0, cd
+    assert cd["tx_frames"] > 0 and sd["tx_frames"] > 0 and cd["tx_batches"] > 0
+    if tso:
+        assert cd["tx_segments"] > cd["tx_frames"], cd
+    else:
+        assert cd["tx_segments"] == cd["tx_frames"], cd

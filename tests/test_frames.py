@@ -371,3 +371,23 @@ def test_frames_tuned_rejects_bad_geometry():
     assert f(2, A, A, A, 4, A, None, csum.Tuning(group=16, unroll=4), None) == 1
     assert f(0, A, A, A, 4, A, None, csum.Tuning(group=16, unroll=4, block=384), None) == 1
     assert f(0, A, A, A, 0, None, None, csum.Tuning(group=16, unroll=6), None) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [False, True])
+def test_gpu_generate_host_context(oracle, pinned):
+    """tulips_csum_generate_frames_host: host frames through the pinned
+    pipeline, only the 4 field bytes per frame written back — byte-exact with
+    the oracle (itself pinned to reference-generated frames above), across
+    many pipeline stages (small chunk)."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(77)
+    src = scramble_fields(fx, rng)
+    exp_arena, exp_flags = oracle.generate_frames(src, fx["offsets"], fx["lengths"])
+    arena = torch.from_numpy(src.copy()).pin_memory().numpy() if pinned else src.copy()
+    with csum.HostContext(0, chunk_bytes=1 << 17) as ctx:
+        fl = ctx.generate_frames(arena, fx["offsets"], fx["lengths"])
+    np.testing.assert_array_equal(fl, exp_flags)
+    assert np.array_equal(arena, exp_arena), np.nonzero(arena != exp_arena)[0][:10]

@@ -98,3 +98,108 @@ def test_burst_sizes(burst):
     np.testing.assert_array_equal(fwd, exp)
     if burst == 4096:
         assert int(st[4]) == 1          # the whole poll burst in one launch
+
+
+# ------------------------------------------------------------ transmit -----
+def tx_run(arena, offs, lens, mss, tx_burst, tso, wire_mtu=1514):
+    from tulips_amd import csum  # noqa: F401
+    lib = C.CDLL(HARNESS)
+    f = lib.gpucsum_tx_run
+    f.restype = C.c_int64
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint16, C.c_uint32,
+                  C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
+                  C.c_void_p]
+    n = len(offs)
+    cap_n = int(sum(int(x) // max(mss, 1) + 2 for x in lens)) + 16
+    out = np.zeros(cap_n * wire_mtu, dtype=np.uint8)
+    olen = np.zeros(cap_n, dtype=np.uint16)
+    st = np.zeros(5, dtype=np.uint64)
+    arena = np.ascontiguousarray(arena)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    k = f(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, mss, tx_burst, tso,
+          wire_mtu, out.ctypes.data, out.nbytes, olen.ctypes.data, cap_n, st.ctypes.data)
+    assert k >= 0, f"gpucsum_tx_run rc={k}"
+    olen = olen[:k]
+    pos = np.concatenate([[0], np.cumsum(olen.astype(np.int64))])
+    frames = [bytes(out[pos[i]:pos[i + 1]]) for i in range(k)]
+    return frames, st
+
+
+@needs_harness
+@pytest.mark.gpu
+@pytest.mark.parametrize("tx_burst", [1, 5, 64])
+def test_tx_generates_checksums_before_the_wire(oracle, tx_burst):
+    """Config::tx: the fixture's frames (checksum fields scrambled) committed
+    through the decorator reach the wire exactly as the oracle's generation
+    writes them (pinned to reference-generated bytes in test_frames.py), in
+    commit order; the stack's buffers are reported sent and released."""
+    from test_frames import scramble_fields
+    fx = fixture()
+    rng = np.random.default_rng(tx_burst)
+    src = scramble_fields(fx, rng)
+    n = 700
+    offs, lens = fx["offsets"][:n], fx["lengths"][:n]
+    keep = lens <= 1514                       # what fits the list device's buffers
+    offs, lens = offs[keep], lens[keep]
+    exp_arena, exp_flags = oracle.generate_frames(src, offs, lens)
+    frames, st = tx_run(src, offs, lens, 0, tx_burst, 0)
+    assert len(frames) == len(offs)
+    for i, f in enumerate(frames):
+        o, ln = int(offs[i]), int(lens[i])
+        assert f == bytes(exp_arena[o:o + ln]), i
+    assert int(st[0]) == len(offs) and int(st[1]) == len(offs)
+    assert int(st[2]) == (len(offs) + tx_burst - 1) // tx_burst
+    assert int(st[3]) == len(offs) and int(st[4]) == len(offs)
+
+
+@needs_harness
+@pytest.mark.gpu
+@pytest.mark.parametrize("mss", [0, 536, 1460])
+def test_tx_tso_segments_super_frames(oracle, mss):
+    """Config::tso: super-frames up to 64 KB committed with the stack's MSS
+    are cut on the GPU into wire frames that (1) equal the oracle's
+    segmentation, (2) verify with the REFERENCE's own ipv4::checksum and
+    tcpv4::Processor::checksum (oracle/_ref), and (3) reassemble to the
+    super-frame's payload; one sent() per super-frame reaches the stack.
+    mss 0 = the largest that fits the inner buffer, as the OFED device
+    adjusts it (src/transport/ofed/Device.cpp:711-714)."""
+    from oracle import Reference
+    from test_segment import check_properties, pack, super_frame
+    ref = Reference()
+    rng = np.random.default_rng(mss + 1)
+    pays = [0, 40, 1460, 1461, 3000, 9000, 20000, 65535 - 54 - 40]
+    frames_in = [super_frame(oracle, rng, p, doff=[5, 8][i % 2]) for i, p in enumerate(pays)]
+    arena, offs, lens = pack(frames_in, rng)
+    wire, st = tx_run(arena, offs, lens, mss, 4, 65535)
+    eff = []
+    for f in frames_in:
+        hl = 34 + 4 * (f[46] >> 4)
+        lm = mss if mss and mss <= 1514 - hl else 1514 - hl
+        eff.append(lm)
+    # group the wire frames back per super-frame and check each
+    at = 0
+    for f, lm in zip(frames_in, eff):
+        hl = 34 + 4 * (f[46] >> 4)
+        total = f[16] << 8 | f[17]
+        npay = total - 20 - (hl - 34)
+        cnt = 1 if len(f) <= 1514 else max(1, -(-npay // lm))
+        segs = wire[at:at + cnt]
+        at += cnt
+        if len(f) <= 1514:
+            exp_arena, _ = oracle.generate_frames(np.frombuffer(f, np.uint8).copy(),
+                                                  np.zeros(1, np.uint64),
+                                                  np.array([len(f)], np.uint16))
+            assert segs[0] == bytes(exp_arena)
+        else:
+            check_properties(oracle, f, segs, lm)
+        for s in segs:
+            ip = s[14:34]
+            assert ref.ipv4_checksum(ip) == 0xFFFF
+            src = int.from_bytes(s[26:30], "little")
+            dst = int.from_bytes(s[30:34], "little")
+            tl = (s[16] << 8 | s[17]) - 20
+            assert ref.tcp_checksum(src, dst, s[34:34 + tl]) == 0xFFFF
+    assert at == len(wire)
+    assert int(st[0]) == len(frames_in) and int(st[1]) == len(wire)
+    assert int(st[3]) == len(frames_in) and int(st[4]) == len(frames_in)

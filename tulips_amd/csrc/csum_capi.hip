@@ -83,6 +83,26 @@ checksum(const uint8_t* const data)
 }
 }
 
+// tulips::stack::tcpv4::Processor::checksum (private static,
+// include/tulips/stack/tcpv4/Processor.h:142-145, src/stack/tcpv4/
+// Processor.cpp:337-357). Exported under its mangled name so a stack linked
+// against this library before its own objects resolves the verify
+// (Processor.cpp:121) and generate (Send.cpp:448) sites here without a
+// source change. The ipv4::Address arguments arrive by const reference, i.e.
+// as pointers to the 4-byte m_data word (include/tulips/stack/IPv4.h:55).
+extern "C" __attribute__((visibility("default"))) uint16_t
+tulips_tcpv4_processor_checksum(const uint32_t* src, const uint32_t* dst,
+                                const uint16_t len, const uint8_t* const data)
+  __asm__("_ZN6tulips5stack5tcpv49Processor8checksumERKNS0_4ipv47AddressES6_tPKh");
+
+uint16_t
+tulips_tcpv4_processor_checksum(const uint32_t* src, const uint32_t* dst,
+                                const uint16_t len, const uint8_t* const data)
+{
+  // the reference returns the uncomplemented sum in network order, 0 -> 0xffff
+  return uint16_t(inet_post(host_checksum(tcp_seed(*src, *dst, len), data, len)));
+}
+
 extern "C" {
 
 uint16_t

@@ -146,6 +146,7 @@ struct Slot
   uint32_t* h_dst = nullptr;
   uint16_t* h_out = nullptr;
   uint32_t* h_cnt = nullptr;
+  uint32_t* h_fields = nullptr;
   uint8_t* d_bytes = nullptr;
   uint64_t* d_offs = nullptr;
   uint16_t* d_lens = nullptr;
@@ -154,6 +155,7 @@ struct Slot
   uint32_t* d_dst = nullptr;
   uint16_t* d_out = nullptr;
   uint32_t* d_cnt = nullptr;
+  uint32_t* d_fields = nullptr;
   bool busy = false;
   uint32_t i0 = 0, i1 = 0;
 };
@@ -187,6 +189,13 @@ struct tulips_csum_ctx
   uint64_t chunk = DEFAULT_CHUNK;
   Slot slots[NSLOTS];
   PackPool pool;
+  // segmentation output (tulips_csum_segment_frames_host), grown on demand
+  uint8_t* d_seg_out = nullptr;
+  uint64_t seg_out_bytes = 0;
+  uint16_t* d_seg_lens = nullptr;
+  uint64_t seg_lens_n = 0;
+  uint32_t* d_first = nullptr;
+  uint32_t* h_first = nullptr;
 };
 
 namespace {
@@ -205,6 +214,7 @@ free_slot(Slot& s)
   (void)hipHostFree(s.h_dst);
   (void)hipHostFree(s.h_out);
   (void)hipHostFree(s.h_cnt);
+  (void)hipHostFree(s.h_fields);
   (void)hipFree(s.d_bytes);
   (void)hipFree(s.d_offs);
   (void)hipFree(s.d_lens);
@@ -213,6 +223,7 @@ free_slot(Slot& s)
   (void)hipFree(s.d_dst);
   (void)hipFree(s.d_out);
   (void)hipFree(s.d_cnt);
+  (void)hipFree(s.d_fields);
   if (s.done) {
     (void)hipEventDestroy(s.done);
   }
@@ -242,6 +253,7 @@ alloc_slot(Slot& s, uint64_t chunk)
   TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_dst), m * 4, 0));
   TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), m * 2, 0));
   TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_cnt), 16, 0));
+  TCS_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_fields), m * 4, 0));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_bytes), chunk));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_offs), m * 8));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_lens), m * 2));
@@ -250,6 +262,7 @@ alloc_slot(Slot& s, uint64_t chunk)
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_dst), m * 4));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_out), m * 2));
   TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_cnt), 16));
+  TCS_TRY(hipMalloc(reinterpret_cast<void**>(&s.d_fields), m * 4));
 #undef TCS_TRY
   return hipSuccess;
 }
@@ -259,11 +272,15 @@ alloc_slot(Slot& s, uint64_t chunk)
 struct Job
 {
   bool frames = false;
+  bool generate = false;          // frames: write both checksum fields
+  uint8_t* patch_base = nullptr;  // generate: the caller's frames
+  const uint64_t* offsets = nullptr;
   const uint16_t* seeds = nullptr;
   const uint32_t* src = nullptr;
   const uint32_t* dst = nullptr;
   uint32_t mode = 0;
-  uint8_t* out = nullptr; // host results, elem() bytes per entry
+  uint8_t* out = nullptr; // host results, elem() bytes per entry (nullable
+                          // for generate)
   uint32_t* counters = nullptr;
   size_t elem() const { return frames ? 1 : 2; }
 };
@@ -276,7 +293,24 @@ retire(Slot& s, const Job& job)
     return hipSuccess;
   }
   const hipError_t e = hipEventSynchronize(s.done);
-  if (e == hipSuccess) {
+  if (e == hipSuccess && job.generate) {
+    // the generated fields into the caller's frames (Eth 14 + IPv4 10 and
+    // Eth 14 + IPv4 20 + TCP 16), where the flags say they were written
+    const uint8_t* fl = reinterpret_cast<const uint8_t*>(s.h_out);
+    for (uint32_t k = s.i0; k < s.i1; ++k) {
+      uint8_t* f = job.patch_base + job.offsets[k];
+      const uint32_t v = s.h_fields[k - s.i0];
+      if (fl[k - s.i0] & TULIPS_FRAME_IP_CSUM_OK) {
+        f[24] = uint8_t(v);
+        f[25] = uint8_t(v >> 8);
+      }
+      if (fl[k - s.i0] & TULIPS_FRAME_L4_CSUM_OK) {
+        f[50] = uint8_t(v >> 16);
+        f[51] = uint8_t(v >> 24);
+      }
+    }
+  }
+  if (e == hipSuccess && job.out) {
     memcpy(job.out + size_t(s.i0) * job.elem(), s.h_out,
            size_t(s.i1 - s.i0) * job.elem());
     if (job.counters) {
@@ -379,6 +413,10 @@ tulips_csum_ctx_destroy(tulips_csum_ctx* ctx)
   for (auto& s : ctx->slots) {
     free_slot(s);
   }
+  (void)hipFree(ctx->d_seg_out);
+  (void)hipFree(ctx->d_seg_lens);
+  (void)hipFree(ctx->d_first);
+  (void)hipHostFree(ctx->h_first);
   (void)hipSetDevice(prev);
   delete ctx;
   return TULIPS_STATUS_OK;
@@ -461,7 +499,13 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
       TCS_Q(hipMemcpyAsync(s.d_dst, s.h_dst, size_t(cnt) * 4,
                            hipMemcpyHostToDevice, st));
     }
-    if (job.frames) {
+    if (job.generate) {
+      TCS_Q(launch_generate(const_cast<uint8_t*>(dbase), s.d_offs, s.d_lens, cnt,
+                            reinterpret_cast<uint8_t*>(s.d_out), st, FrameLaunch{},
+                            s.d_fields));
+      TCS_Q(hipMemcpyAsync(s.h_fields, s.d_fields, size_t(cnt) * 4,
+                           hipMemcpyDeviceToHost, st));
+    } else if (job.frames) {
       TCS_Q(launch_frames(dbase, s.d_offs, s.d_lens, cnt,
                           reinterpret_cast<uint8_t*>(s.d_out),
                           job.counters ? s.d_cnt : nullptr, st));
@@ -578,6 +622,171 @@ tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
   job.out = flags;
   job.counters = counters;
   return run(ctx, base, offsets, lengths, n, job);
+}
+
+} // extern "C"
+
+namespace {
+
+// grow *p to at least `bytes` (device memory of the ctx's device, current)
+hipError_t
+grow(void** p, uint64_t* have, uint64_t bytes)
+{
+  if (*have >= bytes) {
+    return hipSuccess;
+  }
+  (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  const hipError_t e = hipMalloc(p, bytes);
+  if (e == hipSuccess) {
+    *have = bytes;
+  }
+  return e;
+}
+
+int
+segment_host(tulips_csum_ctx* ctx, const uint8_t* in_base, const uint64_t* in_offsets,
+             const uint16_t* in_lengths, uint32_t n, uint32_t mss, uint8_t* out_base,
+             uint64_t out_stride, uint32_t out_capacity, uint16_t* out_lengths,
+             uint32_t* out_first)
+{
+  Slot& s = ctx->slots[0];
+  hipStream_t st = s.stream;
+  hipError_t e = hipSuccess;
+  if (!ctx->d_first) {
+    if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->d_first),
+                       sizeof(uint32_t) * (MAX_SEGS_PER_CHUNK + 1))) != hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&ctx->h_first),
+                           sizeof(uint32_t) * (MAX_SEGS_PER_CHUNK + 1), 0)) != hipSuccess) {
+      return status_of(e);
+    }
+  }
+  uint64_t produced = 0; // segments of the frames before this chunk
+  uint32_t i = 0;
+  while (i < n) {
+    // frames [i, j) that fit one staging chunk
+    uint64_t bytes = 0;
+    uint32_t j = i;
+    while (j < n && j - i < MAX_SEGS_PER_CHUNK && bytes + in_lengths[j] <= ctx->chunk) {
+      s.h_offs[j - i] = bytes;
+      bytes += in_lengths[j];
+      ++j;
+    }
+    const uint32_t cnt = j - i;
+    pack(ctx->pool, s, in_base, in_offsets, in_lengths, i, j);
+    memcpy(s.h_lens, in_lengths + i, size_t(cnt) * 2);
+    const uint32_t room =
+      produced >= out_capacity ? 0u : uint32_t(out_capacity - produced);
+    if (room) {
+      uint64_t have_lens = ctx->seg_lens_n * 2;
+      if ((e = grow(reinterpret_cast<void**>(&ctx->d_seg_out), &ctx->seg_out_bytes,
+                    uint64_t(room) * out_stride)) != hipSuccess ||
+          (e = grow(reinterpret_cast<void**>(&ctx->d_seg_lens), &have_lens,
+                    uint64_t(room) * 2)) != hipSuccess) {
+        return status_of(e);
+      }
+      ctx->seg_lens_n = have_lens / 2;
+    }
+    if ((e = hipMemcpyAsync(s.d_bytes, s.h_bytes, bytes, hipMemcpyHostToDevice, st)) !=
+          hipSuccess ||
+        (e = hipMemcpyAsync(s.d_offs, s.h_offs, size_t(cnt) * 8, hipMemcpyHostToDevice,
+                            st)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_lens, s.h_lens, size_t(cnt) * 2, hipMemcpyHostToDevice,
+                            st)) != hipSuccess) {
+      return status_of(e);
+    }
+    int rc = tulips_csum_segment_frames(s.d_bytes, s.d_offs, s.d_lens, cnt, mss,
+                                        room ? ctx->d_seg_out : nullptr, out_stride, room,
+                                        room ? ctx->d_seg_lens : nullptr, ctx->d_first, st);
+    if (rc != TULIPS_STATUS_OK) {
+      return rc;
+    }
+    if ((e = hipMemcpyAsync(ctx->h_first, ctx->d_first, sizeof(uint32_t) * (cnt + 1),
+                            hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess) {
+      return status_of(e);
+    }
+    const uint32_t made = ctx->h_first[cnt];
+    const uint32_t kept = made < room ? made : room;
+    for (uint32_t k = 0; k < cnt; ++k) {
+      out_first[i + k] = uint32_t(produced + ctx->h_first[k]);
+    }
+    if (kept) {
+      if ((e = hipMemcpyAsync(out_base + produced * out_stride, ctx->d_seg_out,
+                              uint64_t(kept) * out_stride, hipMemcpyDeviceToHost, st)) !=
+            hipSuccess ||
+          (e = hipMemcpyAsync(out_lengths + produced, ctx->d_seg_lens,
+                              uint64_t(kept) * 2, hipMemcpyDeviceToHost, st)) !=
+            hipSuccess ||
+          (e = hipStreamSynchronize(st)) != hipSuccess) {
+        return status_of(e);
+      }
+    }
+    produced += made;
+    i = j;
+  }
+  out_first[n] = uint32_t(produced);
+  return TULIPS_STATUS_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int
+tulips_csum_generate_frames_host(tulips_csum_ctx* ctx, uint8_t* base,
+                                 const uint64_t* offsets, const uint16_t* lengths,
+                                 uint32_t n, uint8_t* flags)
+{
+  if (!ctx) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  Job job;
+  job.frames = true;
+  job.generate = true;
+  job.patch_base = base;
+  job.offsets = offsets;
+  job.out = flags;
+  return run(ctx, base, offsets, lengths, n, job);
+}
+
+int
+tulips_csum_segment_frames_host(tulips_csum_ctx* ctx, const uint8_t* in_base,
+                                const uint64_t* in_offsets,
+                                const uint16_t* in_lengths, uint32_t n,
+                                uint32_t mss, uint8_t* out_base,
+                                uint64_t out_stride, uint32_t out_capacity,
+                                uint16_t* out_lengths, uint32_t* out_first)
+{
+  if (!ctx || !out_first || mss == 0 || mss > 0xffffu) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (n == 0) {
+    out_first[0] = 0;
+    return TULIPS_STATUS_OK;
+  }
+  if (!in_base || !in_offsets || !in_lengths ||
+      (out_capacity && (!out_base || !out_lengths || out_stride < 16 ||
+                        (out_stride & 15)))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  const hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  const int rc = segment_host(ctx, in_base, in_offsets, in_lengths, n, mss, out_base,
+                              out_stride, out_capacity, out_lengths, out_first);
+  (void)hipSetDevice(prev);
+  return rc;
 }
 
 } // extern "C"

@@ -54,9 +54,12 @@ struct FrameLaunch
   int nontemporal = 1;     // nt chunk loads
 };
 bool frame_geometry_ok(int group, int unroll, uint32_t block);
+// fields (nullable): per frame, the IPv4 (low 16 bits) and TCP (high 16)
+// checksum values as stored, 0 where not written (see flags)
 hipError_t launch_generate(uint8_t* base, const uint64_t* offs,
                            const uint16_t* lens, uint32_t n, uint8_t* flags,
-                           hipStream_t stream, const FrameLaunch& fl = {});
+                           hipStream_t stream, const FrameLaunch& fl = {},
+                           uint32_t* fields = nullptr);
 hipError_t launch_frames(const uint8_t* base, const uint64_t* offs,
                          const uint16_t* lens, uint32_t n, uint8_t* flags,
                          uint32_t* counters, hipStream_t stream,

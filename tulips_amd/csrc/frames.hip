@@ -73,7 +73,8 @@ template<bool GENERATE, int FG, int FU, bool NT>
 __global__ __launch_bounds__(1024, GENERATE ? TULIPS_FRAME_GEN_WAVES : TULIPS_FRAME_VAL_WAVES) void
 frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
-             uint8_t* __restrict__ flags, uint32_t* __restrict__ shards)
+             uint8_t* __restrict__ flags, uint32_t* __restrict__ shards,
+             uint32_t* __restrict__ fields)
 {
   const int lane64 = threadIdx.x & 63;
   const int lane = lane64 & (FG - 1);
@@ -116,11 +117,13 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
             : 0));
     if (lane == 0) {
       if (GENERATE) {
+        uint32_t written = 0;
         if (h.ipv4) {
           const uint32_t p =
             fold32(ip_part) + (0xffffu - field_contrib(fa + 24, h.ipck0, h.ipck1));
           const uint32_t r = finish(p, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20);
           store_field(fa + 24, ~r & 0xffffu);
+          written = ~r & 0xffffu;
         }
         if (do_l4) {
           const uint32_t p =
@@ -128,6 +131,12 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
           const uint32_t r =
             finish(p, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst, h.tcplen);
           store_field(fa + 50, ~r & 0xffffu);
+          written |= (~r & 0xffffu) << 16;
+        }
+        if (fields) {
+          // the two field values as stored (little-endian u16s) for a host
+          // copy of the frames (tulips_csum_generate_frames_host)
+          fields[f] = written;
         }
         if (flags) {
           flags[f] = uint8_t(frame_flags(h, h.ipv4, do_l4));
@@ -203,7 +212,7 @@ constexpr int DEFAULT_G = 16, DEFAULT_U = 6;
 template<bool GENERATE, int G, int U, bool NT>
 hipError_t
 launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
-           uint8_t* flags, uint32_t* counters, const FrameLaunch& fl,
+           uint8_t* flags, uint32_t* counters, uint32_t* fields, const FrameLaunch& fl,
            hipStream_t stream)
 {
   const uint32_t block = fl.block ? fl.block : 256;
@@ -215,14 +224,14 @@ launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n
   }
   (void)hipGetLastError();
   hipLaunchKernelGGL((frame_kernel<GENERATE, G, U, NT>), dim3(uint32_t(blocks)),
-                     dim3(block), 0, stream, base, offs, lens, n, flags, counters);
+                     dim3(block), 0, stream, base, offs, lens, n, flags, counters, fields);
   return hipGetLastError();
 }
 
 template<bool GENERATE>
 hipError_t
 dispatch(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
-         uint8_t* flags, uint32_t* counters, const FrameLaunch& fl,
+         uint8_t* flags, uint32_t* counters, uint32_t* fields, const FrameLaunch& fl,
          hipStream_t stream)
 {
   const int g = fl.group ? fl.group : DEFAULT_G, u = fl.unroll ? fl.unroll : DEFAULT_U;
@@ -230,9 +239,10 @@ dispatch(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
 #define TCS_F(G, U)                                                            \
   if (g == G && u == U) {                                                      \
     return nt ? launch_one<GENERATE, G, U, true>(base, offs, lens, n, flags,    \
-                                                 counters, fl, stream)         \
+                                                 counters, fields, fl, stream) \
               : launch_one<GENERATE, G, U, false>(base, offs, lens, n, flags,   \
-                                                  counters, fl, stream);       \
+                                                  counters, fields, fl,        \
+                                                  stream);                     \
   }
   TCS_F(16, 4)
   TCS_F(16, 6)
@@ -280,7 +290,7 @@ launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
   }
   if (!counters) {
     return dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n, flags, nullptr,
-                           fl, stream);
+                           nullptr, fl, stream);
   }
   std::shared_ptr<StreamState> ss;
   hipError_t e = stream_state(stream, &ss);
@@ -293,8 +303,8 @@ launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
   if ((e = call_shards(*ss, capturing, &shards)) != hipSuccess) {
     return e;
   }
-  e = dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n, flags, shards, fl,
-                      stream);
+  e = dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n, flags, shards, nullptr,
+                      fl, stream);
   if (e == hipSuccess) {
     e = launch_counters_finalize(shards, counters, 4, stream);
   }
@@ -306,12 +316,13 @@ launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
 
 hipError_t
 launch_generate(uint8_t* base, const uint64_t* offs, const uint16_t* lens,
-                uint32_t n, uint8_t* flags, hipStream_t stream, const FrameLaunch& fl)
+                uint32_t n, uint8_t* flags, hipStream_t stream, const FrameLaunch& fl,
+                uint32_t* fields)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  return dispatch<true>(base, offs, lens, n, flags, nullptr, fl, stream);
+  return dispatch<true>(base, offs, lens, n, flags, nullptr, fields, fl, stream);
 }
 
 } // namespace tulips_amd

@@ -134,6 +134,9 @@ _SIGNATURES = {
     "tulips_csum_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
                                                    _vp]),
     "tulips_csum_release_stream": (C.c_int, [_vp]),
+    "tulips_csum_generate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp]),
+    "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
+                                                  _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
 }
 
 # include/tulips_csum.h TULIPS_FRAME_* (per-frame validation flags)
@@ -148,6 +151,7 @@ CXX_SYMBOLS = (
     "_ZN6tulips5stack5utils8checksumEtPKht",
     "_ZN6tulips5stack4ipv48checksumEPKh",
     "_ZN6tulips5stack6icmpv48checksumEPKh",
+    "_ZN6tulips5stack5tcpv49Processor8checksumERKNS0_4ipv47AddressES6_tPKh",
     "_ZN6tulips5stack5utils8toeplitzERKNS0_4ipv47AddressES5_ttmPKhj",
 )
 
@@ -414,6 +418,48 @@ class HostContext:
             cnt.ctypes.data if with_counters else None)
         _check(rc, "tulips_csum_validate_frames_host")
         return (flags, cnt) if with_counters else flags
+
+    def generate_frames(self, arena, offsets, lengths):
+        """Write both checksum fields of host frames in `arena` (a writable
+        uint8 numpy array) in place; returns the FRAME_* flags of what was
+        written."""
+        import numpy as np
+        if not (isinstance(arena, np.ndarray) and arena.dtype == np.uint8 and
+                arena.flags.c_contiguous and arena.flags.writeable):
+            raise ValueError("arena must be a writable contiguous uint8 array")
+        off = _host(offsets, np.uint64)
+        ln = _host(lengths, np.uint16)
+        n = len(off.keep)
+        if len(ln.keep) != n:
+            raise ValueError("offsets/lengths size mismatch")
+        flags = np.empty(n, dtype=np.uint8)
+        _check(lib.tulips_csum_generate_frames_host(self._h, arena.ctypes.data, off.ptr,
+                                                    ln.ptr, n, flags.ctypes.data),
+               "tulips_csum_generate_frames_host")
+        return flags
+
+    def segment_frames(self, arena, offsets, lengths, mss: int, *, stride: int = 2048,
+                       capacity: int | None = None):
+        """Host super-frames -> (out bytes, out_lengths, first)."""
+        import numpy as np
+        ar = _host(arena, np.uint8)
+        off = _host(offsets, np.uint64)
+        ln = _host(lengths, np.uint16)
+        n = len(off.keep)
+        first = np.zeros(n + 1, dtype=np.uint32)
+        if capacity is None:
+            _check(lib.tulips_csum_segment_frames_host(self._h, ar.ptr, off.ptr, ln.ptr, n,
+                                                       mss, None, stride, 0, None,
+                                                       first.ctypes.data),
+                   "tulips_csum_segment_frames_host")
+            capacity = int(first[n])
+        out = np.zeros(max(capacity, 1) * stride, dtype=np.uint8)
+        olen = np.zeros(max(capacity, 1), dtype=np.uint16)
+        _check(lib.tulips_csum_segment_frames_host(self._h, ar.ptr, off.ptr, ln.ptr, n, mss,
+                                                   out.ctypes.data, stride, capacity,
+                                                   olen.ctypes.data, first.ctypes.data),
+               "tulips_csum_segment_frames_host")
+        return out, olen[:capacity], first
 
 
 def toeplitz(saddr: int, daddr: int, sport: int, dport: int, key: bytes,
