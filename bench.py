@@ -281,25 +281,17 @@ def main():
     parity = "ok" if all_ranks_ok(ok, dist, cdev) else "MISMATCH"
     shard_digests = gather_strings(digest, dist)
 
-    # exchange-inclusive figure (N>1, reported beside `value`): the K steps'
-    # results gathered to every rank — 16 batches x 65,536 x 2 B = 2 MiB per
-    # rank over RCCL — timed on its own and added to the compute time
+    # exchange-inclusive figures (N>1, reported beside `value`, never as it):
+    # the results all-gathered after the compute (sequential) and overlapped
+    # with it, the golden ZIPF batch split byte-balanced over the ranks, and
+    # data starting on GPU 0 scattered over xGMI
     exchange = None
+    multi = None
     if world > 1:
-        dist.barrier()
-        torch.cuda.synchronize()
-        tg0 = time.perf_counter()
-        gathered = gather_results(outs, dist, cdev)
-        torch.cuda.synchronize()
-        tg = max_over_ranks(time.perf_counter() - tg0, dist, cdev)
-        g_ok = all(fnv1a_u16(gathered[r * outs.numel():(r + 1) * outs.numel()]
-                             .cpu().numpy().view(np.uint16)) == shard_digests[r]
-                   for r in range(world)) if rank == 0 else True
-        exchange = {"op": "all_gather of the result words", "bytes_per_rank": outs.numel() * 2,
-                    "ms": round(tg * 1e3, 3),
-                    "value_exchange_inclusive": round(total_bytes / (t_max + tg) / GIB, 2),
-                    "parity": "ok" if g_ok else "MISMATCH"}
-        del gathered
+        exchange = exchange_sequential(torch, dist, cdev, outs, total_bytes, t_max,
+                                       shard_digests, rank, world)
+        multi = multi_rank_legs(torch, dist, csum, dev, cdev, stream, arena, outs,
+                                rank, world, args, shard_digests, total_bytes)
 
     result = {
         "metric": METRIC,
@@ -327,6 +319,7 @@ def main():
         "parity": parity,
         "shard_digests": shard_digests,
         "exchange": exchange,
+        "multi_gpu": multi,
         "wall_s_timed": round(t_wall, 4),
     }
 
@@ -367,6 +360,226 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def exchange_sequential(torch, dist, cdev, outs, total_bytes, t_max, shard_digests, rank,
+                        world):
+    """The K steps' results gathered to every rank after the compute - 16
+    batches x 65,536 x 2 B = 2 MiB per rank - timed on its own and added to
+    the compute time."""
+    from tulips_amd.shard import gather_results, max_over_ranks
+    dist.barrier()
+    torch.cuda.synchronize()
+    tg0 = time.perf_counter()
+    gathered = gather_results(outs, dist, cdev)
+    torch.cuda.synchronize()
+    tg = max_over_ranks(time.perf_counter() - tg0, dist, cdev)
+    g_ok = all(fnv1a_u16(gathered[r * outs.numel():(r + 1) * outs.numel()]
+                         .cpu().numpy().view(np.uint16)) == shard_digests[r]
+               for r in range(world)) if rank == 0 else True
+    return {"op": "all_gather of the result words, after the compute",
+            "bytes_per_rank": outs.numel() * 2, "ms": round(tg * 1e3, 3),
+            "value_exchange_inclusive": round(total_bytes / (t_max + tg) / GIB, 2),
+            "parity": "ok" if g_ok else "MISMATCH"}
+
+
+def _leg(fn, *a):
+    """Run one multi-rank side measurement; an exception becomes an error
+    entry (every rank runs the same code, so they fail alike)."""
+    try:
+        return fn(*a)
+    except Exception as e:  # noqa: BLE001 - reported, never hidden
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def multi_rank_legs(torch, dist, csum, dev, cdev, stream, arena, outs, rank, world, args,
+                    shard_digests, total_bytes):
+    # (under gloo, the one-GPU rehearsal, the collectives take the same CUDA
+    # tensors through host memory)
+    res = {"backend": args.dist_backend}
+    res["exchange_overlapped"] = _leg(exchange_overlapped, torch, dist, csum, cdev,
+                                      stream, arena, rank, world, args, shard_digests)
+    res["scatter_from_gpu0"] = _leg(scatter_leg, torch, dist, csum, dev, cdev, arena,
+                                    outs, rank, world)
+    res["zipf_byte_balanced"] = _leg(zipf_sharded_leg, torch, dist, csum, dev, cdev, stream,
+                                     rank, world)
+    return res
+
+
+def exchange_overlapped(torch, dist, csum, cdev, stream, arena, rank, world, args,
+                        shard_digests):
+    """Results all-gathered WHILE the next rotation computes: rotation r (16
+    launches, one per batch of the shard) writes result buffer r % 2, and the
+    all-gather of buffer r runs on a communication stream behind an event,
+    overlapping rotation r + 1; rotation r + 2 waits for that gather before
+    overwriting its buffer. Timed end to end (max over ranks) beside the same
+    rotations without the gathers."""
+    from tulips_amd.shard import max_over_ranks
+    fixed = csum.lib.tulips_csum_batch_fixed
+    batch_bytes = NSEG * SEG
+    base = arena.data_ptr()
+    bufs = [torch.empty(NBATCH * NSEG, dtype=torch.uint16, device=arena.device)
+            for _ in range(2)]
+    gath = [torch.empty(world * NBATCH * NSEG * 2, dtype=torch.uint8, device=arena.device)
+            for _ in range(2)]
+    side = [torch.cuda.Stream() for _ in range(PIPE)]
+    graphs = []
+    for k in range(2):
+        for b in range(NBATCH):     # warm (per-stream state outside the capture)
+            fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
+                  bufs[k].data_ptr() + b * NSEG * 2, NSEG, 0, stream.cuda_stream)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            main = torch.cuda.current_stream()
+            for sd in side:
+                sd.wait_stream(main)
+            for b in range(NBATCH):
+                fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
+                      bufs[k].data_ptr() + b * NSEG * 2, NSEG, 0,
+                      side[b % PIPE].cuda_stream)
+            for sd in side:
+                main.wait_stream(sd)
+        graphs.append(g)
+    comm = torch.cuda.Stream()
+    rot = max(4, args.steps // NBATCH)
+
+    def run(with_gather):
+        done = [None, None]
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for r in range(rot):
+            k = r % 2
+            if done[k] is not None:
+                stream.wait_event(done[k])
+            graphs[k].replay()
+            if with_gather:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                with torch.cuda.stream(comm):
+                    comm.wait_event(ev)
+                    dist.all_gather_into_tensor(gath[k], bufs[k].view(torch.uint8))
+                    de = torch.cuda.Event()
+                    de.record(comm)
+                done[k] = de if with_gather else None
+        torch.cuda.synchronize()
+        return max_over_ranks(time.perf_counter() - t0, dist, cdev)
+
+    t_compute = run(False)
+    t_both = run(True)
+    last = gath[(rot - 1) % 2].view(torch.uint16).cpu().numpy()
+    per = NBATCH * NSEG
+    ok = all(fnv1a_u16(last[r * per:(r + 1) * per]) == shard_digests[r]
+             for r in range(world)) if rank == 0 else True
+    from tulips_amd.shard import all_ranks_ok
+    ok = all_ranks_ok(ok, dist, cdev)
+    nbytes = float(world) * rot * NBATCH * batch_bytes
+    return {"op": "all_gather of each rotation's 2 MiB of result words on a comm stream, "
+                  "overlapping the next rotation's 16 launches (double-buffered results)",
+            "rotations": rot, "ms_compute_only": round(t_compute * 1e3, 3),
+            "ms_with_exchange": round(t_both * 1e3, 3),
+            "value_compute_only": round(nbytes / t_compute / GIB, 2),
+            "value_exchange_inclusive": round(nbytes / t_both / GIB, 2),
+            "exchange_hidden_frac": round(min(1.0, t_compute / t_both), 4),
+            "parity": "ok" if ok else "MISMATCH"}
+
+
+def scatter_leg(torch, dist, csum, dev, cdev, arena, outs, rank, world):
+    """Data starting on GPU 0: rank 0 holds `world` F1500
+    batches, RCCL scatters batch r to rank r over xGMI, every rank checksums
+    what it received; timed scatter + kernel (max over ranks). Parity: rank
+    r's results equal rank 0's own results for batch r of its shard."""
+    from tulips_amd.shard import all_ranks_ok, gather_strings, max_over_ranks
+    batch_bytes = NSEG * SEG
+    if world > NBATCH:
+        return {"skipped": "more ranks than batches per shard"}
+    recv = torch.empty(batch_bytes + 256, dtype=torch.uint8, device=dev)
+    out = torch.empty(NSEG, dtype=torch.uint16, device=dev)
+    chunks = [arena[b * batch_bytes:(b + 1) * batch_bytes] for b in range(world)] \
+        if rank == 0 else None
+    fixed = csum.lib.tulips_csum_batch_fixed
+    best = None
+    for _ in range(3):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dist.scatter(recv[:batch_bytes], chunks, src=0)
+        rc = fixed(recv.data_ptr(), SEG, SEG, None, None, None, out.data_ptr(), NSEG, 0,
+                   torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        t = max_over_ranks(time.perf_counter() - t0, dist, cdev)
+        if rc:
+            raise csum.CsumError(rc, "tulips_csum_batch_fixed")
+        best = t if best is None else min(best, t)
+    digs = gather_strings(fnv1a_u16(out.cpu().numpy().view(np.uint16)), dist)
+    ok = True
+    if rank == 0:
+        own = outs.cpu().numpy().view(np.uint16)
+        ok = all(digs[r] == fnv1a_u16(own[r * NSEG:(r + 1) * NSEG]) for r in range(world))
+    ok = all_ranks_ok(ok, dist, cdev)
+    return {"op": "dist.scatter (RCCL send/recv over xGMI) of one 98.3 MB F1500 batch per "
+                  "rank from GPU 0, then the kernel on each rank",
+            "bytes_moved": (world - 1) * batch_bytes, "ms": round(best * 1e3, 3),
+            "value_scatter_inclusive": round(world * batch_bytes / best / GIB, 2),
+            "parity": "ok" if ok else "MISMATCH"}
+
+
+def zipf_sharded_leg(torch, dist, csum, dev, cdev, stream, rank, world):
+    """A Zipf batch of world x 65,536 segments (the §8c length sequence,
+    continued: its first 65,536 segments and their bytes ARE the golden ZIPF
+    batch, configs[3]) split over the ranks by BYTES (tulips_csum_shard_plan):
+    each rank fills and checksums its contiguous shard of the global packed
+    arena (serial chain of launches, HIP events). Aggregate = all bytes /
+    slowest rank. Parity: the gathered results of the first 65,536 segments
+    equal the reference's ZIPF digest."""
+    from tulips_amd.shard import all_ranks_ok, byte_shard_for, max_over_ranks
+    lens = zipf_lengths(world * NSEG)
+    zb = int(lens.astype(np.int64).sum()) / world    # mean bytes per rank
+    bs = byte_shard_for(rank, world, lens)
+    ll = lens[bs.seg_begin:bs.seg_begin + bs.seg_count]
+    offs = np.zeros(len(ll), dtype=np.uint64)
+    if len(ll) > 1:
+        np.cumsum(ll[:-1], dtype=np.uint64, out=offs[1:])
+    az = torch.empty(bs.nbytes + 256, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(az, bs.nbytes, byte_off=bs.byte_offset)
+    doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    dlens = torch.from_numpy(ll.view(np.int16).copy()).to(dev)
+    out = torch.empty(max(1, len(ll)), dtype=torch.uint16, device=dev)
+    batch = csum.lib.tulips_csum_batch
+
+    def fz(i, st):
+        batch(az.data_ptr(), doffs.data_ptr(), dlens.data_ptr(), None, None, None,
+              out.data_ptr(), len(ll), 0, st)
+    fz(0, stream.cuda_stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = Timer(torch, stream)(fz, 40)
+    t_max = max_over_ranks(t, dist, cdev)
+    t_min = -max_over_ranks(-t, dist, cdev)
+    # per-rank byte spread of this plan vs a split by segment count
+    cnt_b = np.add.reduceat(lens.astype(np.int64), np.arange(0, len(lens), len(lens) // world))
+    plan = csum.shard_plan(lens, world)
+    byt_b = np.add.reduceat(lens.astype(np.int64), plan[:-1].astype(np.int64))
+    # parity over the golden arena: results of global segments [0, 65536)
+    cmax = int(max_over_ranks(float(len(ll)), dist, cdev))
+    pad = torch.zeros(cmax, dtype=torch.uint16, device=dev)
+    pad[:len(ll)] = out[:len(ll)]
+    from tulips_amd.shard import gather_results
+    allw = gather_results(pad, dist, cdev).cpu().numpy().view(np.uint16)
+    glob = np.concatenate([allw[r * cmax:r * cmax + int(plan[r + 1] - plan[r])]
+                           for r in range(world)])
+    gold = golden_digests().get("ZIPF", {}).get("fnv1a64")
+    ok = all_ranks_ok(fnv1a_u16(glob[:NSEG]) == gold, dist, cdev)
+    return {"workload": f"Zipf batch of {world} x 65,536 segments ({int(world * zb)} B), "
+                        "byte-balanced shards",
+            "shard_segments": int(bs.seg_count), "shard_bytes": int(bs.nbytes),
+            "us_per_launch_max": round(t_max * 1e6, 2),
+            "us_per_launch_min": round(t_min * 1e6, 2),
+            "value_GiBps": round(world * zb / t_max / GIB, 2),
+            "bytes_spread_byte_plan": int(byt_b.max() - byt_b.min()),
+            "bytes_spread_count_split": int(cnt_b.max() - cnt_b.min()),
+            "parity": "ok" if ok else "MISMATCH"}
 
 
 PIPE = 4   # graph branches for the "pipeline" figures (bench --streams default)

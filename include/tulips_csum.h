@@ -142,6 +142,42 @@ int tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
                            const uint32_t* dst, uint16_t* out, uint32_t n,
                            uint32_t mode);
 
+/* ---- several GPUs, one process ---------------------------- */
+/*
+ * Byte-balanced contiguous split of a batch into `nshards` shards: bounds
+ * (nshards + 1 entries) gets shard k = segments [bounds[k], bounds[k+1]),
+ * each holding about 1/nshards of the bytes (prefix sum of lengths; shard k
+ * starts at the first segment whose prefix reaches k/nshards of the total).
+ * lengths is a host array.
+ */
+int tulips_csum_shard_plan(const uint16_t* lengths, uint32_t n, uint32_t nshards,
+                           uint32_t* bounds);
+
+typedef struct tulips_csum_mctx tulips_csum_mctx;
+
+/* One host context (tulips_csum_ctx_create) per listed device, the CPUs
+ * shared among them; a device may be listed more than once (independent
+ * pipelines on one GPU). */
+int tulips_csum_mctx_create(const int* devices, uint32_t ndevices,
+                            uint64_t chunk_bytes, tulips_csum_mctx** ctx);
+int tulips_csum_mctx_destroy(tulips_csum_mctx* ctx);
+
+/* As the single-device *_host calls, over all devices at once: the batch is
+ * split by tulips_csum_shard_plan, shard k runs on devices[k], results are
+ * written in segment order (counters summed). Blocks until done. */
+int tulips_csum_mctx_batch_host(tulips_csum_mctx* ctx, const uint8_t* base,
+                                const uint64_t* offsets, const uint16_t* lengths,
+                                const uint16_t* seeds, const uint32_t* src,
+                                const uint32_t* dst, uint16_t* out, uint32_t n,
+                                uint32_t mode);
+int tulips_csum_mctx_validate_frames_host(tulips_csum_mctx* ctx,
+                                          const uint8_t* base,
+                                          const uint64_t* offsets,
+                                          const uint16_t* lengths, uint32_t n,
+                                          uint8_t* flags, uint32_t* counters);
+/* The shard bounds (ndevices + 1 entries) of the context's last call. */
+int tulips_csum_mctx_shard_bounds(const tulips_csum_mctx* ctx, uint32_t* bounds);
+
 /* ---- Toeplitz RSS hash -------------------------------- */
 /*
  * tulips::stack::utils::toeplitz (include/tulips/stack/Utils.h:25-28,

@@ -46,6 +46,9 @@ constexpr int NSLOTS = 3;
 // on the MI355X box, alternating builds).
 constexpr int MAX_PACK_THREADS = 16;
 
+} // namespace
+
+namespace tulips_amd {
 int
 pack_threads()
 {
@@ -60,6 +63,10 @@ pack_threads()
   }
   return n < 1 ? 1 : (n > MAX_PACK_THREADS ? MAX_PACK_THREADS : n);
 }
+} // namespace tulips_amd
+
+namespace {
+using tulips_amd::pack_threads;
 
 // Persistent workers for the staging copy (a thread per pack would cost
 // tens of microseconds per chunk to create). run(f) calls f(0..size()-1)
@@ -67,7 +74,7 @@ pack_threads()
 class PackPool
 {
 public:
-  PackPool() : n_(pack_threads())
+  explicit PackPool(int n) : n_(n < 1 ? 1 : n)
   {
     for (int t = 1; t < n_; ++t) {
       threads_.emplace_back([this, t] { worker(t); });
@@ -185,6 +192,7 @@ is_pinned(const void* p)
 
 struct tulips_csum_ctx
 {
+  explicit tulips_csum_ctx(int threads) : pool(threads) {}
   int device = 0;
   uint64_t chunk = DEFAULT_CHUNK;
   Slot slots[NSLOTS];
@@ -349,10 +357,11 @@ pack(PackPool& pool, Slot& s, const uint8_t* base, const uint64_t* offsets,
 
 } // namespace
 
-extern "C" {
-
+namespace tulips_amd {
+// tulips_csum_ctx_create with an explicit staging-copy thread count (the
+// multi-device context gives each device its share of the CPUs).
 int
-tulips_csum_ctx_create(int device, uint64_t chunk_bytes, tulips_csum_ctx** ctx)
+ctx_create(int device, uint64_t chunk_bytes, int threads, tulips_csum_ctx** ctx)
 {
   if (!ctx) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
@@ -376,7 +385,7 @@ tulips_csum_ctx_create(int device, uint64_t chunk_bytes, tulips_csum_ctx** ctx)
   }
   tulips_csum_ctx* c = nullptr;
   try {
-    c = new tulips_csum_ctx(); // starts the pack threads
+    c = new tulips_csum_ctx(threads); // starts the pack threads
   } catch (...) {
     c = nullptr;
   }
@@ -399,6 +408,16 @@ tulips_csum_ctx_create(int device, uint64_t chunk_bytes, tulips_csum_ctx** ctx)
   (void)hipSetDevice(prev);
   *ctx = c;
   return TULIPS_STATUS_OK;
+}
+
+} // namespace tulips_amd
+
+extern "C" {
+
+int
+tulips_csum_ctx_create(int device, uint64_t chunk_bytes, tulips_csum_ctx** ctx)
+{
+  return tulips_amd::ctx_create(device, chunk_bytes, pack_threads(), ctx);
 }
 
 int

@@ -134,6 +134,14 @@ _SIGNATURES = {
     "tulips_csum_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
                                                    _vp]),
     "tulips_csum_release_stream": (C.c_int, [_vp]),
+    "tulips_csum_shard_plan": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _vp]),
+    "tulips_csum_mctx_create": (C.c_int, [_vp, C.c_uint32, C.c_uint64, C.POINTER(_vp)]),
+    "tulips_csum_mctx_destroy": (C.c_int, [_vp]),
+    "tulips_csum_mctx_batch_host": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                              C.c_uint32, C.c_uint32]),
+    "tulips_csum_mctx_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32,
+                                                        _vp, _vp]),
+    "tulips_csum_mctx_shard_bounds": (C.c_int, [_vp, _vp]),
     "tulips_csum_generate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp]),
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
@@ -460,6 +468,81 @@ class HostContext:
                                                    olen.ctypes.data, first.ctypes.data),
                "tulips_csum_segment_frames_host")
         return out, olen[:capacity], first
+
+
+def shard_plan(lengths, nshards: int):
+    """Byte-balanced contiguous shard bounds (tulips_csum_shard_plan)."""
+    import numpy as np
+    ln = _host(lengths, np.uint16)
+    n = len(ln.keep)
+    bounds = np.zeros(nshards + 1, dtype=np.uint32)
+    _check(lib.tulips_csum_shard_plan(ln.ptr, n, nshards, bounds.ctypes.data),
+           "tulips_csum_shard_plan")
+    return bounds
+
+
+class MultiContext(HostContext):
+    """tulips_csum_mctx: host-resident batches split byte-balanced over
+    several devices (a device may repeat)."""
+
+    def __init__(self, devices, chunk_bytes: int = 0):
+        import numpy as np
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        h = C.c_void_p()
+        _check(lib.tulips_csum_mctx_create(devs.ctypes.data, len(devs), chunk_bytes,
+                                           C.byref(h)), "tulips_csum_mctx_create")
+        self._h = h
+        self.ndev = len(devs)
+
+    def close(self):
+        if self._h:
+            lib.tulips_csum_mctx_destroy(self._h)
+            self._h = None
+
+    def bounds(self):
+        import numpy as np
+        b = np.zeros(self.ndev + 1, dtype=np.uint32)
+        _check(lib.tulips_csum_mctx_shard_bounds(self._h, b.ctypes.data), "shard_bounds")
+        return b
+
+    def batch(self, arena, offsets, lengths, *, seeds=None, src=None, dst=None,
+              mode: int = RAW, out=None):
+        import numpy as np
+        ar = arena if isinstance(arena, int) else _host(arena, np.uint8)
+        base = ar if isinstance(ar, int) else ar.ptr
+        off = _host(offsets, np.uint64)
+        ln = _host(lengths, np.uint16)
+        n = len(off.keep)
+        if out is None:
+            out = np.empty(n, dtype=np.uint16)
+        sd, s, d = _host(seeds, np.uint16), _host(src, np.uint32), _host(dst, np.uint32)
+        _check(lib.tulips_csum_mctx_batch_host(self._h, base, off.ptr, ln.ptr, sd.ptr, s.ptr,
+                                               d.ptr, out.ctypes.data, n, mode),
+               "tulips_csum_mctx_batch_host")
+        return out
+
+    def validate_frames(self, arena, offsets, lengths, *, flags=None,
+                        with_counters: bool = False):
+        import numpy as np
+        ar = arena if isinstance(arena, int) else _host(arena, np.uint8)
+        base = ar if isinstance(ar, int) else ar.ptr
+        off = _host(offsets, np.uint64)
+        ln = _host(lengths, np.uint16)
+        n = len(off.keep)
+        if flags is None:
+            flags = np.empty(n, dtype=np.uint8)
+        cnt = np.zeros(4, dtype=np.uint32)
+        _check(lib.tulips_csum_mctx_validate_frames_host(
+            self._h, base, off.ptr, ln.ptr, n, flags.ctypes.data,
+            cnt.ctypes.data if with_counters else None),
+            "tulips_csum_mctx_validate_frames_host")
+        return (flags, cnt) if with_counters else flags
+
+    def generate_frames(self, *a, **k):
+        raise NotImplementedError("use HostContext for generation")
+
+    def segment_frames(self, *a, **k):
+        raise NotImplementedError("use HostContext for segmentation")
 
 
 def toeplitz(saddr: int, daddr: int, sport: int, dport: int, key: bytes,

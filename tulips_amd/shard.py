@@ -88,3 +88,31 @@ def gather_results(out, dist=None, device=None):
     dst = torch.empty(world * flat.numel(), dtype=torch.uint8, device=flat.device)
     dist.all_gather_into_tensor(dst, flat)
     return dst.view(out.dtype)
+
+
+@dataclass(frozen=True)
+class ByteShard:
+    """A rank's part of a variable-length batch, cut by the library's
+    byte-balanced plan (tulips_csum_shard_plan)."""
+    rank: int
+    world: int
+    seg_begin: int
+    seg_count: int
+    byte_offset: int    # offset of the shard's first segment in the packed arena
+    nbytes: int
+
+
+def byte_shard_for(rank: int, world: int, lengths) -> ByteShard:
+    """Contiguous shard `rank` of a packed batch with these lengths, balanced
+    by bytes ("balance by bytes for Zipf (prefix sum of
+    lengths)"); every rank computes the same plan locally, no exchange."""
+    import numpy as np
+    from tulips_amd import csum
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    lens = np.ascontiguousarray(lengths, dtype=np.uint16)
+    b = csum.shard_plan(lens, world)
+    i0, i1 = int(b[rank]), int(b[rank + 1])
+    pre = int(lens[:i0].astype(np.int64).sum())
+    nb = int(lens[i0:i1].astype(np.int64).sum())
+    return ByteShard(rank, world, i0, i1 - i0, pre, nb)
