@@ -22,6 +22,12 @@ extern "C" {
                                        segments (8/16/32/64), their chunks
                                        packed end to end, `unroll` 64-chunk
                                        windows in flight (2/4/8) */
+#define TULIPS_CSUM_KIND_BALANCED 4 /* variable only: a workgroup of `block`/64
+                                       waves (4 or 8) owns 8 segments per wave;
+                                       the workgroup's chunks are packed end to
+                                       end and split evenly over its waves,
+                                       `unroll` windows (2/4) per batch,
+                                       double-buffered; `group` must be 8 */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning

@@ -190,7 +190,14 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
               (group == 16 && unroll == 4 && (spw == 1 || spw == 2)) ||
               (group == 16 && unroll == 8 && spw == 1) ||
               (group == 32 && unroll == 4 && spw == 1));
+    case TULIPS_CSUM_KIND_BALANCED:
+      return variable && (group == 8 || group == 0) &&
+             (unroll == 2 || unroll == 4 || unroll == 6) && (spw == 1 || spw == 2);
     case TULIPS_CSUM_KIND_PACKED:
+      if (spw == 4) { // lane-parallel cursors: up to 32 segments, 2 or 4 windows
+        return variable && (group == 4 || group == 8 || group == 16 || group == 32) &&
+               (unroll == 2 || unroll == 4);
+      }
       return variable && (spw == 1 || spw == 2 || spw == 3) &&
              (((group == 4 || group == 6 || group == 12) && unroll == 4) ||
               ((group == 8) && (unroll == 2 || unroll == 4)) ||

@@ -692,6 +692,414 @@ launch_packed(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// VPACKED: the packed kernel's chunk space with lane-parallel cursors.
+//
+// rocprofv3 counters of csum_packed_kernel on the §8c ZIPF batch
+// (tools/pmc_var.sh): 462 VALU + 360 SALU instructions per wave for 5.3 KB,
+// waves stalled on instruction issue 41 % of their life (SQ_WAIT_INST_ANY)
+// vs 36 % on memory — with 8 waves per SIMD the launch is bound by issuing
+// the two scalar cursors' per-segment loops, not by HBM. Here both cursors
+// become a few vector instructions per 64-chunk window, whatever the number
+// of segments in it:
+//   * window -> address: lane j (chunk c = b + j) owns segment
+//     s(c) = #{k : P_k <= c} - 1 (the starts P_k sit in SGPRs; an empty
+//     segment shares its start with the next one and never wins), and takes
+//     D_s with two ds_bpermutes: address = D_s + 16c;
+//   * sums: the wave's running prefix R (inclusive scan, as before); lane k
+//     captures e_k = R(its last chunk) with one ds_bpermute in the window
+//     holding that chunk; after the last window sum_k = e_k - e_{k-1} (a DPP
+//     shift; e_{-1} = 0, and an empty segment repeats its predecessor's e).
+// Batches of U windows ping-pong between two register sets with every load
+// unconditional (a batch past T re-reads chunk T - 1 and is dropped), so at
+// each scan only the other set's U loads are newer (vmcnt(U)).
+// ---------------------------------------------------------------------------
+template<int S, int U, bool NT>
+__global__ __launch_bounds__(256, 8) void
+csum_vpacked_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
+                    const uint32_t* __restrict__ src,
+                    const uint32_t* __restrict__ dst, uint16_t* __restrict__ out,
+                    uint32_t* __restrict__ bad, uint32_t n, uint32_t mode,
+                    bool nt_store)
+{
+  static_assert(S >= 1 && S <= 32, "segment starts are held in SGPRs");
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(
+    (xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
+  const uintptr_t zero_chunk = reinterpret_cast<uintptr_t>(k_zero_chunk);
+  for (uint32_t g0 = wave * S; g0 < n; g0 += nwaves * S) {
+    const uint32_t seg = g0 + lane;
+    const bool mine = lane < uint32_t(S) && seg < n;
+    const uint32_t sk = mine ? seg : n - 1;
+    const uint32_t len = mine ? segs.length(sk) : 0u;
+    const uintptr_t sa = base + segs.off(sk);
+    const SideIn side = load_side(sk, seeds, src, dst, mode);
+    const uintptr_t a0 = sa & ~uintptr_t(15);
+    const uint32_t nch = len ? uint32_t((sa + len - a0 + 15) >> 4) : 0u;
+    const int head = int(sa - a0);
+    const int tail = nch ? int(sa + len - a0) - 16 * int(nch - 1) : 16;
+    const gchunk_ptr pf = reinterpret_cast<gchunk_ptr>(
+      (nch && head != 0) ? a0 : zero_chunk);
+    const gchunk_ptr pl = reinterpret_cast<gchunk_ptr>(
+      (nch && tail != 16) ? a0 + 16 * uintptr_t(nch - 1) : zero_chunk);
+    const u32x4 cfirst = load_chunk<NT>(pf);
+    const u32x4 clast = load_chunk<NT>(pl);
+    // ---- packed chunk space ------------------------------------------------
+    const uint32_t incl = wave_incl_scan(nch);
+    const uint32_t P = incl - nch;
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t Lst = incl - 1;
+    const uint64_t D = uint64_t(a0) - 16ull * P;
+    const int dlo = int(uint32_t(D)), dhi = int(uint32_t(D >> 32));
+    uint32_t ps[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      ps[k] = __builtin_amdgcn_readlane(P, k);
+    }
+    uint32_t run = 0;
+    uint32_t e = 0; // R at this lane's segment's last chunk
+    auto issue = [&](uint32_t w0, u32x4 (&v)[U]) {
+      uint64_t addr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t c = min(w0 + 64u * u + lane, T - 1u); // past T: re-read
+        uint32_t sidx = 0;
+#pragma unroll
+        for (int k = 1; k < S; ++k) {
+          sidx += c >= ps[k] ? 1u : 0u;
+        }
+        const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(int(sidx << 2), dlo));
+        const uint32_t hi = uint32_t(__builtin_amdgcn_ds_bpermute(int(sidx << 2), dhi));
+        addr[u] = ((uint64_t(hi) << 32) | lo) + 16ull * c;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(addr[u]));
+      }
+    };
+    auto consume = [&](uint32_t w0, const u32x4 (&v)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t b = w0 + 64u * u;
+        const uint32_t val = b + lane < T ? chunk_value(v[u]) : 0u;
+        const uint32_t r = wave_incl_scan(val) + run;
+        const uint32_t at = Lst - b;                 // wraps when outside
+        const uint32_t rv = uint32_t(__builtin_amdgcn_ds_bpermute(int(at << 2), int(r)));
+        e = at < 64u ? rv : e;
+        run = __builtin_amdgcn_readlane(r, 63);
+      }
+    };
+    if (T != 0) {
+      // (sched_barrier: hipcc otherwise hoists a set's next loads above the
+      // scan of its current ones, renaming into extra registers, and then
+      // waits for every load before issuing them)
+      u32x4 A[U], Bf[U];
+      issue(0, A);
+      issue(64u * U, Bf);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t w0 = 0;
+      while (true) {
+        consume(w0, A);
+        __builtin_amdgcn_sched_barrier(0);
+        w0 += 64u * U;
+        if (w0 >= T) {
+          break;
+        }
+        issue(w0 + 64u * U, A);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(w0, Bf);
+        __builtin_amdgcn_sched_barrier(0);
+        w0 += 64u * U;
+        if (w0 >= T) {
+          break;
+        }
+        issue(w0 + 64u * U, Bf);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // sum_k = e_k - e_{k-1}: lane k - 1's value one lane up (row_shr:1 within
+    // each row of 16, then the row boundary lanes from readlane)
+    uint32_t eprev = uint32_t(__builtin_amdgcn_update_dpp(0, int(e), 0x111, 0xf, 0xf, false));
+    if constexpr (S > 16) {
+      const uint32_t e15 = __builtin_amdgcn_readlane(e, 15);
+      eprev = lane == 16 ? e15 : eprev;
+    }
+    const uint32_t sum = e - eprev;
+    const uint32_t outside =
+      masked_value(cfirst, 0, head) + masked_value(clast, tail, 16);
+    if (mine) {
+      emit_with(seg, sum - outside, sa, len, side, out, bad, mode, nt_store);
+    }
+  }
+}
+
+template<int S, int U, bool NT>
+hipError_t
+launch_vpacked(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
+{
+  const uint64_t per_block = uint64_t(256 / 64) * S;
+  uint64_t blocks = (uint64_t(a.n) + per_block - 1) / per_block;
+  if (a.max_blocks && blocks > a.max_blocks) {
+    blocks = a.max_blocks;
+  }
+  if (blocks == 0) {
+    return hipSuccess;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_vpacked_kernel<S, U, NT>), dim3(uint32_t(blocks)), dim3(256), 0,
+                     stream, segs, a.seeds, a.src, a.dst, a.out, a.bad, a.n, a.mode,
+                     a.nt_store);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// BALANCED variable-length kernel: the packed chunk space of a whole
+// WORKGROUP, split evenly over its waves.
+//
+// With one wave per 8 Zipf segments the launch lasts as long as its heaviest
+// wave: the sum of 8 draws reaches 28.8 KB against a 5.3 KB mean, and such a
+// wave needs 4-5 dependent batches after the bulk of the chip's requests has
+// drained (the latency-bound tail of csum_packed_kernel). Here a workgroup of
+// NW waves owns 8*NW consecutive segments; their chunk lists are laid end to
+// end in one workgroup packed space of TB chunks, and wave w reads chunks
+// [w*TB/NW, (w+1)*TB/NW) with the packed kernel's window machinery. The
+// heaviest wave drops to 16.0 KB (NW = 4) / 10.6 KB (NW = 8) for the §8c Zipf
+// batch. A segment cut by a range boundary gets its partial sums from two or
+// more waves; they meet in LDS (one ds_add per touched segment per wave).
+//
+//   1. lane k < 8 of wave w: metadata of segment 8w + k, its boundary chunks
+//      (as the packed kernel), nch / chunk base into LDS, its LDS sum zeroed;
+//   2. barrier; every wave reads the workgroup's table (lane j = segment j,
+//      8*NW <= 64) and scans it (P_j, D_j = chunkbase_j - 16*P_j, last chunk);
+//   3. wave w walks its range in 64-chunk windows, U windows per batch,
+//      double-buffered; per-segment prefix differences as in the packed
+//      kernel; the open segment at the range end takes run - eprev;
+//   4. each lane adds its segment's partial to LDS; barrier; lane k < 8 of
+//      wave w takes out the boundary bytes and emits segment 8w + k.
+// ---------------------------------------------------------------------------
+// 8 waves per SIMD (= 32 per CU, the whole grid of a 65,536-segment batch
+// resident at once): the register budget is 64 VGPRs
+template<int NW, int U, bool NT, int PF>
+__global__ __launch_bounds__(64 * NW, 8) void
+csum_balanced_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
+                     const uint32_t* __restrict__ src,
+                     const uint32_t* __restrict__ dst, uint16_t* __restrict__ out,
+                     uint32_t* __restrict__ bad, uint32_t n, uint32_t mode,
+                     bool nt_store)
+{
+  constexpr uint32_t S = 8, B = S * NW;
+  static_assert(B <= 64, "the workgroup table lives in one wave's lanes");
+  // the table, and what the owners need back at the end (held in LDS, not in
+  // VGPRs, across the window loop: 8 waves per SIMD leave 64 VGPRs)
+  __shared__ uint32_t s_nch[B];
+  __shared__ uint64_t s_a0[B];
+  __shared__ uint32_t s_sum[B];
+  __shared__ uint32_t s_len[B];   // length | start-odd << 16
+  __shared__ uint32_t s_out[B];   // boundary bytes outside the segment
+  __shared__ SideIn s_side[B];
+  const uint32_t lane = threadIdx.x & 63;
+  // wave index as a scalar: the range [r0, r1) and the window loop derived
+  // from it must be wave-uniform (SGPRs), or hipcc builds an exec-masked loop
+  // whose buffer rotation waits for every load (vmcnt(0)) each iteration
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
+  const uintptr_t zero_chunk = reinterpret_cast<uintptr_t>(k_zero_chunk);
+  for (uint32_t blk = xcd_block(blockIdx.x, gridDim.x); blk * B < n; blk += gridDim.x) {
+    // ---- 1. own segments' metadata ----------------------------------------
+    // (__syncthreads() waits for every outstanding load of the wave, so
+    // nothing but the metadata may be in flight at the barrier: the boundary
+    // chunks are loaded after it, in front of the first windows)
+    gchunk_ptr pf, pl;
+    int head, tail;
+    {
+      const uint32_t seg = blk * B + w * S + lane;
+      const bool mine = lane < S && seg < n;
+      const uint32_t sk = mine ? seg : n - 1;
+      const uint32_t len = mine ? segs.length(sk) : 0u;
+      const uintptr_t sa = base + segs.off(sk);
+      const SideIn side = load_side(sk, seeds, src, dst, mode);
+      const uintptr_t a0 = sa & ~uintptr_t(15);
+      const uint32_t nch = len ? uint32_t((sa + len - a0 + 15) >> 4) : 0u;
+      head = int(sa - a0);
+      tail = nch ? int(sa + len - a0) - 16 * int(nch - 1) : 16;
+      pf = reinterpret_cast<gchunk_ptr>((nch && head != 0) ? a0 : zero_chunk);
+      pl = reinterpret_cast<gchunk_ptr>(
+        (nch && tail != 16) ? a0 + 16 * uintptr_t(nch - 1) : zero_chunk);
+      if (lane < S) {
+        const uint32_t j = w * S + lane;
+        s_nch[j] = nch;
+        s_a0[j] = uint64_t(a0);
+        s_sum[j] = 0u;
+        s_len[j] = len | (uint32_t(sa & 1) << 16);
+        s_side[j] = side;
+      }
+    }
+    __syncthreads();
+    // ---- 2. the workgroup's packed space ----------------------------------
+    const uint32_t tn = lane < B ? s_nch[lane] : 0u;
+    const uint32_t incl = wave_incl_scan(tn);
+    const uint32_t P = incl - tn;
+    const uint32_t TB = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t Lst = incl - 1;
+    const uint64_t D = (lane < B ? s_a0[lane] : 0ull) - 16ull * P;
+    const uint32_t r0 = uint32_t((uint64_t(TB) * w) / NW);
+    const uint32_t r1 = uint32_t((uint64_t(TB) * (w + 1)) / NW);
+    // segments that end inside or after this range, in packed order
+    const uint64_t live = __ballot(tn != 0 && incl > r0);
+    uint64_t pend_start = live, pend_end = live;
+    uint64_t dcur = uint64_t(zero_chunk);
+    uint32_t run = 0, eprev = 0;
+    uint32_t part = 0;                               // this wave's share, lane j
+    auto issue = [&](uint32_t w0, u32x4 (&v)[U]) {
+      uint64_t addr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t b = w0 + 64u * u;
+        uint64_t dl = dcur;
+        while (pend_start) {
+          const uint32_t k = uint32_t(__builtin_ctzll(pend_start));
+          const uint32_t pk = __builtin_amdgcn_readlane(P, k);
+          // segments starting at r1 or later belong to the next wave: their
+          // D must not reach the lanes clamped to chunk r1 - 1
+          if (pk >= b + 64u || pk >= r1) {
+            break;
+          }
+          pend_start &= pend_start - 1;
+          const uint64_t dk = readlane64(D, k);
+          dl = lane + b >= pk ? dk : dl;
+          dcur = dk;
+        }
+        const uint32_t c = min(b + lane, r1 - 1u);  // past r1: re-read, dropped
+        addr[u] = dl + 16ull * c;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(addr[u]));
+      }
+    };
+    auto consume = [&](uint32_t w0, const u32x4 (&v)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t b = w0 + 64u * u;
+        const uint32_t val = b + lane < r1 ? chunk_value(v[u]) : 0u;
+        const uint32_t r = wave_incl_scan(val) + run;
+        while (pend_end) {
+          const uint32_t k = uint32_t(__builtin_ctzll(pend_end));
+          const uint32_t lk = __builtin_amdgcn_readlane(Lst, k);
+          if (lk >= b + 64u || lk >= r1) {
+            break;
+          }
+          pend_end &= pend_end - 1;
+          const uint32_t e = __builtin_amdgcn_readlane(r, lk - b);
+          part = lane == k ? e - eprev : part;
+          eprev = e;
+        }
+        run = __builtin_amdgcn_readlane(r, 63);
+      }
+    };
+    // the boundary chunks are older than the windows: their outside bytes
+    // are taken right after the first batch is issued (vmcnt(U)), so they do
+    // not occupy 8 VGPRs through the loop
+    const u32x4 cfirst = load_chunk<NT>(pf);
+    const u32x4 clast = load_chunk<NT>(pl);
+    auto retire_boundary = [&]() {
+      if (lane < S) {
+        s_out[w * S + lane] =
+          masked_value(cfirst, 0, head) + masked_value(clast, tail, 16);
+      }
+    };
+    if (r1 > r0 && PF == 0) {
+      // one batch of U windows at a time
+      uint32_t w0 = r0;
+      u32x4 A[U];
+      issue(w0, A);
+      retire_boundary();
+      while (true) {
+        consume(w0, A);
+        w0 += 64u * U;
+        if (w0 >= r1) {
+          break;
+        }
+        issue(w0, A);
+      }
+    } else if (r1 > r0) {
+      // Ping-pong buffers A/B with every batch load unconditional: at each
+      // consume the other buffer's U loads are the only newer ones in flight
+      // (vmcnt(U), no drain), and no register copy between buffers forces a
+      // wait (a cur = nxt rotation made hipcc wait for nxt at every latch).
+      // A batch past r1 re-reads chunk r1 - 1 (merged into one line) and is
+      // dropped.
+      u32x4 A[U], Bf[U];
+      issue(r0, A);
+      retire_boundary();
+      issue(r0 + 64u * U, Bf);
+      uint32_t w0 = r0;
+      while (true) {
+        consume(w0, A);
+        w0 += 64u * U;
+        if (w0 >= r1) {
+          break;
+        }
+        issue(w0 + 64u * U, A);
+        consume(w0, Bf);
+        w0 += 64u * U;
+        if (w0 >= r1) {
+          break;
+        }
+        issue(w0 + 64u * U, Bf);
+      }
+    } else {
+      retire_boundary();
+    }
+    // the segment still open at the range end continues in the next wave
+    if (r1 > r0 && pend_end) {
+      const uint32_t k = uint32_t(__builtin_ctzll(pend_end));
+      if (__builtin_amdgcn_readlane(P, k) < r1) {
+        part = lane == k ? run - eprev : part;
+      }
+    }
+    // ---- 4. partials meet in LDS; owners finish -----------------------------
+    if (lane < B && part != 0u) {
+      atomicAdd(&s_sum[lane], part);
+    }
+    __syncthreads();
+    {
+      const uint32_t j = w * S + lane;
+      const uint32_t seg = blk * B + j;
+      if (lane < S && seg < n) {
+        const uint32_t lw = s_len[j];
+        // emit_with reads only the start's parity from the address
+        emit_with(seg, s_sum[j] - s_out[j], uintptr_t(lw >> 16), lw & 0xffffu, s_side[j],
+                  out, bad, mode, nt_store);
+      }
+    }
+    if (blk + gridDim.x < (n + B - 1) / B) {
+      __syncthreads(); // the table is rewritten by the next iteration
+    }
+  }
+}
+
+template<int NW, int U, bool NT, int PF>
+hipError_t
+launch_balanced(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
+{
+  constexpr uint64_t B = 8 * NW;
+  uint64_t blocks = (uint64_t(a.n) + B - 1) / B;
+  if (a.max_blocks && blocks > a.max_blocks) {
+    blocks = a.max_blocks;
+  }
+  if (blocks == 0) {
+    return hipSuccess;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_balanced_kernel<NW, U, NT, PF>), dim3(uint32_t(blocks)),
+                     dim3(64 * NW), 0, stream, segs, a.seeds, a.src, a.dst, a.out, a.bad,
+                     a.n, a.mode, a.nt_store);
+  return hipGetLastError();
+}
+
 template<int GS, int US, int UL, int SPS, bool NT>
 hipError_t
 launch_hybrid(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
@@ -782,6 +1190,19 @@ tulips_csum_stamps_count()
 }
 #endif
 
+// PACKED sps = 4: the lane-parallel-cursor form (csum_vpacked_kernel)
+template<int S, int U>
+hipError_t
+vpacked(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
+{
+  if constexpr (S > 32 || U > 4) {
+    return hipErrorInvalidValue;
+  } else {
+    return a.nontemporal ? launch_vpacked<S, U, true>(segs, a, stream)
+                         : launch_vpacked<S, U, false>(segs, a, stream);
+  }
+}
+
 hipError_t
 launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,
              const LaunchArgs& a, hipStream_t stream)
@@ -800,6 +1221,9 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
     // spw = 2: double-buffered (next windows in flight while scanning)
 #define TCS_PCASE(S_, U_)                                                      \
   if (a.group == S_ && a.unroll == U_) {                                       \
+    if (a.spw == 4) {                                                          \
+      return vpacked<S_, U_>(segs, a, stream);                                 \
+    }                                                                          \
     if (a.spw == 3) {                                                          \
       return a.nontemporal ? launch_packed<S_, U_, true, 2>(segs, a, stream)   \
                            : launch_packed<S_, U_, false, 2>(segs, a, stream); \
@@ -824,6 +1248,27 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
     TCS_PCASE(64, 4)
     TCS_PCASE(64, 8)
 #undef TCS_PCASE
+    return hipErrorInvalidValue;
+  }
+  if (a.kind == TULIPS_CSUM_KIND_BALANCED) {
+    // block = 64 * waves per workgroup, unroll = windows per batch
+    const int nw = a.block / 64;
+#define TCS_BCASE(NW_, U_)                                                     \
+  if (nw == NW_ && a.unroll == U_) {                                           \
+    if (a.spw == 2) {                                                          \
+      return a.nontemporal ? launch_balanced<NW_, U_, true, 1>(segs, a, stream)  \
+                           : launch_balanced<NW_, U_, false, 1>(segs, a, stream); \
+    }                                                                          \
+    return a.nontemporal ? launch_balanced<NW_, U_, true, 0>(segs, a, stream)  \
+                         : launch_balanced<NW_, U_, false, 0>(segs, a, stream); \
+  }
+    TCS_BCASE(4, 2)
+    TCS_BCASE(4, 4)
+    TCS_BCASE(4, 6)
+    TCS_BCASE(8, 2)
+    TCS_BCASE(8, 4)
+    TCS_BCASE(8, 6)
+#undef TCS_BCASE
     return hipErrorInvalidValue;
   }
   if (a.kind == TULIPS_CSUM_KIND_HYBRID) {

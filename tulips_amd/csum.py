@@ -58,7 +58,7 @@ def _check(rc: int, what: str) -> None:
     raise CsumError(rc, f"{what} [{detail}]" if detail else what)
 
 
-KIND_DEFAULT, KIND_SUBGROUP, KIND_HYBRID, KIND_PACKED = 0, 1, 2, 3
+KIND_DEFAULT, KIND_SUBGROUP, KIND_HYBRID, KIND_PACKED, KIND_BALANCED = 0, 1, 2, 3, 4
 
 
 class Tuning(C.Structure):
