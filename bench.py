@@ -698,8 +698,57 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                          "parity": "ok" if fnv1a_u16(out) == gold.get("F1500", {}).get(
                              "fnv1a64") else "MISMATCH"}
     ex["e2e_host_F1500"] = e2e
+    ex["burst_latency_host"] = burst_latency(torch, csum)
     ex.update(frame_extras(torch, csum, dev, timer))
     return ex
+
+
+BURSTS = (1, 64, 1024)
+
+
+def burst_frames(nf):
+    """nf TCP frames of 1514 B (checksums generated, so they verify) in 2 KiB
+    host slots, as one receive poll burst: (arena, offsets, lengths)."""
+    from tulips_amd import csum
+    slot = 2048
+    rng = np.random.default_rng(nf)
+    ar = rng.integers(0, 256, nf * slot, dtype=np.uint8)
+    v = ar.reshape(nf, slot)
+    for off, val in ((12, 0x08), (13, 0), (14, 0x45), (15, 0), (16, SEG >> 8),
+                     (17, SEG & 0xFF), (20, 0x40), (21, 0), (23, 6), (46, 0x50)):
+        v[:, off] = val
+    offs = np.arange(nf, dtype=np.uint64) * np.uint64(slot)
+    lens = np.full(nf, SEG + 14, np.uint16)
+    with csum.HostContext(0) as ctx:
+        ctx.generate_frames(ar, offs, lens)
+    return ar, offs, lens
+
+
+def burst_latency(torch, csum):
+    """What one receive poll burst costs on the GPU path the gpucsum decorator
+    takes (tulips_csum_validate_frames_host: pinned staging, H2D, one launch,
+    D2H of the flags), per burst size, median of repeated calls. The reference
+    verifies each frame on the CPU as it arrives (ipv4/Processor.cpp:94-103,
+    tcpv4/Processor.cpp:121-131); its cost for the same bursts is in
+    cpu_baseline.burst_latency."""
+    res = {}
+    with csum.HostContext(torch.cuda.current_device(), chunk_bytes=4 << 20) as ctx:
+        for nf in BURSTS:
+            ar, offs, lens = burst_frames(nf)
+            pinned = torch.from_numpy(ar).pin_memory()
+            flags = np.empty(nf, np.uint8)
+            ts = []
+            for i in range(300 if nf < 1024 else 100):
+                t0 = time.perf_counter()
+                ctx.validate_frames(pinned.data_ptr(), offs, lens, flags=flags)
+                ts.append(time.perf_counter() - t0)
+            res[str(nf)] = {"us_per_burst": round(float(np.median(ts)) * 1e6, 2),
+                            "us_p99": round(float(np.percentile(ts, 99)) * 1e6, 2),
+                            "ns_per_frame": round(float(np.median(ts)) * 1e9 / nf, 1),
+                            "parity": "ok" if bool((flags == 0x0F).all()) else "MISMATCH"}
+    return {"workload": "TCP frames of 1514 B in 2 KiB pinned host slots, one "
+                        "tulips_csum_validate_frames_host call per burst (the gpucsum "
+                        "decorator's path)", "bursts": res}
 
 
 def rate_entry(alg_bytes, t, **kw):
@@ -836,6 +885,17 @@ def frame_extras(torch, csum, dev, timer):
     return ex
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(arena, batch_bytes, seconds):
     """The reference CPU checksum (oracle/_ref: the reference's own src/stack
     compiled with -O3 -mssse3), else the C restatement, on this box's cores,
@@ -868,6 +928,32 @@ def cpu_baseline(arena, batch_bytes, seconds):
            "sample": f"F1500 batch 0 (65,536 x 1500 B = 98.3 MB) copied to host; "
                      f"{nN} passes on {threads} pinned threads + {n1} passes on 1 "
                      f"thread, ~{seconds:.1f} s wall each; g++ -O3 -mssse3"}
+    res["cpu_model"] = cpu_model()
+    # the reference's per-frame receive verification over the same bursts as
+    # extras.burst_latency_host: ipv4::checksum of each header and the tcpv4
+    # checksum of each segment (its own build), one thread, as the stack's
+    # poll loop runs it
+    lat = {}
+    for nf in BURSTS:
+        far, foffs, flens = burst_frames(nf)
+        ip_offs, tcp_offs = foffs + np.uint64(14), foffs + np.uint64(34)
+        ip_lens = np.full(nf, 20, np.uint16)
+        tcp_lens = (flens - 34).astype(np.uint16)
+        src = far[(foffs + 26).astype(np.int64)[:, None] + np.arange(4)].copy().view("<u4")[:, 0]
+        dst = far[(foffs + 30).astype(np.int64)[:, None] + np.arange(4)].copy().view("<u4")[:, 0]
+        ts = []
+        for i in range(200 if nf < 1024 else 50):
+            t0 = time.perf_counter()
+            a = impl.batch(far, ip_offs, ip_lens, mode=1)
+            b = impl.batch(far, tcp_offs, tcp_lens, src=src, dst=dst, mode=2)
+            ts.append(time.perf_counter() - t0)
+        ok = bool((a == 0xFFFF).all() and (b == 0xFFFF).all())
+        lat[str(nf)] = {"us_per_burst": round(float(np.median(ts)) * 1e6, 2),
+                        "ns_per_frame": round(float(np.median(ts)) * 1e9 / nf, 1),
+                        "parity": "ok" if ok else "MISMATCH"}
+    res["burst_latency"] = {"what": "reference ipv4 + tcpv4 checksum verification of each "
+                                    "frame of the burst, 1 thread (includes one ctypes "
+                                    "call per protocol per burst)", "bursts": lat}
     if kind == "reference" and Reference.available(REF_CLANG_SO):
         # the same reference sources built with clang, the compiler the
         # reference's CMake prefers (CMakeLists.txt:20-21)

@@ -34,9 +34,10 @@ def run():
     geoms = {"packed": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                    block=256, sps=2),
              "balanced": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=2, nontemporal=1,
-                                     block=256, sps=2)}
-    shapes = {"zipf": bench.zipf_lengths(N), "v64": np.full(N, 64, np.uint16),
-              "v668": np.full(N, 668, np.uint16)}
+                                     block=256, sps=2),
+             "vpacked": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=2, nontemporal=1,
+                                    block=256, sps=4)}
+    shapes = {"zipf": bench.zipf_lengths(N)}
     out = torch.empty(N, dtype=torch.uint16, device=dev)
     order = []
     for sname, lens in shapes.items():
@@ -75,7 +76,8 @@ def summarise(path):
         per.setdefault((disp, k), {})[r["Counter_Name"]] = float(r["Counter_Value"])
     out = {}
     for (disp, k), c in sorted(per.items(), key=lambda x: int(x[0][0])):
-        kk = ("balanced" if "balanced" in k else "packed" if "packed" in k else
+        kk = ("balanced" if "balanced" in k else "vpacked" if "vpacked" in k else
+              "packed" if "packed" in k else
               "fixed" if "csum_kernel" in k else k[:40])
         out.setdefault(kk, []).append(c)
     for kk, lst in out.items():

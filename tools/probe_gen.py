@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Launch time vs batch size for the variable-length kernels on Zipf lengths
+(the first n of the §8c sequence): a jump where the grid outgrows one
+resident generation of waves (8 per SIMD) shows a second generation."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from tulips_amd import csum  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream()
+    timer = bench.Timer(torch, stream)
+    lib = csum.lib
+    NB = 4
+    NMAX = 98304
+    lens_all = bench.zipf_lengths(NMAX)
+    geoms = {"packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
+                                        block=256, sps=2),
+             "vpacked8x2": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=2, nontemporal=1,
+                                       block=256, sps=4),
+             "vpacked16x2": csum.Tuning(kind=csum.KIND_PACKED, group=16, unroll=2, nontemporal=1,
+                                        block=256, sps=4),
+             "bal8w_u4pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=4, nontemporal=1,
+                                       block=512, sps=2),
+             "bal8w_u2pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=2, nontemporal=1,
+                                       block=512, sps=2),
+             "bal4w_u4pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=4, nontemporal=1,
+                                       block=256, sps=2),
+             "bal4w_u2pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=2, nontemporal=1,
+                                       block=256, sps=2)}
+    if os.environ.get("PROBE_UNIFORM"):
+        lens_all = np.full(NMAX, int(os.environ["PROBE_UNIFORM"]), np.uint16)
+    out = torch.empty(NB * NMAX, dtype=torch.uint16, device=dev)
+    for n in (1024, 8192, 32768, 65536, 98304):
+        lens = lens_all[:n]
+        offs = np.zeros(n, np.uint64)
+        np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+        nb = int(lens.astype(np.int64).sum())
+        arena = torch.empty(NB * nb + 256, dtype=torch.uint8, device=dev)
+        csum.fill_splitmix(arena, NB * nb)
+        doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        dlens = torch.from_numpy(lens.view(np.int16)).to(dev)
+        row = {"n": n, "bytes": nb}
+        for gname, t in geoms.items():
+            def fn(i, sh, t=t):
+                b = i % NB
+                assert lib.tulips_csum_batch_tuned(arena.data_ptr() + b * nb, doffs.data_ptr(),
+                                                   dlens.data_ptr(), None, None, None,
+                                                   out.data_ptr() + b * n * 2, n, 0, t, sh) == 0
+            for i in range(NB):
+                fn(i, stream.cuda_stream)
+            tm = float(np.median([timer(fn, 64) for _ in range(3)]))
+            row[gname] = round(tm * 1e6, 2)
+        print(json.dumps(row), flush=True)
+        del arena
+
+
+if __name__ == "__main__":
+    main()

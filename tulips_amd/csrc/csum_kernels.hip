@@ -692,6 +692,17 @@ launch_packed(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
   return hipGetLastError();
 }
 
+// Workgroup barrier for LDS hand-offs only: the wave's LDS operations are
+// complete (lgkmcnt(0)), its vector-memory loads may still be in flight.
+// __syncthreads() would also wait for every outstanding global load
+// (vmcnt(0)), i.e. for the slowest of them, at each barrier.
+__device__ __forceinline__ void
+lds_barrier()
+{
+  __builtin_amdgcn_s_waitcnt(0xc07f); // vmcnt(63) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
+
 // ---------------------------------------------------------------------------
 // VPACKED: the packed kernel's chunk space with lane-parallel cursors.
 //
@@ -729,6 +740,9 @@ csum_vpacked_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
   const uintptr_t zero_chunk = reinterpret_cast<uintptr_t>(k_zero_chunk);
+#ifdef TULIPS_CSUM_STAMPS
+  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (uint32_t g0 = wave * S; g0 < n; g0 += nwaves * S) {
     const uint32_t seg = g0 + lane;
     const bool mine = lane < uint32_t(S) && seg < n;
@@ -792,31 +806,25 @@ csum_vpacked_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
       }
     };
     if (T != 0) {
-      // (sched_barrier: hipcc otherwise hoists a set's next loads above the
-      // scan of its current ones, renaming into extra registers, and then
-      // waits for every load before issuing them)
-      u32x4 A[U], Bf[U];
+      // pairs of batches, nothing in flight across a loop edge or a join
+      // (see csum_balanced_kernel)
+      u32x4 A[U];
       issue(0, A);
-      issue(64u * U, Bf);
-      __builtin_amdgcn_sched_barrier(0);
-      uint32_t w0 = 0;
-      while (true) {
-        consume(w0, A);
-        __builtin_amdgcn_sched_barrier(0);
-        w0 += 64u * U;
-        if (w0 >= T) {
-          break;
+      if (64u * U < T) {
+        u32x4 Bf[U];
+        issue(64u * U, Bf);
+        consume(0, A);
+        consume(64u * U, Bf);
+        for (uint32_t w0 = 128u * U; w0 < T; w0 += 128u * U) {
+          issue(w0, A);
+          issue(w0 + 64u * U, Bf);
+          consume(w0, A);
+          if (w0 + 64u * U < T) {
+            consume(w0 + 64u * U, Bf);
+          }
         }
-        issue(w0 + 64u * U, A);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(w0, Bf);
-        __builtin_amdgcn_sched_barrier(0);
-        w0 += 64u * U;
-        if (w0 >= T) {
-          break;
-        }
-        issue(w0 + 64u * U, Bf);
-        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        consume(0, A);
       }
     }
     // sum_k = e_k - e_{k-1}: lane k - 1's value one lane up (row_shr:1 within
@@ -833,6 +841,9 @@ csum_vpacked_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
       emit_with(seg, sum - outside, sa, len, side, out, bad, mode, nt_store);
     }
   }
+#ifdef TULIPS_CSUM_STAMPS
+  stamp_wave(stamp0);
+#endif
 }
 
 template<int S, int U, bool NT>
@@ -906,9 +917,12 @@ csum_balanced_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uintptr_t base = reinterpret_cast<uintptr_t>(segs.base);
   const uintptr_t zero_chunk = reinterpret_cast<uintptr_t>(k_zero_chunk);
+#ifdef TULIPS_CSUM_STAMPS
+  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (uint32_t blk = xcd_block(blockIdx.x, gridDim.x); blk * B < n; blk += gridDim.x) {
     // ---- 1. own segments' metadata ----------------------------------------
-    // (__syncthreads() waits for every outstanding load of the wave, so
+    // (lds_barrier() waits for every outstanding load of the wave, so
     // nothing but the metadata may be in flight at the barrier: the boundary
     // chunks are loaded after it, in front of the first windows)
     gchunk_ptr pf, pl;
@@ -936,7 +950,7 @@ csum_balanced_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
         s_side[j] = side;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // ---- 2. the workgroup's packed space ----------------------------------
     const uint32_t tn = lane < B ? s_nch[lane] : 0u;
     const uint32_t incl = wave_incl_scan(tn);
@@ -1010,45 +1024,30 @@ csum_balanced_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
           masked_value(cfirst, 0, head) + masked_value(clast, tail, 16);
       }
     };
-    if (r1 > r0 && PF == 0) {
-      // one batch of U windows at a time
-      uint32_t w0 = r0;
+    if (r1 > r0) {
+      // Pairs of batches: A and B (U windows each) are issued back to back
+      // and scanned in order, so A's scan waits vmcnt(U) while B is still in
+      // flight; no load is in flight across a loop edge or a branch join (a
+      // loop-carried buffer made hipcc wait for every load at the loop
+      // header). A wave's range of up to 2U windows costs one round trip.
       u32x4 A[U];
-      issue(w0, A);
-      retire_boundary();
-      while (true) {
-        consume(w0, A);
-        w0 += 64u * U;
-        if (w0 >= r1) {
-          break;
-        }
-        issue(w0, A);
-      }
-    } else if (r1 > r0) {
-      // Ping-pong buffers A/B with every batch load unconditional: at each
-      // consume the other buffer's U loads are the only newer ones in flight
-      // (vmcnt(U), no drain), and no register copy between buffers forces a
-      // wait (a cur = nxt rotation made hipcc wait for nxt at every latch).
-      // A batch past r1 re-reads chunk r1 - 1 (merged into one line) and is
-      // dropped.
-      u32x4 A[U], Bf[U];
       issue(r0, A);
       retire_boundary();
-      issue(r0 + 64u * U, Bf);
-      uint32_t w0 = r0;
-      while (true) {
-        consume(w0, A);
-        w0 += 64u * U;
-        if (w0 >= r1) {
-          break;
+      if (r0 + 64u * U < r1) {
+        u32x4 Bf[U];
+        issue(r0 + 64u * U, Bf);
+        consume(r0, A);
+        consume(r0 + 64u * U, Bf);
+        for (uint32_t w0 = r0 + 128u * U; w0 < r1; w0 += 128u * U) {
+          issue(w0, A);
+          issue(w0 + 64u * U, Bf);   // past r1: re-reads chunk r1 - 1, dropped
+          consume(w0, A);
+          if (w0 + 64u * U < r1) {
+            consume(w0 + 64u * U, Bf);
+          }
         }
-        issue(w0 + 64u * U, A);
-        consume(w0, Bf);
-        w0 += 64u * U;
-        if (w0 >= r1) {
-          break;
-        }
-        issue(w0 + 64u * U, Bf);
+      } else {
+        consume(r0, A);
       }
     } else {
       retire_boundary();
@@ -1064,7 +1063,7 @@ csum_balanced_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
     if (lane < B && part != 0u) {
       atomicAdd(&s_sum[lane], part);
     }
-    __syncthreads();
+    lds_barrier();
     {
       const uint32_t j = w * S + lane;
       const uint32_t seg = blk * B + j;
@@ -1076,9 +1075,12 @@ csum_balanced_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
       }
     }
     if (blk + gridDim.x < (n + B - 1) / B) {
-      __syncthreads(); // the table is rewritten by the next iteration
+      lds_barrier(); // the table is rewritten by the next iteration
     }
   }
+#ifdef TULIPS_CSUM_STAMPS
+  stamp_wave(stamp0);
+#endif
 }
 
 template<int NW, int U, bool NT, int PF>
@@ -1337,17 +1339,20 @@ fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t nbytes, uint64_t seed,
 }
 
 // Plain streaming read of [p, p+nbytes) (16-byte chunks, nbytes % 16 == 0):
-// the calibration ceiling for the checksum kernel's HBM read rate.
+// the calibration ceiling for the checksum kernels' HBM read rate. It reads
+// exactly as the fastest checksum geometry does (the F9000 kernel: one wave
+// per contiguous 12 KiB tile = 64 lanes x 12 nt dwordx4 loads issued back to
+// back, 256-thread blocks in the XCD-clustered order of csum_common.h) and
+// only XORs what it loaded, so it bounds that kernel from above.
 __global__ __launch_bounds__(256) void
 stream_read_kernel(uintptr_t base, uint64_t nchunks,
                    uint32_t* __restrict__ sink)
 {
-  // Each wave streams contiguous 8 KiB tiles: 8 nt dwordx4 loads per lane
-  // (1 KiB per wave-instruction) issued back to back, grid-stride over tiles.
-  constexpr int U = 8;
+  constexpr int U = 12;
   const gchunk_ptr p = reinterpret_cast<gchunk_ptr>(base);
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t wave =
+    (uint64_t(xcd_block(blockIdx.x, gridDim.x)) * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = (uint64_t(gridDim.x) * blockDim.x) >> 6;
   const uint64_t ntiles = nchunks / (64 * U);
   uint32_t x = 0;
@@ -1402,8 +1407,10 @@ launch_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
   if (nchunks == 0) {
     return hipSuccess;
   }
-  uint64_t blocks = (nchunks + 255) / 256;
-  const uint64_t cap = max_blocks ? max_blocks : 4096;
+  // one 12 KiB tile per wave (4 waves per block), as the checksum kernel's
+  // one 9000 B segment per wave: no grid-stride cap by default
+  uint64_t blocks = (nchunks + 4 * 64 * 12 - 1) / (4 * 64 * 12);
+  const uint64_t cap = max_blocks ? max_blocks : (1u << 30);
   if (blocks > cap) {
     blocks = cap;
   }
