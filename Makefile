@@ -16,7 +16,7 @@ HDRS = tulips_amd/csrc/csum_common.h tulips_amd/csrc/csum_launch.h \
        include/tulips_csum.h include/tulips_csum_util.h
 OBJS = $(patsubst tulips_amd/csrc/%.hip,build/%.o,$(SRCS))
 
-.PHONY: all lib oracle clean asm stamps xcd_ab
+.PHONY: all lib oracle clean asm stamps xcd_ab spandiag
 
 all: lib oracle
 
@@ -46,6 +46,16 @@ xcd_ab: $(foreach c,$(XCD_AB),tools/libcsum_xcd$(c).so)
 
 tools/libcsum_xcd%.so: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DTULIPS_XCD_CLUSTER=$* -shared -o $@ $(SRCS)
+
+# Diagnostic builds of the arena-span kernel that stop after staging the
+# chunks (1: without, 2: with the offsets window), once [lo, hi) is known (3),
+# before the segment pass (4), or without result stores (5)
+# (tools/probe_spandiag.py).
+# Never loaded by the product.
+spandiag: $(foreach d,1 2 3 4 5,tools/libcsum_spandiag$(d).so)
+
+tools/libcsum_spandiag%.so: $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DTULIPS_SPAN_DIAG=$* -shared -o $@ $(SRCS)
 
 # Device assembly + resource usage of the kernels (for inspection).
 asm:

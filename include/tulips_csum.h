@@ -101,6 +101,22 @@ int tulips_csum_batch(const uint8_t* base, const uint64_t* offsets,
                       const uint32_t* src, const uint32_t* dst, uint16_t* out,
                       uint32_t n, uint32_t mode, void* stream);
 
+/*
+ * In-order arena: the same batch when its segments lie in order inside one
+ * allocation, offsets[i] + lengths[i] <= offsets[i+1] and
+ * offsets[n-1] + lengths[n-1] <= arena_bytes (a receive ring, a packed
+ * staging buffer). The work is then cut by arena bytes instead of by
+ * segments (every workgroup gets the same bytes whatever the length mix).
+ * Bytes of [base, base + arena_bytes) between segments may be read. A batch
+ * that breaks the order gets undefined results but no access outside the
+ * arena's 16-byte-aligned hull.
+ */
+int tulips_csum_batch_arena(const uint8_t* base, uint64_t arena_bytes,
+                            const uint64_t* offsets, const uint16_t* lengths,
+                            const uint16_t* seeds, const uint32_t* src,
+                            const uint32_t* dst, uint16_t* out, uint32_t n,
+                            uint32_t mode, void* stream);
+
 /* Segment i is base[i*stride .. i*stride + length); length <= 65535. */
 int tulips_csum_batch_fixed(const uint8_t* base, uint64_t stride,
                             uint32_t length, const uint16_t* seeds,
@@ -118,6 +134,13 @@ int tulips_csum_verify(const uint8_t* base, const uint64_t* offsets,
                        const uint32_t* dst, uint16_t* out,
                        uint32_t* bad_count, uint32_t n, uint32_t mode,
                        void* stream);
+
+/* tulips_csum_verify over an in-order arena (see tulips_csum_batch_arena). */
+int tulips_csum_verify_arena(const uint8_t* base, uint64_t arena_bytes,
+                             const uint64_t* offsets, const uint16_t* lengths,
+                             const uint32_t* src, const uint32_t* dst, uint16_t* out,
+                             uint32_t* bad_count, uint32_t n, uint32_t mode,
+                             void* stream);
 
 /* ---- host-resident batches (end-to-end path) ----------------------------- */
 

@@ -28,6 +28,12 @@ extern "C" {
                                        end and split evenly over its waves,
                                        `unroll` windows (2/4) per batch,
                                        double-buffered; `group` must be 8 */
+#define TULIPS_CSUM_KIND_SPAN 5     /* in-order arenas only
+                                       (tulips_csum_batch_arena): a workgroup
+                                       per 4 KiB * `unroll` (2/4/6/8/10/12) of arena
+                                       bytes, segments finished where they
+                                       start; `group` = 4 KiB rows read past
+                                       the range (1/2, 0 = 2) */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning
@@ -62,6 +68,13 @@ int tulips_csum_batch_tuned(const uint8_t* base, const uint64_t* offsets,
                             const uint32_t* src, const uint32_t* dst,
                             uint16_t* out, uint32_t n, uint32_t mode,
                             const tulips_csum_tuning* tuning, void* stream);
+
+int tulips_csum_batch_arena_tuned(const uint8_t* base, uint64_t arena_bytes,
+                                  const uint64_t* offsets, const uint16_t* lengths,
+                                  const uint16_t* seeds, const uint32_t* src,
+                                  const uint32_t* dst, uint16_t* out, uint32_t n,
+                                  uint32_t mode, const tulips_csum_tuning* tuning,
+                                  void* stream);
 
 /* Frame kernels (include/tulips_csum.h) with an explicit geometry: op 0 =
  * tulips_csum_validate_frames, op 1 = tulips_csum_generate_frames (counters

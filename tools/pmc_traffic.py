@@ -22,15 +22,17 @@ import shutil
 import sys
 from collections import defaultdict
 
-# kernel name fragment -> workload label (bench.py default geometries)
 # (kernel name fragment, grid size or None, workload label): bench.py's
-# default geometries. The ZIPF kernel is also what the host path launches
-# per staging chunk, so ZIPF is told apart by its grid (65,536 segments /
-# 8 per wave = 8,192 waves = 524,288 threads).
+# default geometries. The ZIPF kernels are also what the host path launches
+# per staging chunk, so ZIPF is told apart by its grid: the arena-span kernel
+# has one 256-thread workgroup per 32 KiB of the 43,772,673-byte arena (1,336
+# ranges = 342,016 threads), the any-layout packed kernel 8 segments per wave
+# (8,192 waves = 524,288 threads).
 WORKLOADS = [
     ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
     ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
-    ("csum_packed_kernel<8, 4, true, 1>", 524288, "ZIPF"),  # PF = 1: double-buffered
+    ("csum_span_kernel<8, 2, true>", 342016, "ZIPF"),
+    ("csum_packed_kernel<8, 4, true, 1>", 524288, "ZIPF_any_layout"),  # PF = 1
     ("frame_kernel<false, 16, 6, true>", None, "frames_validate_F1514"),
     ("frame_kernel<true, 16, 6, true>", None, "frames_generate_F1514"),
     ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
@@ -40,6 +42,7 @@ WORKLOADS = [
 # read + written by segmentation (super-frames in, segments out); RSS 12 B in
 # + 4 B out per tuple
 ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673,
+              "ZIPF_any_layout": 43772673,
               "frames_validate_F1514": 65536 * 1514, "frames_generate_F1514": 65536 * 1514,
               "segment_TSO_64K_mss1460": 1024 * 64294 + 45056 * 1514,
               "rss_toeplitz_16M": (1 << 24) * 16}

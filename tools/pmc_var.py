@@ -36,7 +36,13 @@ def run():
              "balanced": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=2, nontemporal=1,
                                      block=256, sps=2),
              "vpacked": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=2, nontemporal=1,
-                                    block=256, sps=4)}
+                                    block=256, sps=4),
+             "span4": csum.Tuning(kind=csum.KIND_SPAN, unroll=4, nontemporal=1),
+             "span8": csum.Tuning(kind=csum.KIND_SPAN, unroll=8, nontemporal=1),
+             "span8t": csum.Tuning(kind=csum.KIND_SPAN, unroll=8, nontemporal=0)}
+    only = os.environ.get("PMC_GEOMS")
+    if only:
+        geoms = {k: v for k, v in geoms.items() if k in only.split(",")}
     shapes = {"zipf": bench.zipf_lengths(N)}
     out = torch.empty(N, dtype=torch.uint16, device=dev)
     order = []
@@ -50,9 +56,14 @@ def run():
         dlens = torch.from_numpy(lens.view(np.int16)).to(dev)
         for gname, t in geoms.items():
             for _ in range(REPS):
-                assert lib.tulips_csum_batch_tuned(arena.data_ptr(), doffs.data_ptr(),
-                                                   dlens.data_ptr(), None, None, None,
-                                                   out.data_ptr(), N, 0, t, sh) == 0
+                if t.kind == csum.KIND_SPAN:
+                    assert lib.tulips_csum_batch_arena_tuned(
+                        arena.data_ptr(), nb, doffs.data_ptr(), dlens.data_ptr(), None, None,
+                        None, out.data_ptr(), N, 0, t, sh) == 0
+                else:
+                    assert lib.tulips_csum_batch_tuned(arena.data_ptr(), doffs.data_ptr(),
+                                                       dlens.data_ptr(), None, None, None,
+                                                       out.data_ptr(), N, 0, t, sh) == 0
                 order.append((gname, sname, nb))
             torch.cuda.synchronize()
     a = torch.empty(N * 1500 + 256, dtype=torch.uint8, device=dev)
@@ -76,7 +87,8 @@ def summarise(path):
         per.setdefault((disp, k), {})[r["Counter_Name"]] = float(r["Counter_Value"])
     out = {}
     for (disp, k), c in sorted(per.items(), key=lambda x: int(x[0][0])):
-        kk = ("balanced" if "balanced" in k else "vpacked" if "vpacked" in k else
+        kk = ("span" + k.split("csum_span_kernel")[1][:12] if "csum_span_kernel" in k else
+              "balanced" if "balanced" in k else "vpacked" if "vpacked" in k else
               "packed" if "packed" in k else
               "fixed" if "csum_kernel" in k else k[:40])
         out.setdefault(kk, []).append(c)

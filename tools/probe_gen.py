@@ -23,18 +23,12 @@ def main():
     NB = 4
     NMAX = 98304
     lens_all = bench.zipf_lengths(NMAX)
-    geoms = {"packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
+    geoms = {"span4": ("span", 4), "span6": ("span", 6), "span8": ("span", 8),
+             "span10": ("span", 10), "span12": ("span", 12),
+             "packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                         block=256, sps=2),
              "vpacked8x2": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=2, nontemporal=1,
                                        block=256, sps=4),
-             "vpacked16x2": csum.Tuning(kind=csum.KIND_PACKED, group=16, unroll=2, nontemporal=1,
-                                        block=256, sps=4),
-             "bal8w_u4pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=4, nontemporal=1,
-                                       block=512, sps=2),
-             "bal8w_u2pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=2, nontemporal=1,
-                                       block=512, sps=2),
-             "bal4w_u4pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=4, nontemporal=1,
-                                       block=256, sps=2),
              "bal4w_u2pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=2, nontemporal=1,
                                        block=256, sps=2)}
     if os.environ.get("PROBE_UNIFORM"):
@@ -51,15 +45,27 @@ def main():
         dlens = torch.from_numpy(lens.view(np.int16)).to(dev)
         row = {"n": n, "bytes": nb}
         for gname, t in geoms.items():
-            def fn(i, sh, t=t):
-                b = i % NB
-                assert lib.tulips_csum_batch_tuned(arena.data_ptr() + b * nb, doffs.data_ptr(),
-                                                   dlens.data_ptr(), None, None, None,
-                                                   out.data_ptr() + b * n * 2, n, 0, t, sh) == 0
+            if isinstance(t, tuple):
+                t = csum.Tuning(kind=csum.KIND_SPAN, unroll=t[1], nontemporal=1)
+
+                def fn(i, sh, t=t):
+                    b = i % NB
+                    assert lib.tulips_csum_batch_arena_tuned(
+                        arena.data_ptr() + b * nb, nb, doffs.data_ptr(), dlens.data_ptr(),
+                        None, None, None, out.data_ptr() + b * n * 2, n, 0, t, sh) == 0
+            else:
+                def fn(i, sh, t=t):
+                    b = i % NB
+                    assert lib.tulips_csum_batch_tuned(
+                        arena.data_ptr() + b * nb, doffs.data_ptr(), dlens.data_ptr(), None,
+                        None, None, out.data_ptr() + b * n * 2, n, 0, t, sh) == 0
             for i in range(NB):
                 fn(i, stream.cuda_stream)
             tm = float(np.median([timer(fn, 64) for _ in range(3)]))
             row[gname] = round(tm * 1e6, 2)
+            if os.environ.get("PROBE_PIPE"):
+                tp = float(np.median([timer(fn, 64, branches=4) for _ in range(3)]))
+                row[gname + "_pipe4"] = round(tp * 1e6, 2)
         print(json.dumps(row), flush=True)
         del arena
 

@@ -41,19 +41,28 @@ def main():
     stamps = torch.zeros(4 * 300000, dtype=torch.int64, device=dev)
     sh = torch.cuda.current_stream().cuda_stream
     geoms = {"packed8x4pf": (csum.KIND_PACKED, 8, 4, 2, 256),
-             "vpacked8x2": (csum.KIND_PACKED, 8, 2, 4, 256),
-             "bal8w_u4pp": (csum.KIND_BALANCED, 8, 4, 2, 512)}
+             "span4": (csum.KIND_SPAN, 2, 4, 0, 0),
+             "span6": (csum.KIND_SPAN, 2, 6, 0, 0),
+             "span8": (csum.KIND_SPAN, 2, 8, 0, 0)}
+    only = os.environ.get("PROBE_GEOMS")
+    if only:
+        geoms = {k: v for k, v in geoms.items() if k in only.split(",")}
+
+    def run(t, i):
+        if t.kind == csum.KIND_SPAN:
+            return lib.tulips_csum_batch_arena_tuned(
+                buf.data_ptr() + (i % NB) * nb, nb, doffs.data_ptr(), dlens.data_ptr(), None,
+                None, None, out.data_ptr(), n, 0, C.byref(t), sh)
+        return lib.tulips_csum_batch_tuned(buf.data_ptr() + (i % NB) * nb, doffs.data_ptr(),
+                                           dlens.data_ptr(), None, None, None, out.data_ptr(),
+                                           n, 0, C.byref(t), sh)
     for gname, (kind, g, u, sps, blk) in geoms.items():
         t = csum.Tuning(kind=kind, group=g, unroll=u, nontemporal=1, sps=sps, block=blk)
         for i in range(8):
-            lib.tulips_csum_batch_tuned(buf.data_ptr() + (i % NB) * nb, doffs.data_ptr(),
-                                        dlens.data_ptr(), None, None, None, out.data_ptr(),
-                                        n, 0, C.byref(t), sh)
+            assert run(t, i) == 0
         torch.cuda.synchronize()
         assert lib.tulips_csum_stamps_arm(stamps.data_ptr()) == 0
-        lib.tulips_csum_batch_tuned(buf.data_ptr() + 3 * nb, doffs.data_ptr(),
-                                    dlens.data_ptr(), None, None, None, out.data_ptr(), n, 0,
-                                    C.byref(t), sh)
+        assert run(t, 3) == 0
         torch.cuda.synchronize()
         m = lib.tulips_csum_stamps_count()
         st = stamps[: 4 * m].cpu().numpy().reshape(m, 4)
@@ -71,6 +80,17 @@ def main():
                "last10_end_life_start_bytes": [[round(float(t1[i]), 2), round(float(life[i]), 2),
                                                 round(float(t0[i]), 2), int(wb[i])]
                                                for i in np.argsort(-t1)[:10]]}
+        if kind == csum.KIND_SPAN:
+            # field 2 = the stamp after the first barrier (window counted,
+            # every wave's chunks staged and scanned)
+            tm = (st[:, 2] - base) / 100.0
+            w0 = np.arange(m) % 4 == 0
+            rep["to_staged_p50_p90_max"] = [round(float(np.percentile(tm - t0, q)), 2)
+                                            for q in (50, 90, 100)]
+            rep["after_staged_p50_p90_max"] = [round(float(np.percentile(t1 - tm, q)), 2)
+                                               for q in (50, 90, 100)]
+            rep["wg_start_p10_p50_p90_max"] = [round(float(np.percentile(t0[w0], q)), 2)
+                                               for q in (10, 50, 90, 100)]
         print(json.dumps(rep), flush=True)
 
 

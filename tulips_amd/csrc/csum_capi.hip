@@ -138,6 +138,11 @@ tulips_csum_tcp_host(uint32_t src, uint32_t dst, uint16_t len,
 // ---------------------------------------------------------------------------
 namespace {
 
+// KIND_SPAN chunks per lane: 32 KiB per workgroup range, 8 KiB halo
+// (tools/probe_gen.py, profiles/probe_span_r02.json: ZIPF 11.7 us serial,
+// 8.7 us per launch with 4 launches in flight)
+constexpr int SPAN_DEFAULT_UNROLL = 8;
+
 thread_local char last_error[160] = "";
 
 inline int
@@ -334,6 +339,81 @@ batch_var(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
     launch_var(base, offsets, lengths, a, static_cast<hipStream_t>(stream)));
 }
 
+// In-order arena batches (KIND_SPAN, csum_kernels.hip): the tuning's kind
+// must be DEFAULT or SPAN; unroll = chunks per lane (2, 4, 6, 8; 10 and 12
+// with 2 halo rows), group = halo rows (1, 2; 0 = 2).
+int
+batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
+            const uint16_t* lengths, const uint16_t* seeds, const uint32_t* src,
+            const uint32_t* dst, uint16_t* out, uint32_t* bad, uint32_t n, uint32_t mode,
+            const tulips_csum_tuning* tuning, void* stream)
+{
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if ((!base && arena) || !offsets || !lengths || (!out && !bad) ||
+      !mode_ok(mode, src, dst)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (tuning && tuning->kind != TULIPS_CSUM_KIND_DEFAULT &&
+      tuning->kind != TULIPS_CSUM_KIND_SPAN) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  LaunchArgs a{};
+  a.seeds = seeds;
+  a.src = src;
+  a.dst = dst;
+  a.out = out;
+  a.bad = bad;
+  a.n = n;
+  a.mode = mode;
+  a.kind = TULIPS_CSUM_KIND_SPAN;
+  a.unroll = (tuning && tuning->unroll) ? tuning->unroll : SPAN_DEFAULT_UNROLL;
+  a.group = (tuning && tuning->group) ? tuning->group : 0;
+  if (a.group != 0 && a.group != 1 && a.group != 2) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  const int32_t nt = (tuning && tuning->nontemporal >= 0) ? tuning->nontemporal : 1;
+  a.nontemporal = (nt & 1) != 0;
+  a.nt_store = (nt & 2) != 0;
+  if (a.unroll != 2 && a.unroll != 4 && a.unroll != 6 && a.unroll != 8 && a.unroll != 10 &&
+      a.unroll != 12) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return status_of(
+    launch_span(base, arena, offsets, lengths, a, static_cast<hipStream_t>(stream)));
+}
+
+// A counting call: `launch(shards)` then the finalize into `count`, queued as
+// one sequence under the stream's lock (stream_state.h).
+template<class F>
+int
+counted(void* stream, uint32_t* count, const F& launch)
+{
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::shared_ptr<StreamState> ss;
+  hipError_t e = stream_state(st, &ss);
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  const bool capturing = stream_capturing(st);
+  std::lock_guard<std::mutex> g(ss->call);
+  uint32_t* shards = nullptr;
+  if ((e = call_shards(*ss, capturing, &shards)) != hipSuccess) {
+    return e == hipErrorStreamCaptureUnsupported ? TULIPS_STATUS_INVALID_ARGUMENT
+                                                 : status_of(e);
+  }
+  int rc = launch(shards);
+  if (rc == TULIPS_STATUS_OK) {
+    // count = the shards' sum (0 for n == 0), shards zeroed again
+    rc = status_of(launch_counters_finalize(shards, count, 1, st));
+  }
+  if (rc != TULIPS_STATUS_OK && !capturing) {
+    drop_shards(*ss, shards);
+  }
+  return rc;
+}
+
 } // namespace
 
 extern "C" {
@@ -374,33 +454,60 @@ tulips_csum_verify(const uint8_t* base, const uint64_t* offsets,
   if (!bad_count || (m != TULIPS_CSUM_INET && m != TULIPS_CSUM_TCP)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
-  hipStream_t st = static_cast<hipStream_t>(stream);
   if (n && (!base || !offsets || !lengths || !mode_ok(mode, src, dst))) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
-  std::shared_ptr<StreamState> ss;
-  hipError_t e = stream_state(st, &ss);
-  if (e != hipSuccess) {
-    return status_of(e);
-  }
-  // count kernel + finalize queued as one sequence (stream_state.h)
-  const bool capturing = stream_capturing(st);
-  std::lock_guard<std::mutex> g(ss->call);
-  uint32_t* shards = nullptr;
-  if ((e = call_shards(*ss, capturing, &shards)) != hipSuccess) {
-    return e == hipErrorStreamCaptureUnsupported ? TULIPS_STATUS_INVALID_ARGUMENT
-                                                 : status_of(e);
-  }
-  int rc = batch_var(base, offsets, lengths, nullptr, src, dst, out, shards, n, mode,
+  return counted(stream, bad_count, [&](uint32_t* shards) {
+    return batch_var(base, offsets, lengths, nullptr, src, dst, out, shards, n, mode,
                      nullptr, stream);
-  if (rc == TULIPS_STATUS_OK) {
-    // bad_count = the shards' sum (0 for n == 0), shards zeroed again
-    rc = status_of(launch_counters_finalize(shards, bad_count, 1, st));
+  });
+}
+
+int
+tulips_csum_batch_arena(const uint8_t* base, uint64_t arena_bytes,
+                        const uint64_t* offsets, const uint16_t* lengths,
+                        const uint16_t* seeds, const uint32_t* src, const uint32_t* dst,
+                        uint16_t* out, uint32_t n, uint32_t mode, void* stream)
+{
+  if (n && !out) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
   }
-  if (rc != TULIPS_STATUS_OK && !capturing) {
-    drop_shards(*ss, shards);
+  return batch_arena(base, arena_bytes, offsets, lengths, seeds, src, dst, out, nullptr,
+                     n, mode, nullptr, stream);
+}
+
+int
+tulips_csum_verify_arena(const uint8_t* base, uint64_t arena_bytes,
+                         const uint64_t* offsets, const uint16_t* lengths,
+                         const uint32_t* src, const uint32_t* dst, uint16_t* out,
+                         uint32_t* bad_count, uint32_t n, uint32_t mode, void* stream)
+{
+  const uint32_t m = mode & TULIPS_CSUM_MODE_MASK;
+  if (!bad_count || (m != TULIPS_CSUM_INET && m != TULIPS_CSUM_TCP)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
   }
-  return rc;
+  if (n && ((!base && arena_bytes) || !offsets || !lengths || !mode_ok(mode, src, dst))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return counted(stream, bad_count, [&](uint32_t* shards) {
+    return batch_arena(base, arena_bytes, offsets, lengths, nullptr, src, dst, out,
+                       shards, n, mode, nullptr, stream);
+  });
+}
+
+int
+tulips_csum_batch_arena_tuned(const uint8_t* base, uint64_t arena_bytes,
+                              const uint64_t* offsets, const uint16_t* lengths,
+                              const uint16_t* seeds, const uint32_t* src,
+                              const uint32_t* dst, uint16_t* out, uint32_t n,
+                              uint32_t mode, const tulips_csum_tuning* tuning,
+                              void* stream)
+{
+  if (n && !out) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return batch_arena(base, arena_bytes, offsets, lengths, seeds, src, dst, out, nullptr,
+                     n, mode, tuning, stream);
 }
 
 int

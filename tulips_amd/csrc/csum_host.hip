@@ -41,6 +41,8 @@ namespace {
 constexpr uint64_t DEFAULT_CHUNK = 16ull << 20;
 constexpr uint32_t MAX_SEGS_PER_CHUNK = 1u << 20;
 constexpr int NSLOTS = 3;
+// KIND_SPAN chunks per lane for in-order staged chunks (csum_capi.hip)
+constexpr int SPAN_UNROLL = 8;
 // Staging-copy threads: the CPUs this process may run on, at most 16 (a GPU's
 // share of a host; 16 threads took pageable F1500 from 37 to 44 GiB/s over 8
 // on the MI355X box, alternating builds).
@@ -466,10 +468,12 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
     // Cut the chunk: segments [i, j) with at most ctx->chunk bytes.
     uint64_t bytes = 0, lo = UINT64_MAX, hi = 0;
     uint32_t j = i;
+    bool in_order = true; // caller's offsets ascending, segments disjoint
     while (j < n && j - i < MAX_SEGS_PER_CHUNK &&
            bytes + lengths[j] <= ctx->chunk) {
       s.h_offs[j - i] = bytes;
       bytes += lengths[j];
+      in_order = in_order && (j == i || offsets[j] >= offsets[j - 1] + lengths[j - 1]);
       lo = std::min<uint64_t>(lo, offsets[j]);
       hi = std::max<uint64_t>(hi, offsets[j] + lengths[j]);
       ++j;
@@ -478,7 +482,10 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
     const uint8_t* dbase = s.d_bytes;
     const uint8_t* hsrc;
     uint64_t hbytes;
+    // packed staging is in order by construction (tulips_csum_batch_arena)
+    bool arena_ok = true;
     if (pinned && hi > lo && hi - lo <= ctx->chunk && hi - lo <= 2 * bytes) {
+      arena_ok = in_order;
       // Direct DMA of the caller's span; offsets rebased onto it.
       for (uint32_t k = 0; k < cnt; ++k) {
         s.h_offs[k] = offsets[i + k] - lo;
@@ -540,15 +547,23 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
       a.bad = nullptr;
       a.n = cnt;
       a.mode = job.mode;
-      // the variable-length default geometry (csum_capi.hip default_tuning)
-      a.kind = TULIPS_CSUM_KIND_PACKED;
-      a.group = 8;
-      a.unroll = 4;
-      a.spw = 2;
-      a.block = 256;
       a.nontemporal = true;
       a.max_blocks = 0;
-      TCS_Q(launch_var(dbase, s.d_offs, s.d_lens, a, st));
+      if (arena_ok) {
+        // segments in order in the staged bytes: work cut by bytes
+        a.kind = TULIPS_CSUM_KIND_SPAN;
+        a.unroll = SPAN_UNROLL;
+        a.group = 0;
+        TCS_Q(launch_span(dbase, hbytes, s.d_offs, s.d_lens, a, st));
+      } else {
+        // the variable-length default geometry (csum_capi.hip default_tuning)
+        a.kind = TULIPS_CSUM_KIND_PACKED;
+        a.group = 8;
+        a.unroll = 4;
+        a.spw = 2;
+        a.block = 256;
+        TCS_Q(launch_var(dbase, s.d_offs, s.d_lens, a, st));
+      }
     }
     TCS_Q(hipMemcpyAsync(s.h_out, s.d_out, size_t(cnt) * job.elem(),
                          hipMemcpyDeviceToHost, st));

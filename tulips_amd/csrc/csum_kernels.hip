@@ -154,6 +154,23 @@ stamp_wave(uint64_t t0)
     g_stamps[4 * i + 3] = hwid;
   }
 }
+
+// The same with a mid-life stamp in place of the XCC id.
+__device__ __forceinline__ void
+stamp_wave_mid(uint64_t t0, uint64_t tm)
+{
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && g_stamps) {
+    const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (i == 0) {
+      g_stamp_count = (gridDim.x * blockDim.x) >> 6;
+    }
+    g_stamps[4 * i + 0] = t0;
+    g_stamps[4 * i + 1] = t1;
+    g_stamps[4 * i + 2] = tm;
+    g_stamps[4 * i + 3] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+  }
+}
 #endif
 
 template<int G>
@@ -1055,7 +1072,7 @@ csum_balanced_kernel(VarSegs segs, const uint16_t* __restrict__ seeds,
     // the segment still open at the range end continues in the next wave
     if (r1 > r0 && pend_end) {
       const uint32_t k = uint32_t(__builtin_ctzll(pend_end));
-      if (__builtin_amdgcn_readlane(P, k) < r1) {
+      if (uint32_t(__builtin_amdgcn_readlane(P, k)) < r1) {
         part = lane == k ? run - eprev : part;
       }
     }
@@ -1099,6 +1116,357 @@ launch_balanced(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
   hipLaunchKernelGGL((csum_balanced_kernel<NW, U, NT, PF>), dim3(uint32_t(blocks)),
                      dim3(64 * NW), 0, stream, segs, a.seeds, a.src, a.dst, a.out, a.bad,
                      a.n, a.mode, a.nt_store);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// SPAN: in-order arenas (tulips_csum_batch_arena), work cut by BYTES.
+//
+// Every kernel above hands each wave (or workgroup) a fixed number of
+// segments, so its life is a chain of dependent round trips whose length
+// follows the bytes it drew: on the Zipf batch the heaviest waves (28.8 KB
+// for 8 segments) end ~8 us after the median one whatever the grid does
+// (tools/probe_stamps_small.py; floor of ~8 us even at n = 1024). When the
+// segments lie in order in one arena, the byte range of the arena itself can
+// be cut instead: workgroup k owns the 16-byte-aligned range
+// [A + kW, A + (k+1)W), W = 4 KiB * U, and
+//   * its 4 waves load the range plus a 4 KiB halo past its end at once
+//     (U + 1 chunks per lane, one round trip), stage the range's chunks in
+//     LDS and scan their 16-bit-half sums into an LDS prefix P;
+//   * the segments STARTING in the range,
+//     [lo, hi) = [first s: off_s >= kW - d, first s: off_s >= (k+1)W - d),
+//     come from a 1024-entry window of offsets/lengths loaded in the same
+//     round trip, BEFORE the chunks (vmcnt retires in order), where an evenly
+//     filled arena puts them (n * range middle / arena bytes); on the Zipf
+//     batch it brackets [lo, hi) for all but 0.1 % of the ranges. Otherwise
+//     wave 0 finds lo and hi by a 256-ary search (a few more round trips);
+//   * segment s in [lo, hi) (one per thread) is a prefix difference plus its
+//     two masked boundary chunks, all from LDS. Only hi - 1 can run past the
+//     range: the workgroup sums its bytes in the halo (still in registers)
+//     and past the halo (a tail > 4 KiB: one more round trip, taken only
+//     when such a tail exists).
+// Segment s is finished by the one workgroup its first byte falls in, so no
+// partial crosses workgroups and no workspace or atomic is needed. A
+// workgroup's life is one round trip + LDS work; its bytes are fixed by
+// construction.
+// Contract (include/tulips_csum.h): offsets[i] + lengths[i] <= offsets[i+1]
+// and offsets[n-1] + lengths[n-1] <= arena_bytes. Every access is clamped
+// into the arena, so a batch breaking the contract gets wrong results but no
+// access outside [base & ~15, (base + arena_bytes + 15) & ~15).
+// ---------------------------------------------------------------------------
+struct SpanArgs
+{
+  const uint8_t* base;
+  uint64_t arena;
+  const uint64_t* offs;
+  const uint16_t* lens;
+  const uint16_t* seeds;
+  const uint32_t* src;
+  const uint32_t* dst;
+  uint16_t* out;
+  uint32_t* bad;
+  uint32_t n;
+  uint32_t mode;
+  uint32_t nt_store;
+};
+
+typedef const __attribute__((address_space(1))) uint64_t* gu64_ptr;
+
+// Search interval update after one round of 256 samples L + q*st (q < 256):
+// c of them (a prefix, offsets being sorted) lie below the target.
+__device__ __forceinline__ void
+span_narrow(uint32_t& L, uint32_t& R, uint32_t st, uint32_t c)
+{
+  if (c == 0) {
+    R = L;
+  } else {
+    const uint32_t nl = L + (c - 1) * st + 1;
+    R = min(L + c * st, R);
+    L = nl;
+  }
+}
+
+template<int U, int HR, bool NT>
+__global__ __launch_bounds__(256) void
+csum_span_kernel(SpanArgs p)
+{
+  constexpr uint32_t R = U + HR;         // rows of 256 chunks: range + halo
+  constexpr uint32_t NC = 256u * U;      // chunks per range
+  constexpr uint64_t W = 16ull * NC;     // bytes per range
+  constexpr uint32_t NWIN = 1024;        // speculative window entries
+  constexpr int UE = 4;                  // tail chunks per thread per batch
+  __shared__ u32x4 s_raw[256 * R];       // the range's and the halo's chunks
+  __shared__ uint32_t s_sc[256 * R];     // row-wise wave scans of chunk values
+  __shared__ uint32_t s_tot[4 * R];      // per (row, wave) scan totals
+  __shared__ uint32_t s_woff[4][4 * R];  // each wave's copy of their exclusive prefix
+  __shared__ uint32_t s_cnt[12];         // per wave: window counts, tail flag
+  __shared__ uint64_t s_meta[4];         // end of a segment past the halo; search
+  __shared__ uint32_t s_ext[4];
+
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const uint32_t k = xcd_block(blockIdx.x, gridDim.x);
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p.base);
+  const uint64_t d = b & 15u;
+  const uintptr_t x0 = (b & ~uintptr_t(15)) + uint64_t(k) * W, x1 = x0 + W;
+  const uintptr_t xe = x1 + 16u * 256u * HR; // end of the halo
+  const uintptr_t aend = b + p.arena;
+  const uintptr_t zero = reinterpret_cast<uintptr_t>(k_zero_chunk);
+  const uintptr_t last = p.arena ? ((aend - 1) & ~uintptr_t(15)) : zero;
+  const uint32_t n = p.n;
+  const gu64_ptr offs = reinterpret_cast<gu64_ptr>(reinterpret_cast<uintptr_t>(p.offs));
+  const gu16_ptr lens = reinterpret_cast<gu16_ptr>(reinterpret_cast<uintptr_t>(p.lens));
+  // lo = first s with off_s >= tg0, hi = first s with off_s >= tg1
+  const uint64_t tg0 = k ? uint64_t(k) * W - d : 0, tg1 = uint64_t(k + 1) * W - d;
+#ifdef TULIPS_CSUM_STAMPS
+  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
+
+  // 1. one round trip: the offsets/lengths window where an evenly filled
+  //    arena would put this range's segments, then the range + halo chunks
+  //    (window first: vmcnt retires in order, so its wait never waits for
+  //    the chunks)
+  const uint64_t mid = (tg0 + tg1) / 2;
+  const uint64_t guess = uint64_t(double(n) * double(mid) / double(p.arena ? p.arena : 1));
+  const uint32_t gmax = n > NWIN ? n - NWIN : 0u;
+  const uint32_t G = uint32_t(min(guess > NWIN / 2 ? guess - NWIN / 2 : 0ull, uint64_t(gmax)));
+  uint64_t wo[4];
+  uint32_t wl[4];
+#if TULIPS_SPAN_DIAG == 1
+  // diagnostic build (tools/libcsum_spandiag1.so): no offsets window
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    wo[r] = G + t + 256u * r;
+    wl[r] = 0;
+  }
+#else
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t i = min(G + t + 256u * r, n - 1);
+    wo[r] = offs[i];
+    wl[r] = lens[i];
+  }
+#endif
+  u32x4 v[R];
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    const uintptr_t a = x0 + 16u * (j * 256u + t);
+    v[j] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero));
+  }
+  {
+    // window counts below each target, and whether an entry starting in
+    // the range runs past the halo (at most one can, in order)
+    uint32_t c0 = 0, c1 = 0;
+    bool far = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool in = G + t + 256u * r < n;
+      c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg0));
+      c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg1));
+      const uintptr_t sa = b + wo[r], se = min(b + wo[r] + wl[r], aend);
+      if (in && sa >= x0 && sa < x1 && se > xe) {
+        far = true;
+        s_meta[3] = se;
+      }
+    }
+    const bool anyfar = __builtin_amdgcn_ballot_w64(far) != 0;
+    if (lane == 0) {
+      s_cnt[w] = c0;
+      s_cnt[4 + w] = c1;
+      s_cnt[8 + w] = anyfar;
+    }
+  }
+  // 2. chunks to LDS with the row-wise wave scans of their values
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    s_raw[j * 256u + t] = v[j];
+    const uint32_t sc = wave_incl_scan(chunk_value(v[j]));
+    s_sc[j * 256u + t] = sc;
+    if (lane == 63) {
+      s_tot[4 * j + w] = sc;
+    }
+  }
+  lds_barrier();
+#ifdef TULIPS_CSUM_STAMPS
+  const uint64_t stamp_mid = __builtin_amdgcn_s_memrealtime();
+#endif
+#if defined(TULIPS_SPAN_DIAG) && TULIPS_SPAN_DIAG > 0
+  // diagnostic builds: stop after the chunks are staged and scanned
+  if (t == 0 && p.out && k < n) {
+    p.out[k] = uint16_t(s_tot[0] + s_cnt[0] + s_sc[5]);
+  }
+  return;
+#endif
+
+  // 3. this wave's copy of the (row, wave) offsets: inclusive prefix of
+  //    chunk c = s_woff[c >> 6] + s_sc[c]
+  {
+    const uint32_t x = lane < 4 * R ? s_tot[lane] : 0u;
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane < 4 * R) {
+      s_woff[w][lane] = inc - x;
+    }
+  }
+  auto P = [&](uint32_t c) { return s_woff[w][c >> 6] + s_sc[c]; };
+  const uint32_t c0 = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  const uint32_t c1 = s_cnt[4] + s_cnt[5] + s_cnt[6] + s_cnt[7];
+  const bool tail = (s_cnt[8] | s_cnt[9] | s_cnt[10] | s_cnt[11]) != 0;
+  const uint32_t nw = min(NWIN, n - G);
+  const bool tail_ok = G + NWIN >= n;
+  const bool ok = (c0 > 0 || G == 0) && (c0 < nw || tail_ok) && (c1 > 0 || G == 0) &&
+                  (c1 < nw || tail_ok);
+
+  // 4. rare: a segment runs past the halo (> 4 KiB * HR beyond the range):
+  //    the workgroup sums its bytes past the halo in one more round trip
+  auto tail_sum = [&](uintptr_t te) {
+    const uint32_t tch = uint32_t((te - xe + 15) >> 4);
+    const uintptr_t tlast = xe + 16u * (tch - 1);
+    const int tbytes = int(te - xe) - 16 * int(tch - 1);
+    uint32_t tsum = 0;
+    for (uint32_t q0 = 0; q0 < tch; q0 += 256u * UE) {
+      u32x4 e[UE];
+#pragma unroll
+      for (int j = 0; j < UE; ++j) {
+        const uint32_t c = q0 + t + 256u * j;
+        e[j] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(c < tch ? xe + 16u * c : tlast));
+      }
+#pragma unroll
+      for (int j = 0; j < UE; ++j) {
+        const uint32_t c = q0 + t + 256u * j;
+        tsum += c + 1 < tch ? chunk_value(e[j])
+                            : (c + 1 == tch ? masked_value(e[j], 0, tbytes) : 0u);
+      }
+    }
+    tsum = wave_incl_scan(tsum);
+    if (lane == 63) {
+      s_ext[w] = tsum;
+    }
+    lds_barrier();
+    return s_ext[0] + s_ext[1] + s_ext[2] + s_ext[3];
+  };
+  uint32_t ext = 0;
+
+  // 5. one segment: prefix differences over [x0, xe) plus the tail
+  const uint32_t want = (p.mode & FLAG_COMPLEMENT) ? 0u : 0xffffu;
+  const bool side_in = (p.mode & MODE_MASK) == MODE_TCP || p.seeds != nullptr;
+  auto emit = [&](uint32_t s, bool mine, uint64_t so, uint32_t sl) {
+    SideIn side{0, 0, 0};
+    if (side_in) {
+      side = load_side(mine ? s : 0u, p.seeds, p.src, p.dst, p.mode);
+    }
+    const uintptr_t sa = min(max(b + so, x0), x1 - 1);
+    const uintptr_t se = min(b + so + sl, aend);
+    const uintptr_t ie = min(se, xe);
+    uint32_t sum = 0;
+    if (ie > sa) {
+      const uint32_t ca = uint32_t((sa - x0) >> 4);
+      const uint32_t ce = uint32_t((ie - 1 - x0) >> 4);
+      const int ha = int(sa & 15u), tb = int(((ie - 1) & 15u) + 1u);
+      sum = ca == ce ? masked_value(s_raw[ca], ha, tb)
+                     : masked_value(s_raw[ca], ha, 16) + (P(ce - 1) - P(ca)) +
+                         masked_value(s_raw[ce], 0, tb);
+    }
+    sum += se > xe ? ext : 0u;
+    const uint32_t r =
+      finish(sum, (sa & 1u) != 0, p.mode, side.seed, side.src, side.dst, sl);
+    if (mine && p.out) {
+      if (p.nt_store) {
+        __builtin_nontemporal_store(uint16_t(r), p.out + s);
+      } else {
+        p.out[s] = uint16_t(r);
+      }
+    }
+    if (p.bad) {
+      const uint32_t nb =
+        __builtin_popcountll(__builtin_amdgcn_ballot_w64(mine && r != want));
+      if (lane == 0 && nb) {
+        atomicAdd(p.bad + CNT_LINE * (blockIdx.x % CNT_SHARDS), nb);
+      }
+    }
+  };
+
+  if (ok) {
+    // the window brackets [lo, hi): each thread finishes the segments whose
+    // metadata it loaded
+    const uint32_t lo = G + c0, hi = G + c1;
+    if (tail) {
+      ext = tail_sum(s_meta[3]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t i = G + t + 256u * r;
+      const bool mine = i >= lo && i < hi;
+      if (__builtin_amdgcn_ballot_w64(mine) != 0) {
+        emit(i, mine, mine ? wo[r] : 0, mine ? wl[r] : 0u);
+      }
+    }
+  } else {
+    // rare: wave 0 searches [lo, hi); segments' metadata from memory
+    if (w == 0) {
+      uint32_t L0 = 0, R0 = n, L1 = 0, R1 = n;
+      while (R0 > L0 || R1 > L1) {
+        const uint32_t st0 = (R0 - L0 + 255u) >> 8, st1 = (R1 - L1 + 255u) >> 8;
+        uint64_t o0[4], o1[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t q = lane + 64u * r;
+          o0[r] = offs[min(uint64_t(L0) + uint64_t(q) * st0, uint64_t(n - 1))];
+          o1[r] = offs[min(uint64_t(L1) + uint64_t(q) * st1, uint64_t(n - 1))];
+        }
+        uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t q = lane + 64u * r;
+          const bool in0 = uint64_t(L0) + uint64_t(q) * st0 < R0;
+          const bool in1 = uint64_t(L1) + uint64_t(q) * st1 < R1;
+          d0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in0 && o0[r] < tg0));
+          d1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in1 && o1[r] < tg1));
+        }
+        if (R0 > L0) {
+          span_narrow(L0, R0, st0, __builtin_amdgcn_readfirstlane(d0));
+        }
+        if (R1 > L1) {
+          span_narrow(L1, R1, st1, __builtin_amdgcn_readfirstlane(d1));
+        }
+      }
+      if (lane == 0) {
+        s_meta[0] = L0;
+        s_meta[1] = L1;
+      }
+    }
+    lds_barrier();
+    const uint32_t lo = uint32_t(s_meta[0]), hi = uint32_t(s_meta[1]);
+    if (hi > lo) {
+      const uintptr_t te = min(b + p.offs[hi - 1] + p.lens[hi - 1], aend);
+      if (te > xe) {
+        ext = tail_sum(te);
+      }
+    }
+    for (uint32_t s0 = lo; s0 < hi; s0 += 256u) {
+      const uint32_t s = s0 + t;
+      const bool mine = s < hi;
+      emit(s, mine, mine ? p.offs[s] : 0, mine ? p.lens[s] : 0u);
+    }
+  }
+#ifdef TULIPS_CSUM_STAMPS
+  stamp_wave_mid(stamp0, stamp_mid);
+#endif
+}
+
+template<int U, int HR, bool NT>
+hipError_t
+launch_span_u(const SpanArgs& sp, hipStream_t stream)
+{
+  constexpr uint64_t W = 4096ull * U;
+  // ranges cover [A, A + K W) with A <= base: position base + arena (where
+  // an empty last segment may start) included
+  const uint64_t ranges = ((sp.arena + (reinterpret_cast<uintptr_t>(sp.base) & 15u)) / W) + 1;
+  if (ranges > 0x7fffffffull) {
+    return hipErrorInvalidValue;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_span_kernel<U, HR, NT>), dim3(uint32_t(ranges)), dim3(256), 0, stream,
+                     sp);
   return hipGetLastError();
 }
 
@@ -1297,6 +1665,36 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
     return hipErrorInvalidValue;
   }
   return dispatch(segs, a, stream);
+}
+
+hipError_t
+launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
+            const uint16_t* lens, const LaunchArgs& a, hipStream_t stream)
+{
+  const SpanArgs sp{base, arena, offs, lens, a.seeds, a.src, a.dst, a.out, a.bad,
+                    a.n, a.mode, a.nt_store ? 1u : 0u};
+  if (a.n == 0) {
+    return hipSuccess;
+  }
+  // group = halo rows of 4 KiB past the range (1 or 2; 0 = 2)
+  const int hr = a.group ? a.group : 2;
+#define TCS_SCASE(U_, H_)                                                      \
+  if (a.unroll == U_ && hr == H_) {                                            \
+    return a.nontemporal ? launch_span_u<U_, H_, true>(sp, stream)             \
+                         : launch_span_u<U_, H_, false>(sp, stream);           \
+  }
+  TCS_SCASE(2, 1)
+  TCS_SCASE(2, 2)
+  TCS_SCASE(4, 1)
+  TCS_SCASE(4, 2)
+  TCS_SCASE(6, 1)
+  TCS_SCASE(6, 2)
+  TCS_SCASE(8, 1)
+  TCS_SCASE(8, 2)
+  TCS_SCASE(10, 2)
+  TCS_SCASE(12, 2)
+#undef TCS_SCASE
+  return hipErrorInvalidValue;
 }
 
 // ---------------------------------------------------------------------------

@@ -43,6 +43,11 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,
 hipError_t launch_var(const uint8_t* base, const uint64_t* offs,
                       const uint16_t* lens, const LaunchArgs& a,
                       hipStream_t stream);
+// In-order arena (KIND_SPAN): segments lie in order in [base, base + arena);
+// a.unroll = chunks per lane (2, 4, 8: 8, 16, 32 KiB per workgroup).
+hipError_t launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
+                       const uint16_t* lens, const LaunchArgs& a,
+                       hipStream_t stream);
 // frames.hip: per-frame TULIPS_FRAME_* flags (and optional counters[4]) /
 // in-place checksum generation. Zero fields = defaults.
 struct FrameLaunch

@@ -59,6 +59,7 @@ def _check(rc: int, what: str) -> None:
 
 
 KIND_DEFAULT, KIND_SUBGROUP, KIND_HYBRID, KIND_PACKED, KIND_BALANCED = 0, 1, 2, 3, 4
+KIND_SPAN = 5
 
 
 class Tuning(C.Structure):
@@ -101,6 +102,13 @@ _SIGNATURES = {
                                           _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
     "tulips_csum_verify": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      C.c_uint32, C.c_uint32, _vp]),
+    "tulips_csum_batch_arena": (C.c_int, [_vp, C.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          C.c_uint32, C.c_uint32, _vp]),
+    "tulips_csum_verify_arena": (C.c_int, [_vp, C.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                           C.c_uint32, C.c_uint32, _vp]),
+    "tulips_csum_batch_arena_tuned": (C.c_int, [_vp, C.c_uint64, _vp, _vp, _vp, _vp, _vp,
+                                                _vp, C.c_uint32, C.c_uint32,
+                                                C.POINTER(Tuning), _vp]),
     "tulips_csum_ctx_create": (C.c_int, [C.c_int, C.c_uint64, C.POINTER(_vp)]),
     "tulips_csum_ctx_destroy": (C.c_int, [_vp]),
     "tulips_csum_batch_host": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -288,6 +296,50 @@ def batch(arena, offsets, lengths, *, seeds=None, src=None, dst=None,
         rc = lib.tulips_csum_batch_tuned(*args, C.byref(tuning), _stream(stream))
     _check(rc, "tulips_csum_batch")
     return out
+
+
+def _arena_bytes(arena, arena_bytes):
+    if arena_bytes is not None:
+        return int(arena_bytes)
+    if isinstance(arena, int):
+        raise ValueError("arena_bytes is required with a raw arena address")
+    return int(arena.numel()) * arena.element_size()
+
+
+def batch_arena(arena, offsets, lengths, *, arena_bytes=None, seeds=None, src=None,
+                dst=None, mode: int = RAW, out=None, stream=None,
+                tuning: Tuning | None = None):
+    """batch() for an in-order arena: offsets[i] + lengths[i] <= offsets[i+1],
+    all segments inside arena[:arena_bytes] (default: the whole tensor)."""
+    n = int(offsets.numel())
+    if int(lengths.numel()) != n:
+        raise ValueError("offsets/lengths size mismatch")
+    _check_sizes(n, seeds=seeds, src=src, dst=dst, out=out)
+    if out is None:
+        out = _alloc_out(n, offsets)
+    args = (_addr(arena), _arena_bytes(arena, arena_bytes), _addr(offsets), _addr(lengths),
+            _addr(seeds), _addr(src), _addr(dst), _addr(out), n, mode)
+    if tuning is None:
+        rc = lib.tulips_csum_batch_arena(*args, _stream(stream))
+    else:
+        rc = lib.tulips_csum_batch_arena_tuned(*args, C.byref(tuning), _stream(stream))
+    _check(rc, "tulips_csum_batch_arena")
+    return out
+
+
+def verify_arena(arena, offsets, lengths, *, arena_bytes=None, src=None, dst=None,
+                 mode: int = TCP, out=None, bad=None, stream=None):
+    """verify() for an in-order arena (see batch_arena)."""
+    import torch
+    n = int(offsets.numel())
+    if bad is None:
+        bad = torch.zeros(1, dtype=torch.int32, device=offsets.device)
+    rc = lib.tulips_csum_verify_arena(_addr(arena), _arena_bytes(arena, arena_bytes),
+                                      _addr(offsets), _addr(lengths), _addr(src),
+                                      _addr(dst), _addr(out), _addr(bad), n, mode,
+                                      _stream(stream))
+    _check(rc, "tulips_csum_verify_arena")
+    return bad
 
 
 def batch_fixed(arena, stride: int, length: int, n: int, *, seeds=None,
