@@ -296,6 +296,9 @@ def main():
     result = {
         "metric": METRIC,
         "value": round(value, 2),
+        "value_kind": "overlapped pipeline rate: the K launches replayed as one graph over "
+                      "`config.streams` independent branches (bursts overlap); one launch "
+                      "at a time is roofline.avg_launch_us / roofline.frac",
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": steps_done,

@@ -26,7 +26,7 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 300 python bench.py
 tail -1 $OUT/bench.log > $OUT/bench.json
 step stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python bench.py --no-cpu-baseline
-python tools/trace_bursts.py $OUT/stats/run_kernel_trace.csv > $OUT/bursts_F1500.jsonl
+python tools/trace_bursts.py $OUT/stats/run_kernel_trace.csv --all > $OUT/bursts_all.jsonl
 step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
 step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
 step pmc_rdreq 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d $OUT/pmc_rdreq -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16

@@ -4,9 +4,11 @@
   python tools/pmc_traffic.py gpurun_out/prof_<tag> profiles <tag>
 (after TAG=<tag> tools/gpu_check.sh on the GPU box)
 
-Reads <prof>/stats/run_kernel_stats.csv and the separate --pmc passes
-(<prof>/pmc_fetch, pmc_write, pmc_rdreq), and writes
+Reads <prof>/stats/run_kernel_stats.csv, <prof>/bursts_all.jsonl
+(tools/trace_bursts.py --all over the same run's kernel trace) and the
+separate --pmc passes (<prof>/pmc_fetch, pmc_write, pmc_rdreq), and writes
   profiles/rocprof_<tag>_kernel_stats.csv   (the rocprofv3 --stats summary)
+  profiles/rocprof_<tag>_bursts.jsonl       (per-burst means, every workload)
   profiles/pmc_traffic.json                 (HBM bytes per launch, per workload)
 
 HBM accounting per MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KB;
@@ -36,6 +38,7 @@ WORKLOADS = [
     ("frame_kernel<false, 16, 6, true>", None, "frames_validate_F1514"),
     ("frame_kernel<true, 16, 6, true>", None, "frames_generate_F1514"),
     ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
+    ("seg_prologue_small_kernel", None, "segment_TSO_64K_mss1460_prologue"),
     ("rss_kernel", None, "rss_toeplitz_16M"),
 ]
 # algorithmic bytes per launch (bench.py): segment bytes; frame bytes; bytes
@@ -73,6 +76,10 @@ def main():
     stats = os.path.join(prof, "stats", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(outdir, f"rocprof_{tag}_kernel_stats.csv"))
+    # per-burst serial / overlapped means of every workload (trace_bursts.py --all)
+    bursts = os.path.join(prof, "bursts_all.jsonl")
+    if os.path.exists(bursts):
+        shutil.copy(bursts, os.path.join(outdir, f"rocprof_{tag}_bursts.jsonl"))
     res = {}
     merged = defaultdict(dict)
     for sub in ("pmc_fetch", "pmc_write", "pmc_rdreq"):
