@@ -16,7 +16,7 @@ HDRS = tulips_amd/csrc/csum_common.h tulips_amd/csrc/csum_launch.h \
        include/tulips_csum.h include/tulips_csum_util.h
 OBJS = $(patsubst tulips_amd/csrc/%.hip,build/%.o,$(SRCS))
 
-.PHONY: all lib oracle clean asm stamps xcd_ab spandiag
+.PHONY: all lib oracle clean asm stamps xcd_ab spandiag genstore
 
 all: lib oracle
 
@@ -56,6 +56,15 @@ spandiag: $(foreach d,1 2 3 4 5,tools/libcsum_spandiag$(d).so)
 
 tools/libcsum_spandiag%.so: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DTULIPS_SPAN_DIAG=$* -shared -o $@ $(SRCS)
+
+# Diagnostic builds of frame generation's field stores (1: whole 16-byte
+# chunks, 2: the frame's whole first 64-byte line, 3: 2-byte stores with the
+# header chunks loaded temporal; tools/probe_genstore.py).
+# Never loaded by the product.
+genstore: $(foreach d,1 2 3,tools/libcsum_genstore$(d).so)
+
+tools/libcsum_genstore%.so: $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DTULIPS_GEN_STORE=$* -shared -o $@ $(SRCS)
 
 # Device assembly + resource usage of the kernels (for inspection).
 asm:

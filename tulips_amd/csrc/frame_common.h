@@ -284,7 +284,13 @@ load_frame(uintptr_t fa, uint32_t flen, int lane, FrameChunks<G, U>& fc)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int cc = min(lane + u * G, lim);
+#if defined(TULIPS_GEN_STORE) && TULIPS_GEN_STORE == 3
+    // diagnostic build: the header's slot loaded temporal (kept in L2 for
+    // the field stores)
+    fc.v[u] = (NT && u > 0) ? __builtin_nontemporal_load(p + cc) : p[cc];
+#else
     fc.v[u] = NT ? __builtin_nontemporal_load(p + cc) : p[cc];
+#endif
   }
 }
 
