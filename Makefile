@@ -59,9 +59,9 @@ tools/libcsum_spandiag%.so: $(SRCS) $(HDRS)
 
 # Diagnostic builds of frame generation's field stores (1: whole 16-byte
 # chunks, 2: the frame's whole first 64-byte line, 3: 2-byte stores with the
-# header chunks loaded temporal; tools/probe_genstore.py).
+# header chunks loaded temporal, 4: nt 2-byte stores; tools/probe_genstore.py).
 # Never loaded by the product.
-genstore: $(foreach d,1 2 3,tools/libcsum_genstore$(d).so)
+genstore: $(foreach d,1 2 3 4,tools/libcsum_genstore$(d).so)
 
 tools/libcsum_genstore%.so: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DTULIPS_GEN_STORE=$* -shared -o $@ $(SRCS)

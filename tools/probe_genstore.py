@@ -44,7 +44,7 @@ def main():
     # odd-aligned frames too (fields straddling dwords/chunks) for parity
     offs_odd = offs + 7
     libs = {"product": csum.lib}
-    for k in ():
+    for k in (4,):
         p = os.path.join(ROOT, "tools", f"libcsum_genstore{k}.so")
         if os.path.exists(p):
             libs[f"genstore{k}"] = load(p)
@@ -87,7 +87,7 @@ def main():
                                        round(nf * flen / ts / 8e12, 4)]
             # capped grids: several frames per subgroup, a frame's field
             # stores in flight while the next frame streams in
-            for mb, blk in ((512, 256), (1024, 256), (2048, 256), (1024, 512), (512, 1024)):
+            for mb, blk in ():
                 tc = csum.Tuning(group=16, unroll=6, nontemporal=1, max_blocks=mb, block=blk)
 
                 def fgc(i, st, tc=tc):

@@ -243,7 +243,12 @@ store_field(uintptr_t a, uint32_t v)
   typedef __attribute__((address_space(1))) uint8_t* gbyte_wptr;
   typedef __attribute__((address_space(1))) uint16_t* gshort_wptr;
   if ((a & 1) == 0) {
+#if defined(TULIPS_GEN_STORE) && TULIPS_GEN_STORE == 4
+    // diagnostic build: streaming (nt) field stores
+    __builtin_nontemporal_store(uint16_t(v), reinterpret_cast<gshort_wptr>(a));
+#else
     *reinterpret_cast<gshort_wptr>(a) = uint16_t(v);
+#endif
   } else {
     reinterpret_cast<gbyte_wptr>(a)[0] = uint8_t(v & 0xff);
     reinterpret_cast<gbyte_wptr>(a)[1] = uint8_t(v >> 8);
