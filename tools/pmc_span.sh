@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-export PMC_GEOMS=${PMC_GEOMS:-packed,span4,span8,span8t}
+export PMC_GEOMS=${PMC_GEOMS:-span4,span8}
 OUT=gpurun_out/pmc_span
 mkdir -p $OUT
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/p1 -o run -- python3 tools/pmc_var.py > $OUT/p1.log 2>&1 || { echo "p1 failed"; tail -5 $OUT/p1.log; exit 1; }

@@ -35,8 +35,10 @@ WORKLOADS = [
     ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
     ("csum_span_kernel<8, 2, true>", 342016, "ZIPF"),
     ("csum_packed_kernel<8, 4, true, 1>", 524288, "ZIPF_any_layout"),  # PF = 1
-    ("frame_kernel<false, 16, 6, true>", None, "frames_validate_F1514"),
-    ("frame_kernel<true, 16, 6, true>", None, "frames_generate_F1514"),
+    # 65,536 frames, 16 per 256-thread block (the host path's small bursts
+    # launch the same kernels with smaller grids)
+    ("frame_kernel<false, 16, 6, true>", 1048576, "frames_validate_F1514"),
+    ("frame_kernel<true, 16, 6, true>", 1048576, "frames_generate_F1514"),
     ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
     ("seg_prologue_small_kernel", None, "segment_TSO_64K_mss1460_prologue"),
     ("rss_kernel", None, "rss_toeplitz_16M"),

@@ -23,14 +23,11 @@ def main():
     NB = 4
     NMAX = 98304
     lens_all = bench.zipf_lengths(NMAX)
-    geoms = {"span4": ("span", 4), "span6": ("span", 6), "span8": ("span", 8),
-             "span10": ("span", 10), "span12": ("span", 12),
+    geoms = {"span6h1": ("span", 6, 1), "span6": ("span", 6), "span8h1": ("span", 8, 1),
+             "span8": ("span", 8),
              "packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                         block=256, sps=2),
-             "vpacked8x2": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=2, nontemporal=1,
-                                       block=256, sps=4),
-             "bal4w_u2pp": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=2, nontemporal=1,
-                                       block=256, sps=2)}
+             }
     if os.environ.get("PROBE_UNIFORM"):
         lens_all = np.full(NMAX, int(os.environ["PROBE_UNIFORM"]), np.uint16)
     out = torch.empty(NB * NMAX, dtype=torch.uint16, device=dev)
@@ -46,7 +43,8 @@ def main():
         row = {"n": n, "bytes": nb}
         for gname, t in geoms.items():
             if isinstance(t, tuple):
-                t = csum.Tuning(kind=csum.KIND_SPAN, unroll=t[1], nontemporal=1)
+                t = csum.Tuning(kind=csum.KIND_SPAN, unroll=t[1],
+                                group=t[2] if len(t) > 2 else 0, nontemporal=1)
 
                 def fn(i, sh, t=t):
                     b = i % NB

@@ -1247,11 +1247,15 @@ csum_span_kernel(SpanArgs p)
     wl[r] = lens[i];
   }
 #endif
+  // Rows read twice (this range's first HR rows are the previous range's
+  // halo, the last HR rows are this range's) are loaded temporal so that the
+  // second read, by the neighbouring workgroup, hits L2; the rest streams.
   u32x4 v[R];
 #pragma unroll
   for (uint32_t j = 0; j < R; ++j) {
     const uintptr_t a = x0 + 16u * (j * 256u + t);
-    v[j] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero));
+    const gchunk_ptr q = reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero);
+    v[j] = (j < HR || j >= U) ? load_chunk<false>(q) : load_chunk<NT>(q);
   }
   {
     // window counts below each target, and whether an entry starting in
