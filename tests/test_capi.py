@@ -155,6 +155,25 @@ def test_batch_validation_without_gpu():
     t = csum.Tuning(group=64, unroll=3, nontemporal=0, max_blocks=0)
     assert lib.tulips_csum_batch_tuned(FAKE, FAKE, FAKE, None, None, None, FAKE, 4, 0,
                                        C.byref(t), None) == 1
+    # in-order arenas: same checks, plus the tuning must be SPAN/DEFAULT with a
+    # known unroll and halo
+    assert lib.tulips_csum_batch_arena(None, 0, None, None, None, None, None, None, 0, 0,
+                                       None) == 0
+    assert lib.tulips_csum_batch_arena(None, 16, FAKE, FAKE, None, None, None, FAKE, 4, 0,
+                                       None) == 1
+    assert lib.tulips_csum_batch_arena(FAKE, 16, FAKE, FAKE, None, None, None, None, 4, 0,
+                                       None) == 1
+    assert lib.tulips_csum_batch_arena(FAKE, 16, FAKE, FAKE, None, None, None, FAKE, 4, 2,
+                                       None) == 1
+    assert lib.tulips_csum_verify_arena(FAKE, 16, FAKE, FAKE, FAKE, FAKE, None, None, 4, 2,
+                                        None) == 1
+    assert lib.tulips_csum_verify_arena(FAKE, 16, FAKE, FAKE, None, None, None, FAKE, 4, 0,
+                                        None) == 1
+    for kind, unroll, halo in ((csum.KIND_PACKED, 4, 0), (csum.KIND_SPAN, 3, 0),
+                               (csum.KIND_SPAN, 10, 1), (csum.KIND_SPAN, 8, 3)):
+        t = csum.Tuning(kind=kind, unroll=unroll, group=halo)
+        assert lib.tulips_csum_batch_arena_tuned(FAKE, 16, FAKE, FAKE, None, None, None, FAKE,
+                                                 4, 0, C.byref(t), None) == 1, (kind, unroll)
     # host ctx
     assert lib.tulips_csum_ctx_create(0, 0, None) == 1
     assert lib.tulips_csum_ctx_destroy(None) == 1
