@@ -725,9 +725,32 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                          "parity": "ok" if fnv1a_u16(out) == gold.get("F1500", {}).get(
                              "fnv1a64") else "MISMATCH"}
     ex["e2e_host_F1500"] = e2e
+    ex["mctx_host_F1500"] = mctx_leg(torch, csum, pinned, hoffs, hlens, batch_bytes, gold)
     ex["burst_latency_host"] = burst_latency(torch, csum)
     ex.update(frame_extras(torch, csum, dev, timer))
     return ex
+
+
+def mctx_leg(torch, csum, pinned, hoffs, hlens, batch_bytes, gold):
+    """The multi-device host context (tulips_csum_mctx) over every GPU this
+    process sees: one pinned F1500 host batch split byte-balanced, each
+    device's shard through its own H2D -> kernel -> D2H pipeline at once
+    (on the one-GPU box: one device; on an 8-GPU node: all eight, PCIe-bound)."""
+    ndev = torch.cuda.device_count()
+    with csum.MultiContext(list(range(ndev))) as m:
+        out = m.batch(pinned.data_ptr(), hoffs, hlens)
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 1.0 or reps < 3:
+            out = m.batch(pinned.data_ptr(), hoffs, hlens)
+            reps += 1
+        t = (time.perf_counter() - t0) / reps
+        bounds = m.bounds().tolist()
+    return {"devices": ndev, "GiBps": round(batch_bytes / t / GIB, 2),
+            "ms_per_batch": round(t * 1e3, 3), "shard_bounds": bounds,
+            "workload": "F1500 batch 0 from pinned host memory, one tulips_csum_mctx_batch_host "
+                        "call per batch",
+            "parity": "ok" if fnv1a_u16(out) == gold.get("F1500", {}).get("fnv1a64")
+            else "MISMATCH"}
 
 
 BURSTS = (1, 64, 1024)
