@@ -33,7 +33,9 @@ extern "C" {
                                        per 4 KiB * `unroll` (2/4/6/8/10/12) of arena
                                        bytes, segments finished where they
                                        start; `group` = 4 KiB rows read past
-                                       the range (1/2, 0 = 2) */
+                                       the range (1/2, 0 = 2), or 3 = none
+                                       (the crossing segment's wave reads its
+                                       own tail; `unroll` 6/7/8) */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning

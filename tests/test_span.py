@@ -24,7 +24,10 @@ import tulips_amd  # noqa: E402
 from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
-UNROLLS = (2, 4, 6, 8, 10, 12)
+# (chunks per lane, halo: 0 = default 2 rows, 1/2 rows, 3 = none: the
+# crossing segment's wave reads its own tail)
+GEOMS = ((2, 0), (4, 0), (6, 0), (8, 0), (10, 0), (12, 0), (4, 1), (8, 1), (6, 3), (7, 3),
+         (8, 3))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -43,8 +46,9 @@ def u16(t):
     return t.cpu().numpy().view(np.uint16)
 
 
-def tuning(u, nt=1):
-    return csum.Tuning(kind=csum.KIND_SPAN, unroll=u, nontemporal=nt)
+def tuning(geo, nt=1):
+    u, halo = geo
+    return csum.Tuning(kind=csum.KIND_SPAN, unroll=u, group=halo, nontemporal=nt)
 
 
 def in_order(rng, lens, max_gap=0, gap_p=0.0):
@@ -71,7 +75,7 @@ def test_zipf_digest(golden, oracle, name):
         kw = dict(src=d(np.full(n, ip4(10, 1, 0, 1), np.uint32)),
                   dst=d(np.full(n, ip4(10, 1, 0, 2), np.uint32)), mode=MODE_TCP)
     do, dl = d(offs), d(lens)
-    for t in [None] + [tuning(u) for u in UNROLLS]:
+    for t in [None] + [tuning(g) for g in GEOMS]:
         out = tulips_amd.batch_arena(arena, do, dl, arena_bytes=total, tuning=t, **kw)
         assert f"{oracle.fnv1a_u16(u16(out)):016x}" == b["fnv1a64"], t
 
@@ -89,10 +93,10 @@ def _mixed(rng, n):
     return lens
 
 
-@pytest.mark.parametrize("u", UNROLLS)
+@pytest.mark.parametrize("u", GEOMS)
 @pytest.mark.parametrize("base_off", [0, 1, 6, 15])
 def test_random_layouts_vs_oracle(oracle, u, base_off):
-    rng = np.random.default_rng(9100 + 16 * u + base_off)
+    rng = np.random.default_rng(9100 + 16 * u[0] + 4 * u[1] + base_off)
     n = 12000 + base_off
     lens = _mixed(rng, n)
     lens[-3:] = 0                 # empty segments at the very end of the arena
@@ -117,11 +121,11 @@ def test_random_layouts_vs_oracle(oracle, u, base_off):
             np.testing.assert_array_equal(u16(got), exp, err_msg=f"{hex(mode)} nt={nt}")
 
 
-@pytest.mark.parametrize("u", UNROLLS)
+@pytest.mark.parametrize("u", GEOMS)
 def test_many_segments_more_search_rounds(oracle, u):
     """300,000 segments (two 256-ary rounds before the windows), short and
     tiny lengths, a few long ones."""
-    rng = np.random.default_rng(77 + u)
+    rng = np.random.default_rng(77 + 4 * u[0] + u[1])
     n = 300000
     lens = rng.integers(0, 80, n).astype(np.uint16)
     lens[rng.integers(0, n, 30)] = 65535
@@ -133,12 +137,12 @@ def test_many_segments_more_search_rounds(oracle, u):
     np.testing.assert_array_equal(u16(got), exp)
 
 
-@pytest.mark.parametrize("u", UNROLLS)
+@pytest.mark.parametrize("u", GEOMS)
 def test_skewed_arena_falls_back_to_search(oracle, u):
     """Segment density far from even (the first tenth of the arena holds 95 %
     of the segments): the speculative offset window misses for most ranges
     and the workgroup's search takes over."""
-    rng = np.random.default_rng(31 + u)
+    rng = np.random.default_rng(31 + 4 * u[0] + u[1])
     n = 40000
     lens = np.concatenate([rng.integers(0, 40, 38000), rng.integers(30000, 65536, 2000)])
     lens = lens.astype(np.uint16)
@@ -162,7 +166,7 @@ def test_small_batches(oracle, lens):
     offs, end = in_order(rng, lens, max_gap=7, gap_p=0.5)
     arena = rng.integers(0, 256, max(end, 1) + 16, dtype=np.uint8)
     exp = oracle.batch(arena, offs, lens, mode=MODE_RAW)
-    for u in UNROLLS:
+    for u in GEOMS:
         got = tulips_amd.batch_arena(d(arena), d(offs), d(lens), arena_bytes=end,
                                      tuning=tuning(u))
         np.testing.assert_array_equal(u16(got), exp, err_msg=str(u))
@@ -221,7 +225,7 @@ def test_rejects_bad_arguments():
     rc = csum.lib.tulips_csum_batch_arena_tuned(1, 16, 1, 1, None, None, None, 1, 4, 0, t,
                                                 None)
     assert rc == 1
-    t = tuning(3)
+    t = tuning((13, 0))
     rc = csum.lib.tulips_csum_batch_arena_tuned(1, 16, 1, 1, None, None, None, 1, 4, 0, t,
                                                 None)
     assert rc == 1

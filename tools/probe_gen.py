@@ -20,18 +20,19 @@ def main():
     stream = torch.cuda.current_stream()
     timer = bench.Timer(torch, stream)
     lib = csum.lib
-    NB = 4
+    NB = int(os.environ.get("PROBE_NB", "8"))  # 8 copies: past the 256 MB MALL
     NMAX = 98304
     lens_all = bench.zipf_lengths(NMAX)
-    geoms = {"span6h1": ("span", 6, 1), "span6": ("span", 6), "span8h1": ("span", 8, 1),
-             "span8": ("span", 8),
+    geoms = {"span8": ("span", 8), "span6x": ("span", 6, 3), "span7x": ("span", 7, 3),
+             "span8x": ("span", 8, 3),
              "packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                         block=256, sps=2),
              }
     if os.environ.get("PROBE_UNIFORM"):
         lens_all = np.full(NMAX, int(os.environ["PROBE_UNIFORM"]), np.uint16)
     out = torch.empty(NB * NMAX, dtype=torch.uint16, device=dev)
-    for n in (1024, 8192, 32768, 65536, 98304):
+    sizes = [int(x) for x in os.environ.get("PROBE_SIZES", "1024,8192,32768,65536,98304").split(",")]
+    for n in sizes:
         lens = lens_all[:n]
         offs = np.zeros(n, np.uint64)
         np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])

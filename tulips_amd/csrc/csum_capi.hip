@@ -370,14 +370,13 @@ batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
   a.kind = TULIPS_CSUM_KIND_SPAN;
   a.unroll = (tuning && tuning->unroll) ? tuning->unroll : SPAN_DEFAULT_UNROLL;
   a.group = (tuning && tuning->group) ? tuning->group : 0;
-  if (a.group != 0 && a.group != 1 && a.group != 2) {
+  if (a.group < 0 || a.group > 3) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   const int32_t nt = (tuning && tuning->nontemporal >= 0) ? tuning->nontemporal : 1;
   a.nontemporal = (nt & 1) != 0;
   a.nt_store = (nt & 2) != 0;
-  if (a.unroll != 2 && a.unroll != 4 && a.unroll != 6 && a.unroll != 8 && a.unroll != 10 &&
-      a.unroll != 12) {
+  if (a.unroll < 2 || a.unroll > 12) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   return status_of(

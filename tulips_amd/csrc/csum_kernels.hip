@@ -1195,6 +1195,7 @@ csum_span_kernel(SpanArgs p)
   constexpr uint64_t W = 16ull * NC;     // bytes per range
   constexpr uint32_t NWIN = 1024;        // speculative window entries
   constexpr int UE = 4;                  // tail chunks per thread per batch
+  constexpr int UH = 6;                  // HR = 0: crossing tail chunks per lane
   __shared__ u32x4 s_raw[256 * R];       // the range's and the halo's chunks
   __shared__ uint32_t s_sc[256 * R];     // row-wise wave scans of chunk values
   __shared__ uint32_t s_tot[4 * R];      // per (row, wave) scan totals
@@ -1257,11 +1258,20 @@ csum_span_kernel(SpanArgs p)
     const gchunk_ptr q = reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero);
     v[j] = (j < HR || j >= U) ? load_chunk<false>(q) : load_chunk<NT>(q);
   }
+  // HR = 0: the segment crossing the range end (at most one, in order) is
+  // found in the window by the wave holding its entry, which loads and sums
+  // its bytes past the range itself, as soon as the window is in: no halo
+  // rows, no re-read bytes, no extra barrier.
+  int hold = -1;          // this thread's entry of the crossing segment
+  uint32_t xsum = 0;      // HR = 0: the crossing wave's sum past the range
+  uintptr_t hte = 0;      // HR = 0: the crossing segment's end
+  u32x4 hv[HR == 0 ? UH : 1];
   {
     // window counts below each target, and whether an entry starting in
     // the range runs past the halo (at most one can, in order)
     uint32_t c0 = 0, c1 = 0;
     bool far = false;
+    uintptr_t myte = 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool in = G + t + 256u * r < n;
@@ -1270,14 +1280,34 @@ csum_span_kernel(SpanArgs p)
       const uintptr_t sa = b + wo[r], se = min(b + wo[r] + wl[r], aend);
       if (in && sa >= x0 && sa < x1 && se > xe) {
         far = true;
-        s_meta[3] = se;
+        hold = r;
+        myte = se;
+        if (HR > 0) {
+          s_meta[3] = se;
+        }
       }
     }
-    const bool anyfar = __builtin_amdgcn_ballot_w64(far) != 0;
+    const uint64_t fb = __builtin_amdgcn_ballot_w64(far);
     if (lane == 0) {
       s_cnt[w] = c0;
       s_cnt[4 + w] = c1;
-      s_cnt[8 + w] = anyfar;
+      s_cnt[8 + w] = HR > 0 && fb != 0;
+    }
+    if constexpr (HR == 0) {
+      if (fb != 0) {
+        const uint32_t lc = uint32_t(__builtin_ctzll(fb));
+        hte = uintptr_t(readlane64(uint64_t(myte), lc));
+        hold = lane == lc ? hold : -1;
+        const uint32_t nh = uint32_t((hte - x1 + 15) >> 4);
+        const uintptr_t hl = x1 + 16u * (nh - 1);
+#pragma unroll
+        for (int q = 0; q < UH; ++q) {
+          const uint32_t c = lane + 64u * q;
+          hv[q] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(c < nh ? x1 + 16u * c : hl));
+        }
+      } else {
+        hold = -1;
+      }
     }
   }
   // 2. chunks to LDS with the row-wise wave scans of their values
@@ -1288,6 +1318,35 @@ csum_span_kernel(SpanArgs p)
     s_sc[j * 256u + t] = sc;
     if (lane == 63) {
       s_tot[4 * j + w] = sc;
+    }
+  }
+  if constexpr (HR == 0) {
+    // the crossing wave sums its tail past the range (first UH * 64 chunks
+    // already in flight, any rest in further batches)
+    if (hte > x1) {
+      const uint32_t nh = uint32_t((hte - x1 + 15) >> 4);
+      const uintptr_t hl = x1 + 16u * (nh - 1);
+      const int tb = int(hte - x1) - 16 * int(nh - 1);
+      uint32_t ts = 0;
+#pragma unroll
+      for (int q = 0; q < UH; ++q) {
+        const uint32_t c = lane + 64u * q;
+        ts += c + 1 < nh ? chunk_value(hv[q]) : (c + 1 == nh ? masked_value(hv[q], 0, tb) : 0u);
+      }
+      for (uint32_t c0 = 64u * UH; c0 < nh; c0 += 64u * UH) {
+#pragma unroll
+        for (int q = 0; q < UH; ++q) {
+          const uint32_t c = c0 + lane + 64u * q;
+          hv[q] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(c < nh ? x1 + 16u * c : hl));
+        }
+#pragma unroll
+        for (int q = 0; q < UH; ++q) {
+          const uint32_t c = c0 + lane + 64u * q;
+          ts += c + 1 < nh ? chunk_value(hv[q])
+                           : (c + 1 == nh ? masked_value(hv[q], 0, tb) : 0u);
+        }
+      }
+      xsum = __builtin_amdgcn_readlane(wave_incl_scan(ts), 63);
     }
   }
   lds_barrier();
@@ -1353,7 +1412,7 @@ csum_span_kernel(SpanArgs p)
   // 5. one segment: prefix differences over [x0, xe) plus the tail
   const uint32_t want = (p.mode & FLAG_COMPLEMENT) ? 0u : 0xffffu;
   const bool side_in = (p.mode & MODE_MASK) == MODE_TCP || p.seeds != nullptr;
-  auto emit = [&](uint32_t s, bool mine, uint64_t so, uint32_t sl) {
+  auto emit = [&](uint32_t s, bool mine, uint64_t so, uint32_t sl, uint32_t ext) {
     SideIn side{0, 0, 0};
     if (side_in) {
       side = load_side(mine ? s : 0u, p.seeds, p.src, p.dst, p.mode);
@@ -1401,7 +1460,8 @@ csum_span_kernel(SpanArgs p)
       const uint32_t i = G + t + 256u * r;
       const bool mine = i >= lo && i < hi;
       if (__builtin_amdgcn_ballot_w64(mine) != 0) {
-        emit(i, mine, mine ? wo[r] : 0, mine ? wl[r] : 0u);
+        emit(i, mine, mine ? wo[r] : 0, mine ? wl[r] : 0u, HR == 0 ? (hold == r ? xsum : 0u)
+                                                                     : ext);
       }
     }
   } else {
@@ -1449,7 +1509,7 @@ csum_span_kernel(SpanArgs p)
     for (uint32_t s0 = lo; s0 < hi; s0 += 256u) {
       const uint32_t s = s0 + t;
       const bool mine = s < hi;
-      emit(s, mine, mine ? p.offs[s] : 0, mine ? p.lens[s] : 0u);
+      emit(s, mine, mine ? p.offs[s] : 0, mine ? p.lens[s] : 0u, ext);
     }
   }
 #ifdef TULIPS_CSUM_STAMPS
@@ -1680,13 +1740,17 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
   if (a.n == 0) {
     return hipSuccess;
   }
-  // group = halo rows of 4 KiB past the range (1 or 2; 0 = 2)
-  const int hr = a.group ? a.group : 2;
+  // group = halo rows of 4 KiB read past the range (1 or 2), or 3 = none:
+  // the crossing segment's wave reads exactly its tail (0 = default)
+  const int hr = a.group == 0 ? 2 : (a.group == 3 ? 0 : a.group);
 #define TCS_SCASE(U_, H_)                                                      \
   if (a.unroll == U_ && hr == H_) {                                            \
     return a.nontemporal ? launch_span_u<U_, H_, true>(sp, stream)             \
                          : launch_span_u<U_, H_, false>(sp, stream);           \
   }
+  TCS_SCASE(6, 0)
+  TCS_SCASE(7, 0)
+  TCS_SCASE(8, 0)
   TCS_SCASE(2, 1)
   TCS_SCASE(2, 2)
   TCS_SCASE(4, 1)
