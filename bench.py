@@ -618,6 +618,22 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     t = timer(lambda i, st: lib.tulips_csum_stream_read(arena.data_ptr(), nbytes,
                                                         sink.data_ptr(), 0, st), 10)
     ex["stream_read_ceiling_GBps"] = round(nbytes / t / 1e9, 1)
+    # ... and of one 98.3 MB batch per launch, rotated like the F1500 steps:
+    # what a single launch of that size can read (ramp and drain included)
+    def one(i, st):
+        b = i % NBATCH
+        lib.tulips_csum_stream_read(arena.data_ptr() + b * batch_bytes, batch_bytes,
+                                    sink.data_ptr(), 0, st)
+    for i in range(NBATCH):
+        one(i, sh)
+    t1 = timer(one, 64)
+    tp1 = timer(one, 64, branches=PIPE)
+    ex["stream_read_F1500_batch"] = {
+        "what": "plain 16-byte streaming read of one F1500 batch per launch (98.3 MB), "
+                "batches rotated: the single-launch ceiling roofline.frac compares with",
+        "avg_launch_us": round(t1 * 1e6, 2),
+        "frac_of_peak": round(batch_bytes / t1 / 1e9 / HBM_PEAK_GBS, 4),
+        "pipeline": pipe_entry(batch_bytes, tp1)}
 
     # F9000 (configs[2]): 2 distinct 590 MB batches, rotated (> Infinity Cache)
     L9 = 9000
