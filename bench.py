@@ -702,6 +702,16 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     tp = timer(fz, 80, branches=PIPE)
     o = oz[:NSEG].cpu().numpy().view(np.uint16)
     zgold = gold.get("ZIPF", {}).get("fnv1a64")
+    # the single-launch read ceiling for these bytes: a plain streaming read
+    # of one ZIPF arena per launch, the 8 copies rotated
+    zsink = torch.zeros(4, dtype=torch.int32, device=dev)
+    zr = zb & ~15
+
+    def fzr(i, st):
+        b = i % nz
+        lib.tulips_csum_stream_read(az.data_ptr() + b * zr, zr, zsink.data_ptr(), 0, st)
+    tr = timer(fzr, 80)
+    trp = timer(fzr, 80, branches=PIPE)
     ex["ZIPF"] = {"GiBps": round(zb / t / GIB, 1), "Mseg_per_s": round(NSEG / t / 1e6, 1),
                   "frac_of_peak": round(zb / t / 1e9 / HBM_PEAK_GBS, 4),
                   "avg_launch_us": round(t * 1e6, 2),
@@ -711,6 +721,9 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                               "segments finished where they start",
                   "traffic": read_traffic("ZIPF"),
                   "parity": "ok" if fnv1a_u16(o) == zgold else "MISMATCH",
+                  "read_same_bytes": {"avg_launch_us": round(tr * 1e6, 2),
+                                      "frac_of_peak": round(zr / tr / 1e9 / HBM_PEAK_GBS, 4),
+                                      "pipeline": pipe_entry(zr, trp)},
                   "any_layout": {
                       "entry": "tulips_csum_batch (offsets only)",
                       "geometry": "packed: one wave per 8 segments, chunks packed end to "

@@ -35,7 +35,11 @@ extern "C" {
                                        start; `group` = 4 KiB rows read past
                                        the range (1/2, 0 = 2), or 3 = none
                                        (the crossing segment's wave reads its
-                                       own tail; `unroll` 6/7/8) */
+                                       own tail; `unroll` 6/7/8), or 4/5 =
+                                       boundary-slot form with 2/1 halo rows
+                                       (only the chunks a segment starts or
+                                       ends in are staged; `unroll`
+                                       4/6/8/10/12 for 4, 8 for 5) */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning

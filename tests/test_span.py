@@ -25,9 +25,10 @@ from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
 # (chunks per lane, halo: 0 = default 2 rows, 1/2 rows, 3 = none: the
-# crossing segment's wave reads its own tail)
+# crossing segment's wave reads its own tail, 4/5 = boundary-slot form with
+# 2/1 rows)
 GEOMS = ((2, 0), (4, 0), (6, 0), (8, 0), (10, 0), (12, 0), (4, 1), (8, 1), (6, 3), (7, 3),
-         (8, 3))
+         (8, 3), (4, 4), (6, 4), (8, 4), (8, 5), (10, 4), (12, 4))
 
 
 @pytest.fixture(scope="module", autouse=True)

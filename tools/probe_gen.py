@@ -23,8 +23,8 @@ def main():
     NB = int(os.environ.get("PROBE_NB", "8"))  # 8 copies: past the 256 MB MALL
     NMAX = 98304
     lens_all = bench.zipf_lengths(NMAX)
-    geoms = {"span8": ("span", 8), "span6x": ("span", 6, 3), "span7x": ("span", 7, 3),
-             "span8x": ("span", 8, 3),
+    geoms = {"span8": ("span", 8), "s2_8h2": ("span", 8, 4), "s2_8h1": ("span", 8, 5),
+             "s2_6h2": ("span", 6, 4), "s2_10h2": ("span", 10, 4),
              "packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                         block=256, sps=2),
              }

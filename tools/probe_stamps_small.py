@@ -41,9 +41,8 @@ def main():
     stamps = torch.zeros(4 * 300000, dtype=torch.int64, device=dev)
     sh = torch.cuda.current_stream().cuda_stream
     geoms = {"packed8x4pf": (csum.KIND_PACKED, 8, 4, 2, 256),
-             "span4": (csum.KIND_SPAN, 2, 4, 0, 0),
-             "span6": (csum.KIND_SPAN, 2, 6, 0, 0),
-             "span8": (csum.KIND_SPAN, 2, 8, 0, 0)}
+             "span8": (csum.KIND_SPAN, 2, 8, 0, 0),
+             "s2_8h2": (csum.KIND_SPAN, 4, 8, 0, 0)}
     only = os.environ.get("PROBE_GEOMS")
     if only:
         geoms = {k: v for k, v in geoms.items() if k in only.split(",")}

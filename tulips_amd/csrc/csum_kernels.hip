@@ -1258,6 +1258,11 @@ csum_span_kernel(SpanArgs p)
     const gchunk_ptr q = reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero);
     v[j] = (j < HR || j >= U) ? load_chunk<false>(q) : load_chunk<NT>(q);
   }
+  // every load is out before the first wait: without this fence the
+  // scheduler pulls the window's first uses between the chunk loads, and the
+  // vmcnt waits they bring hold the remaining chunk loads back for a whole
+  // round trip
+  __builtin_amdgcn_sched_barrier(0);
   // HR = 0: the segment crossing the range end (at most one, in order) is
   // found in the window by the wave holding its entry, which loads and sums
   // its bytes past the range itself, as soon as the window is in: no halo
@@ -1517,6 +1522,333 @@ csum_span_kernel(SpanArgs p)
 #endif
 }
 
+// SPAN, boundary-slot form (`group` 4/5 = halo rows 2/1): the same work
+// cut, but only the chunks a segment boundary falls in are staged in LDS.
+// The holder of a segment's window entry knows its first and last chunk as
+// soon as the window is in (before the range's data): it marks them in a
+// per-chunk word (head slot in the low half, tail slot in the high half,
+// slot = window index mod 128); after one barrier the chunk's owner copies
+// the chunk into that slot; after a second the holder sums its segment from
+// the slots and the prefix. LDS per workgroup is ~1.25 KiB per 1 KiB of range
+// smaller than the staged form, so twice as many workgroups are resident.
+// Segments shorter than 32 B (two heads or tails could share a chunk) or
+// more than 128 starting in one range take their boundary chunks from
+// memory instead (uniform per workgroup).
+template<int U, int HR, bool NT>
+__global__ __launch_bounds__(256) void
+csum_span2_kernel(SpanArgs p)
+{
+  constexpr uint32_t R = U + HR;         // rows of 256 chunks: range + halo
+  constexpr uint32_t NC = 256u * U;      // chunks per range
+  constexpr uint64_t W = 16ull * NC;     // bytes per range
+  constexpr uint32_t NWIN = 1024;        // speculative window entries
+  constexpr uint32_t NSLOT = 128;        // boundary slots (window index mod 128)
+  constexpr int UE = 4;                  // tail chunks per thread per batch
+  __shared__ uint32_t s_mk[256 * R];     // per chunk: head slot + 1 | tail slot + 1 << 16
+  __shared__ uint32_t s_sc[256 * R];     // row-wise wave scans of chunk values
+  __shared__ u32x4 s_head[NSLOT];        // a segment's first chunk
+  __shared__ u32x4 s_tail[NSLOT];        // a segment's last chunk
+  __shared__ uint32_t s_tot[4 * R];      // per (row, wave) scan totals
+  __shared__ uint32_t s_woff[4][4 * R];  // each wave's copy of their exclusive prefix
+  __shared__ uint32_t s_cnt[16];         // per wave: window counts, tail flag, tiny flag
+  __shared__ uint64_t s_meta[4];         // end of a segment past the halo; search
+  __shared__ uint32_t s_ext[4];
+
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const uint32_t k = xcd_block(blockIdx.x, gridDim.x);
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p.base);
+  const uint64_t d = b & 15u;
+  const uintptr_t x0 = (b & ~uintptr_t(15)) + uint64_t(k) * W, x1 = x0 + W;
+  const uintptr_t xe = x1 + 16u * 256u * HR; // end of the halo
+  const uintptr_t aend = b + p.arena;
+  const uintptr_t zero = reinterpret_cast<uintptr_t>(k_zero_chunk);
+  const uintptr_t last = p.arena ? ((aend - 1) & ~uintptr_t(15)) : zero;
+  const uint32_t n = p.n;
+  const gu64_ptr offs = reinterpret_cast<gu64_ptr>(reinterpret_cast<uintptr_t>(p.offs));
+  const gu16_ptr lens = reinterpret_cast<gu16_ptr>(reinterpret_cast<uintptr_t>(p.lens));
+  const uint64_t tg0 = k ? uint64_t(k) * W - d : 0, tg1 = uint64_t(k + 1) * W - d;
+  auto chunk_at = [&](uintptr_t a) {
+    return load_chunk<false>(reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero));
+  };
+#ifdef TULIPS_CSUM_STAMPS
+  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
+
+  // 0. clear the marks (the barrier costs little before any load is out)
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    s_mk[j * 256u + t] = 0;
+  }
+  lds_barrier();
+  // 1. one round trip: the offsets window, then the range + halo
+  const uint64_t mid = (tg0 + tg1) / 2;
+  const uint64_t guess = uint64_t(double(n) * double(mid) / double(p.arena ? p.arena : 1));
+  const uint32_t gmax = n > NWIN ? n - NWIN : 0u;
+  const uint32_t G = uint32_t(min(guess > NWIN / 2 ? guess - NWIN / 2 : 0ull, uint64_t(gmax)));
+  uint64_t wo[4];
+  uint32_t wl[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t i = min(G + t + 256u * r, n - 1);
+    wo[r] = offs[i];
+    wl[r] = lens[i];
+  }
+  u32x4 v[R];
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    const uintptr_t a = x0 + 16u * (j * 256u + t);
+    const gchunk_ptr q = reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero);
+    v[j] = (j < HR || j >= U) ? load_chunk<false>(q) : load_chunk<NT>(q);
+  }
+  // every load is out before the first wait: without this fence the
+  // scheduler pulls the window's first uses between the chunk loads, and the
+  // vmcnt waits they bring hold the remaining chunk loads back for a whole
+  // round trip
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    // window counts, the segment past the halo, and the boundary marks of
+    // every entry starting in the range
+    uint32_t c0 = 0, c1 = 0;
+    bool far = false, tiny = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t e = G + t + 256u * r;
+      const bool in = e < n;
+      c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg0));
+      c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg1));
+      const uintptr_t sa = b + wo[r], se = min(b + wo[r] + wl[r], aend);
+      const bool starts = in && sa >= x0 && sa < x1;
+      if (starts && se > xe) {
+        far = true;
+        s_meta[3] = se;
+      }
+      if (starts && se > sa) {
+        tiny = tiny || wl[r] < 32u;
+        const uintptr_t ie = min(se, xe);
+        const uint32_t ca = uint32_t((sa - x0) >> 4), ce = uint32_t((ie - 1 - x0) >> 4);
+        const uint32_t slot = (e & (NSLOT - 1)) + 1;
+        atomicOr(&s_mk[ca], slot);
+        atomicOr(&s_mk[ce], slot << 16);
+      }
+    }
+    const bool anyfar = __builtin_amdgcn_ballot_w64(far) != 0;
+    const bool anytiny = __builtin_amdgcn_ballot_w64(tiny) != 0;
+    if (lane == 0) {
+      s_cnt[w] = c0;
+      s_cnt[4 + w] = c1;
+      s_cnt[8 + w] = anyfar;
+      s_cnt[12 + w] = anytiny;
+    }
+  }
+  // 2. row-wise wave scans of the chunk values
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    const uint32_t sc = wave_incl_scan(chunk_value(v[j]));
+    s_sc[j * 256u + t] = sc;
+    if (lane == 63) {
+      s_tot[4 * j + w] = sc;
+    }
+  }
+  lds_barrier();
+  // 3. requested chunks to their slots (all marks read first: a read after a
+  //    slot store would wait for it)
+  uint32_t mks[R];
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    mks[j] = s_mk[j * 256u + t];
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    // (marks OR-ed together by colliding entries are never read back, but
+    // must not index past the slots)
+    const uint32_t mk = mks[j];
+    const uint32_t mh = (mk & 0xffffu) - 1, mt = (mk >> 16) - 1;
+    if (mh < NSLOT) {
+      s_head[mh] = v[j];
+    }
+    if (mt < NSLOT) {
+      s_tail[mt] = v[j];
+    }
+  }
+  {
+    const uint32_t x = lane < 4 * R ? s_tot[lane] : 0u;
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane < 4 * R) {
+      s_woff[w][lane] = inc - x;
+    }
+  }
+  lds_barrier();
+#ifdef TULIPS_CSUM_STAMPS
+  const uint64_t stamp_mid = __builtin_amdgcn_s_memrealtime();
+#endif
+  auto P = [&](uint32_t c) { return s_woff[w][c >> 6] + s_sc[c]; };
+  const uint32_t c0 = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  const uint32_t c1 = s_cnt[4] + s_cnt[5] + s_cnt[6] + s_cnt[7];
+  const bool tail = (s_cnt[8] | s_cnt[9] | s_cnt[10] | s_cnt[11]) != 0;
+  const bool tiny = (s_cnt[12] | s_cnt[13] | s_cnt[14] | s_cnt[15]) != 0;
+  const uint32_t nw = min(NWIN, n - G);
+  const bool tail_ok = G + NWIN >= n;
+  const bool ok = (c0 > 0 || G == 0) && (c0 < nw || tail_ok) && (c1 > 0 || G == 0) &&
+                  (c1 < nw || tail_ok);
+
+  auto tail_sum = [&](uintptr_t te) {
+    const uint32_t tch = uint32_t((te - xe + 15) >> 4);
+    const uintptr_t tlast = xe + 16u * (tch - 1);
+    const int tbytes = int(te - xe) - 16 * int(tch - 1);
+    uint32_t tsum = 0;
+    for (uint32_t q0 = 0; q0 < tch; q0 += 256u * UE) {
+      u32x4 e[UE];
+#pragma unroll
+      for (int j = 0; j < UE; ++j) {
+        const uint32_t c = q0 + t + 256u * j;
+        e[j] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(c < tch ? xe + 16u * c : tlast));
+      }
+#pragma unroll
+      for (int j = 0; j < UE; ++j) {
+        const uint32_t c = q0 + t + 256u * j;
+        tsum += c + 1 < tch ? chunk_value(e[j])
+                            : (c + 1 == tch ? masked_value(e[j], 0, tbytes) : 0u);
+      }
+    }
+    tsum = wave_incl_scan(tsum);
+    if (lane == 63) {
+      s_ext[w] = tsum;
+    }
+    lds_barrier();
+    return s_ext[0] + s_ext[1] + s_ext[2] + s_ext[3];
+  };
+  uint32_t ext = 0;
+
+  const uint32_t want = (p.mode & FLAG_COMPLEMENT) ? 0u : 0xffffu;
+  const bool side_in = (p.mode & MODE_MASK) == MODE_TCP || p.seeds != nullptr;
+  // slots: boundary chunks from the LDS slots (slot >= 0) or from memory
+  auto emit = [&](uint32_t s, bool mine, uint64_t so, uint32_t sl, int slot) {
+    SideIn side{0, 0, 0};
+    if (side_in) {
+      side = load_side(mine ? s : 0u, p.seeds, p.src, p.dst, p.mode);
+    }
+    const uintptr_t sa = min(max(b + so, x0), x1 - 1);
+    const uintptr_t se = min(b + so + sl, aend);
+    const uintptr_t ie = min(se, xe);
+    uint32_t sum = 0;
+    if (ie > sa) {
+      const uint32_t ca = uint32_t((sa - x0) >> 4);
+      const uint32_t ce = uint32_t((ie - 1 - x0) >> 4);
+      const int ha = int(sa & 15u), tb = int(((ie - 1) & 15u) + 1u);
+      u32x4 hv, tv;
+      if (slot >= 0) {
+        hv = s_head[slot];
+        tv = s_tail[slot];
+      } else {
+        hv = chunk_at(x0 + 16u * ca);
+        tv = chunk_at(x0 + 16u * ce);
+      }
+      sum = ca == ce ? masked_value(hv, ha, tb)
+                     : masked_value(hv, ha, 16) + (P(ce - 1) - P(ca)) + masked_value(tv, 0, tb);
+    }
+    sum += se > xe ? ext : 0u;
+    const uint32_t r =
+      finish(sum, (sa & 1u) != 0, p.mode, side.seed, side.src, side.dst, sl);
+    if (mine && p.out) {
+      if (p.nt_store) {
+        __builtin_nontemporal_store(uint16_t(r), p.out + s);
+      } else {
+        p.out[s] = uint16_t(r);
+      }
+    }
+    if (p.bad) {
+      const uint32_t nb =
+        __builtin_popcountll(__builtin_amdgcn_ballot_w64(mine && r != want));
+      if (lane == 0 && nb) {
+        atomicAdd(p.bad + CNT_LINE * (blockIdx.x % CNT_SHARDS), nb);
+      }
+    }
+  };
+
+  if (ok) {
+    const uint32_t lo = G + c0, hi = G + c1;
+    if (tail) {
+      ext = tail_sum(s_meta[3]);
+    }
+    // slots are unambiguous unless > 128 segments start here or some are short
+    const bool slots = !tiny && hi - lo <= NSLOT;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t i = G + t + 256u * r;
+      const bool mine = i >= lo && i < hi;
+      if (__builtin_amdgcn_ballot_w64(mine) != 0) {
+        emit(i, mine, mine ? wo[r] : 0, mine ? wl[r] : 0u,
+             slots ? int(i & (NSLOT - 1)) : -1);
+      }
+    }
+  } else {
+    if (w == 0) {
+      uint32_t L0 = 0, R0 = n, L1 = 0, R1 = n;
+      while (R0 > L0 || R1 > L1) {
+        const uint32_t st0 = (R0 - L0 + 255u) >> 8, st1 = (R1 - L1 + 255u) >> 8;
+        uint64_t o0[4], o1[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t q = lane + 64u * r;
+          o0[r] = offs[min(uint64_t(L0) + uint64_t(q) * st0, uint64_t(n - 1))];
+          o1[r] = offs[min(uint64_t(L1) + uint64_t(q) * st1, uint64_t(n - 1))];
+        }
+        uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t q = lane + 64u * r;
+          const bool in0 = uint64_t(L0) + uint64_t(q) * st0 < R0;
+          const bool in1 = uint64_t(L1) + uint64_t(q) * st1 < R1;
+          d0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in0 && o0[r] < tg0));
+          d1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in1 && o1[r] < tg1));
+        }
+        if (R0 > L0) {
+          span_narrow(L0, R0, st0, __builtin_amdgcn_readfirstlane(d0));
+        }
+        if (R1 > L1) {
+          span_narrow(L1, R1, st1, __builtin_amdgcn_readfirstlane(d1));
+        }
+      }
+      if (lane == 0) {
+        s_meta[0] = L0;
+        s_meta[1] = L1;
+      }
+    }
+    lds_barrier();
+    const uint32_t lo = uint32_t(s_meta[0]), hi = uint32_t(s_meta[1]);
+    if (hi > lo) {
+      const uintptr_t te = min(b + p.offs[hi - 1] + p.lens[hi - 1], aend);
+      if (te > xe) {
+        ext = tail_sum(te);
+      }
+    }
+    for (uint32_t s0 = lo; s0 < hi; s0 += 256u) {
+      const uint32_t s = s0 + t;
+      const bool mine = s < hi;
+      emit(s, mine, mine ? p.offs[s] : 0, mine ? p.lens[s] : 0u, -1);
+    }
+  }
+#ifdef TULIPS_CSUM_STAMPS
+  stamp_wave_mid(stamp0, stamp_mid);
+#endif
+}
+
+template<int U, int HR, bool NT>
+hipError_t
+launch_span2_u(const SpanArgs& sp, hipStream_t stream)
+{
+  constexpr uint64_t W = 4096ull * U;
+  const uint64_t ranges = ((sp.arena + (reinterpret_cast<uintptr_t>(sp.base) & 15u)) / W) + 1;
+  if (ranges > 0x7fffffffull) {
+    return hipErrorInvalidValue;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_span2_kernel<U, HR, NT>), dim3(uint32_t(ranges)), dim3(256), 0,
+                     stream, sp);
+  return hipGetLastError();
+}
+
 template<int U, int HR, bool NT>
 hipError_t
 launch_span_u(const SpanArgs& sp, hipStream_t stream)
@@ -1741,7 +2073,23 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
     return hipSuccess;
   }
   // group = halo rows of 4 KiB read past the range (1 or 2), or 3 = none:
-  // the crossing segment's wave reads exactly its tail (0 = default)
+  // the crossing segment's wave reads exactly its tail (0 = default);
+  // 4 / 5 = the boundary-slot form with 2 / 1 halo rows
+  if (a.group == 4 || a.group == 5) {
+#define TCS_S2CASE(U_, H_)                                                     \
+  if (a.unroll == U_ && (a.group == 4 ? 2 : 1) == H_) {                        \
+    return a.nontemporal ? launch_span2_u<U_, H_, true>(sp, stream)            \
+                         : launch_span2_u<U_, H_, false>(sp, stream);          \
+  }
+    TCS_S2CASE(4, 2)
+    TCS_S2CASE(6, 2)
+    TCS_S2CASE(8, 2)
+    TCS_S2CASE(8, 1)
+    TCS_S2CASE(10, 2)
+    TCS_S2CASE(12, 2)
+#undef TCS_S2CASE
+    return hipErrorInvalidValue;
+  }
   const int hr = a.group == 0 ? 2 : (a.group == 3 ? 0 : a.group);
 #define TCS_SCASE(U_, H_)                                                      \
   if (a.unroll == U_ && hr == H_) {                                            \
