@@ -49,10 +49,11 @@ tools/libcsum_xcd%.so: $(SRCS) $(HDRS)
 
 # Diagnostic builds of the arena-span kernel that stop after staging the
 # chunks (1: without, 2: with the offsets window), once [lo, hi) is known (3),
-# before the segment pass (4), or without result stores (5)
+# before the segment pass (4), without result stores (5), or with each
+# workgroup's results stored to its own 256-byte block (6)
 # (tools/probe_spandiag.py).
 # Never loaded by the product.
-spandiag: $(foreach d,1 2 3 4 5,tools/libcsum_spandiag$(d).so)
+spandiag: $(foreach d,1 2 3 4 5 6,tools/libcsum_spandiag$(d).so)
 
 tools/libcsum_spandiag%.so: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DTULIPS_SPAN_DIAG=$* -shared -o $@ $(SRCS)

@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Where the arena-span kernel's time goes on the §8c ZIPF batch: the product
 kernel vs diagnostic builds that stop after staging the chunks in LDS
-(tools/libcsum_spandiag1.so: no offsets window; 2: with it), and the plain
-streaming read of the same bytes; serial and 4-branch pipelined."""
+(tools/libcsum_spandiag1.so: no offsets window; 2, 3: with it), before the
+segment pass (4; the boundary-slot form: once its slots are filled) or that
+skip the result stores (5) or store each workgroup's results to a 256-byte
+block of its own (6, v5 only), and the plain streaming read of the same bytes;
+serial and 4-branch pipelined. `g` = tuning group: 2 = v5 (product), 4 =
+boundary-slot form."""
 import ctypes as C
 import json
 import os
@@ -34,7 +38,7 @@ def main():
     offs = np.zeros(n, np.uint64)
     np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
     nb = int(lens.astype(np.int64).sum())
-    NB = 4
+    NB = int(os.environ.get("PROBE_NB", "8"))  # 8 copies: past the 256 MB MALL
     arena = torch.empty(NB * nb + 256, dtype=torch.uint8, device=dev)
     csum.fill_splitmix(arena, NB * nb)
     doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
@@ -46,13 +50,14 @@ def main():
             "diag2": load(os.path.join(ROOT, "tools", "libcsum_spandiag2.so")),
             "diag3": load(os.path.join(ROOT, "tools", "libcsum_spandiag3.so")),
             "diag4": load(os.path.join(ROOT, "tools", "libcsum_spandiag4.so")),
-            "diag5": load(os.path.join(ROOT, "tools", "libcsum_spandiag5.so"))}
+            "diag5": load(os.path.join(ROOT, "tools", "libcsum_spandiag5.so")),
+            "diag6": load(os.path.join(ROOT, "tools", "libcsum_spandiag6.so"))}
     row = {"n": n, "bytes": nb}
-    for u, hr in ((4, 1), (4, 2), (6, 2), (8, 2)):
+    for u, hr in ((8, 2), (8, 4)):
         t = csum.Tuning(kind=csum.KIND_SPAN, unroll=u, group=hr, nontemporal=1)
-        for lname, lib in libs.items():
-            if lname in ("diag1", "diag2", "diag4"):
-                continue
+        for lname, lib in list(libs.items()) + [("product_ntstore", csum.lib)]:
+            if lname == "product_ntstore":
+                t = csum.Tuning(kind=csum.KIND_SPAN, unroll=u, group=hr, nontemporal=3)
             def fn(i, sh, lib=lib, t=t):
                 b = i % NB
                 assert lib.tulips_csum_batch_arena_tuned(
@@ -62,9 +67,7 @@ def main():
                 fn(i, stream.cuda_stream)
             ts = float(np.median([timer(fn, 64) for _ in range(3)]))
             tp = float(np.median([timer(fn, 64, branches=4) for _ in range(3)]))
-            if lname in ("diag1", "diag2", "diag4"):
-                continue
-            row[f"span{u}h{hr}_{lname}"] = [round(ts * 1e6, 2), round(tp * 1e6, 2)]
+            row[f"span{u}g{hr}_{lname}"] = [round(ts * 1e6, 2), round(tp * 1e6, 2)]
 
     def fr(i, sh):
         b = i % NB

@@ -1358,7 +1358,7 @@ csum_span_kernel(SpanArgs p)
 #ifdef TULIPS_CSUM_STAMPS
   const uint64_t stamp_mid = __builtin_amdgcn_s_memrealtime();
 #endif
-#if defined(TULIPS_SPAN_DIAG) && TULIPS_SPAN_DIAG > 0
+#if defined(TULIPS_SPAN_DIAG) && TULIPS_SPAN_DIAG > 0 && TULIPS_SPAN_DIAG < 4
   // diagnostic builds: stop after the chunks are staged and scanned
   if (t == 0 && p.out && k < n) {
     p.out[k] = uint16_t(s_tot[0] + s_cnt[0] + s_sc[5]);
@@ -1375,6 +1375,13 @@ csum_span_kernel(SpanArgs p)
       s_woff[w][lane] = inc - x;
     }
   }
+#if TULIPS_SPAN_DIAG == 4
+  // diagnostic build: stop before the segment pass
+  if (t == 0 && p.out && k < n) {
+    p.out[k] = uint16_t(s_woff[w][1] + s_cnt[0] + s_sc[5]);
+  }
+  return;
+#endif
   auto P = [&](uint32_t c) { return s_woff[w][c >> 6] + s_sc[c]; };
   const uint32_t c0 = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
   const uint32_t c1 = s_cnt[4] + s_cnt[5] + s_cnt[6] + s_cnt[7];
@@ -1437,12 +1444,22 @@ csum_span_kernel(SpanArgs p)
     sum += se > xe ? ext : 0u;
     const uint32_t r =
       finish(sum, (sa & 1u) != 0, p.mode, side.seed, side.src, side.dst, sl);
+#if TULIPS_SPAN_DIAG == 5
+    if (mine && p.out && r == 0x1234567u) {
+#else
     if (mine && p.out) {
+#endif
+#if TULIPS_SPAN_DIAG == 6
+      // diagnostic build: each workgroup's results to its own 256-byte block
+      // (wrong layout; only the store pattern differs)
+      p.out[(k * 128u + (s & 127u)) % n] = uint16_t(r);
+#else
       if (p.nt_store) {
         __builtin_nontemporal_store(uint16_t(r), p.out + s);
       } else {
         p.out[s] = uint16_t(r);
       }
+#endif
     }
     if (p.bad) {
       const uint32_t nb =
@@ -1651,6 +1668,13 @@ csum_span2_kernel(SpanArgs p)
     }
   }
   lds_barrier();
+#if TULIPS_SPAN_DIAG == 2 || TULIPS_SPAN_DIAG == 3
+  // diagnostic builds: stop once the range is in and scanned
+  if (t == 0 && p.out && k < n) {
+    p.out[k] = uint16_t(s_tot[0] + s_cnt[0] + s_mk[5]);
+  }
+  return;
+#endif
   // 3. requested chunks to their slots (all marks read first: a read after a
   //    slot store would wait for it)
   uint32_t mks[R];
@@ -1681,6 +1705,13 @@ csum_span2_kernel(SpanArgs p)
   lds_barrier();
 #ifdef TULIPS_CSUM_STAMPS
   const uint64_t stamp_mid = __builtin_amdgcn_s_memrealtime();
+#endif
+#if TULIPS_SPAN_DIAG == 4
+  // diagnostic build: stop once the slots are filled
+  if (t == 0 && p.out && k < n) {
+    p.out[k] = uint16_t(s_woff[w][1] + s_cnt[0] + s_head[5][0]);
+  }
+  return;
 #endif
   auto P = [&](uint32_t c) { return s_woff[w][c >> 6] + s_sc[c]; };
   const uint32_t c0 = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
@@ -1750,12 +1781,22 @@ csum_span2_kernel(SpanArgs p)
     sum += se > xe ? ext : 0u;
     const uint32_t r =
       finish(sum, (sa & 1u) != 0, p.mode, side.seed, side.src, side.dst, sl);
+#if TULIPS_SPAN_DIAG == 5
+    if (mine && p.out && r == 0x1234567u) {
+#else
     if (mine && p.out) {
+#endif
+#if TULIPS_SPAN_DIAG == 6
+      // diagnostic build: each workgroup's results to its own 256-byte block
+      // (wrong layout; only the store pattern differs)
+      p.out[(k * 128u + (s & 127u)) % n] = uint16_t(r);
+#else
       if (p.nt_store) {
         __builtin_nontemporal_store(uint16_t(r), p.out + s);
       } else {
         p.out[s] = uint16_t(r);
       }
+#endif
     }
     if (p.bad) {
       const uint32_t nb =
