@@ -42,7 +42,10 @@ def main():
         doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
         dlens = torch.from_numpy(lens.view(np.int16)).to(dev)
         row = {"n": n, "bytes": nb}
+        only = os.environ.get("PROBE_GEOMS")
         for gname, t in geoms.items():
+            if only and gname not in only.split(","):
+                continue
             if isinstance(t, tuple):
                 t = csum.Tuning(kind=csum.KIND_SPAN, unroll=t[1],
                                 group=t[2] if len(t) > 2 else 0, nontemporal=1)
