@@ -754,7 +754,10 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                          "parity": "ok" if fnv1a_u16(out) == gold.get("F1500", {}).get(
                              "fnv1a64") else "MISMATCH"}
     ex["e2e_host_F1500"] = e2e
-    ex["mctx_host_F1500"] = mctx_leg(torch, csum, pinned, hoffs, hlens, batch_bytes, gold)
+    try:  # every visible device: on a multi-GPU node a failure here must not cost the line
+        ex["mctx_host_F1500"] = mctx_leg(torch, csum, pinned, hoffs, hlens, batch_bytes, gold)
+    except Exception as e:  # noqa: BLE001
+        ex["mctx_host_F1500"] = {"error": repr(e)}
     ex["burst_latency_host"] = burst_latency(torch, csum)
     ex.update(frame_extras(torch, csum, dev, timer))
     return ex
