@@ -53,7 +53,9 @@ def main():
             "diag5": load(os.path.join(ROOT, "tools", "libcsum_spandiag5.so")),
             "diag6": load(os.path.join(ROOT, "tools", "libcsum_spandiag6.so"))}
     row = {"n": n, "bytes": nb}
-    for u, hr in ((8, 2), (8, 4)):
+    geoms = [tuple(int(x) for x in g.split(":"))
+             for g in os.environ.get("PROBE_SPAN", "8:2,8:4").split(",")]
+    for u, hr in geoms:
         t = csum.Tuning(kind=csum.KIND_SPAN, unroll=u, group=hr, nontemporal=1)
         for lname, lib in list(libs.items()) + [("product_ntstore", csum.lib)]:
             if lname == "product_ntstore":
