@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Fixed-length geometry probe (F1500 and F9000, rotated HBM-resident
-batches): subgroup size x chunks per lane x block size, interleaved over
-rounds; every geometry's results are checked against the default's."""
+batches): subgroup size x chunks per lane x block size (x nontemporal mode,
+PROBE_NT: bit 0 loads, bit 1 stores), interleaved over rounds; every
+geometry's results are checked against the default's."""
 import json
 import os
 import sys
@@ -24,8 +25,14 @@ def main():
     lib = csum.lib
     geoms = [(32, 4, 256), (16, 6, 256), (32, 3, 256), (16, 8, 256), (16, 6, 512),
              (32, 3, 512), (16, 6, 1024), (64, 2, 256)]
+    nts = [int(x) for x in os.environ.get("PROBE_NT", "1").split(",")]
+    lens = [int(x) for x in os.environ.get("PROBE_LENS", "1500,9000").split(",")]
+    if os.environ.get("PROBE_GEOMS"):
+        geoms = [tuple(int(v) for v in g.split(":")) for g in os.environ["PROBE_GEOMS"].split(",")]
     for L, nb in ((1500, 16), (9000, 3)):
-        if L == 9000:
+        if L not in lens:
+            continue
+        if L == 9000 and not os.environ.get("PROBE_GEOMS"):
             geoms = [(64, 8, 256), (64, 9, 256), (64, 12, 256), (64, 4, 256), (64, 9, 512)]
         bb = N * L
         buf = torch.empty(nb * bb + 256, dtype=torch.uint8, device=dev)
@@ -33,8 +40,8 @@ def main():
         out = torch.empty(nb * N, dtype=torch.uint16, device=dev)
         res, ref = {}, None
         for rnd in range(3):
-            for g, u, blk in geoms:
-                t = csum.Tuning(group=g, unroll=u, nontemporal=1, block=blk)
+            for (g, u, blk), nt in [(gm, nt) for gm in geoms for nt in nts]:
+                t = csum.Tuning(group=g, unroll=u, nontemporal=nt, block=blk)
 
                 def fn(i, sh, t=t):
                     b = i % nb
@@ -49,11 +56,11 @@ def main():
                 o = out.cpu().numpy()
                 if ref is None:
                     ref = o
-                assert np.array_equal(o, ref), (g, u, blk)
-                res.setdefault((g, u, blk), []).append(timer(fn, 64))
-        for (g, u, blk), ts in res.items():
+                assert np.array_equal(o, ref), (g, u, blk, nt)
+                res.setdefault((g, u, blk, nt), []).append(timer(fn, 64))
+        for (g, u, blk, nt), ts in res.items():
             tm = float(np.median(ts))
-            print(json.dumps({"L": L, "geom": f"g{g}u{u}b{blk}", "us": round(tm * 1e6, 2),
+            print(json.dumps({"L": L, "geom": f"g{g}u{u}b{blk}nt{nt}", "us": round(tm * 1e6, 2),
                               "GBps": round(bb / tm / 1e9, 1)}), flush=True)
         del buf
 
