@@ -549,11 +549,13 @@ def zipf_sharded_leg(torch, dist, csum, dev, cdev, stream, rank, world):
     doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
     dlens = torch.from_numpy(ll.view(np.int16).copy()).to(dev)
     out = torch.empty(max(1, len(ll)), dtype=torch.uint16, device=dev)
-    batch = csum.lib.tulips_csum_batch
+    batch = csum.lib.tulips_csum_batch_arena   # a shard is a packed, in-order arena
 
     def fz(i, st):
-        batch(az.data_ptr(), doffs.data_ptr(), dlens.data_ptr(), None, None, None,
-              out.data_ptr(), len(ll), 0, st)
+        rc = batch(az.data_ptr(), bs.nbytes, doffs.data_ptr(), dlens.data_ptr(), None, None,
+                   None, out.data_ptr(), len(ll), 0, st)
+        if rc:
+            raise csum.CsumError(rc, "tulips_csum_batch_arena")
     fz(0, stream.cuda_stream)
     torch.cuda.synchronize()
     dist.barrier()
@@ -576,6 +578,7 @@ def zipf_sharded_leg(torch, dist, csum, dev, cdev, stream, rank, world):
     ok = all_ranks_ok(fnv1a_u16(glob[:NSEG]) == gold, dist, cdev)
     return {"workload": f"Zipf batch of {world} x 65,536 segments ({int(world * zb)} B), "
                         "byte-balanced shards",
+            "entry": "tulips_csum_batch_arena (each shard is a packed in-order arena)",
             "shard_segments": int(bs.seg_count), "shard_bytes": int(bs.nbytes),
             "us_per_launch_max": round(t_max * 1e6, 2),
             "us_per_launch_min": round(t_min * 1e6, 2),
