@@ -16,7 +16,7 @@ HDRS = tulips_amd/csrc/csum_common.h tulips_amd/csrc/csum_launch.h \
        include/tulips_csum.h include/tulips_csum_util.h
 OBJS = $(patsubst tulips_amd/csrc/%.hip,build/%.o,$(SRCS))
 
-.PHONY: all lib oracle clean asm stamps xcd_ab spandiag genstore
+.PHONY: all lib oracle clean asm stamps xcd_ab spandiag genstore s3ab
 
 all: lib oracle
 
@@ -66,6 +66,14 @@ genstore: $(foreach d,1 2 3 4,tools/libcsum_genstore$(d).so)
 
 tools/libcsum_genstore%.so: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DTULIPS_GEN_STORE=$* -shared -o $@ $(SRCS)
+
+# Diagnostic A/B builds of the split-form span words' stride (words per
+# range: 1 = packed, 16 = one 128-byte line each; tools/ab_probe.sh).
+# Never loaded by the product.
+s3ab: tools/ab_s3s1.so tools/ab_s3s16.so
+
+tools/ab_s3s%.so: $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DTULIPS_SPAN3_STRIDE=$* -shared -o $@ $(SRCS)
 
 # Device assembly + resource usage of the kernels (for inspection).
 asm:

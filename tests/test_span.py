@@ -26,9 +26,11 @@ from tulips_amd import csum  # noqa: E402
 DEV = "cuda:0"
 # (chunks per lane, halo: 0 = default 2 rows, 1/2 rows, 3 = none: the
 # crossing segment's wave reads its own tail, 4/5 = boundary-slot form with
-# 2/1 rows)
+# 2/1 rows, 6 = split form: no halo, segments split at range boundaries and
+# their parts met in per-range words)
 GEOMS = ((2, 0), (4, 0), (6, 0), (8, 0), (10, 0), (12, 0), (4, 1), (8, 1), (6, 3), (7, 3),
-         (8, 3), (4, 4), (6, 4), (8, 4), (8, 5), (10, 4), (12, 4))
+         (8, 3), (4, 4), (6, 4), (8, 4), (8, 5), (10, 4), (12, 4), (4, 6), (6, 6), (8, 6),
+         (10, 6))
 
 
 @pytest.fixture(scope="module", autouse=True)

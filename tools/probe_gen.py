@@ -25,6 +25,9 @@ def main():
     lens_all = bench.zipf_lengths(NMAX)
     geoms = {"span8": ("span", 8), "s2_8h2": ("span", 8, 4), "s2_8h1": ("span", 8, 5),
              "s2_6h2": ("span", 6, 4), "s2_10h2": ("span", 10, 4),
+             "s3_4": ("span", 4, 6), "s3_5": ("span", 5, 6), "s3_6": ("span", 6, 6),
+             "s3_7": ("span", 7, 6), "s3_8": ("span", 8, 6),
+             "s3_10": ("span", 10, 6),
              "packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                         block=256, sps=2),
              }

@@ -370,7 +370,7 @@ batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
   a.kind = TULIPS_CSUM_KIND_SPAN;
   a.unroll = (tuning && tuning->unroll) ? tuning->unroll : SPAN_DEFAULT_UNROLL;
   a.group = (tuning && tuning->group) ? tuning->group : 0;
-  if (a.group < 0 || a.group > 5) {
+  if (a.group < 0 || a.group > 6) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   const int32_t nt = (tuning && tuning->nontemporal >= 0) ? tuning->nontemporal : 1;

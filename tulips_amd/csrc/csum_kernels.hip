@@ -27,6 +27,10 @@
 #include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
+#include "stream_state.h"
+
+#include <memory>
+#include <mutex>
 
 namespace tulips_amd {
 
@@ -1168,9 +1172,18 @@ struct SpanArgs
   uint32_t n;
   uint32_t mode;
   uint32_t nt_store;
+  uint64_t* slots; // SPAN split form: one zeroed word per range (stream_state.h)
 };
 
 typedef const __attribute__((address_space(1))) uint64_t* gu64_ptr;
+
+// Ranges of W bytes covering [A, A + K W), A = base rounded down to 16 B:
+// position base + arena (where an empty last segment may start) included.
+inline uint64_t
+span_ranges(const uint8_t* base, uint64_t arena, uint64_t W)
+{
+  return ((arena + (reinterpret_cast<uintptr_t>(base) & 15u)) / W) + 1;
+}
 
 // Search interval update after one round of 256 samples L + q*st (q < 256):
 // c of them (a prefix, offsets being sorted) lie below the target.
@@ -1875,6 +1888,250 @@ csum_span2_kernel(SpanArgs p)
 #endif
 }
 
+// SPAN, split form (`group` 6): the same byte cut with NO halo. A segment
+// that crosses range boundaries is split there: every range it touches sums
+// its own part from LDS and adds it, with an arrival count, to the word of
+// the segment's first range (one returning agent-scope atomicAdd, executed at
+// the memory side, so no cross-XCD fence is needed). The range whose add
+// completes the count finishes the segment and zeroes the word, so the words
+// are all zero again when the launch ends. Each range reads exactly its own
+// bytes, and no workgroup ever waits for another.
+// Parts are folded with end-around carry (zero iff every byte is zero), so
+// their sum keeps the closed form's 0 / 0xffff distinction (csum_common.h).
+#ifndef TULIPS_SPAN3_STRIDE
+#define TULIPS_SPAN3_STRIDE 1
+#endif
+constexpr uint64_t SPAN3_STRIDE = TULIPS_SPAN3_STRIDE; // words per range
+
+template<int U, bool NT>
+__global__ __launch_bounds__(256) void
+csum_span3_kernel(SpanArgs p)
+{
+  constexpr uint32_t NC = 256u * U;      // chunks per range
+  constexpr uint64_t W = 16ull * NC;     // bytes per range
+  constexpr uint32_t NWIN = 1024;        // speculative window entries
+  __shared__ u32x4 s_raw[NC];            // the range's chunks
+  __shared__ uint32_t s_sc[NC];          // row-wise wave scans of chunk values
+  __shared__ uint32_t s_tot[4 * U];      // per (row, wave) scan totals
+  __shared__ uint32_t s_woff[4][4 * U];  // each wave's copy of their exclusive prefix
+  __shared__ uint32_t s_cnt[8];          // per wave: window counts
+  __shared__ uint32_t s_meta[2];         // search results
+
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const uint32_t k = xcd_block(blockIdx.x, gridDim.x);
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p.base);
+  const uint64_t d = b & 15u;
+  const uintptr_t A = b & ~uintptr_t(15);
+  const uintptr_t x0 = A + uint64_t(k) * W, x1 = x0 + W;
+  const uintptr_t aend = b + p.arena;
+  const uintptr_t zero = reinterpret_cast<uintptr_t>(k_zero_chunk);
+  const uintptr_t last = p.arena ? ((aend - 1) & ~uintptr_t(15)) : zero;
+  const uint32_t n = p.n;
+  const gu64_ptr offs = reinterpret_cast<gu64_ptr>(reinterpret_cast<uintptr_t>(p.offs));
+  const gu16_ptr lens = reinterpret_cast<gu16_ptr>(reinterpret_cast<uintptr_t>(p.lens));
+  // lo = first s with off_s >= tg0, hi = first s with off_s >= tg1
+  const uint64_t tg0 = k ? uint64_t(k) * W - d : 0, tg1 = uint64_t(k + 1) * W - d;
+
+  // 1. one round trip: the offsets window, then the range's chunks
+  const uint64_t mid = (tg0 + tg1) / 2;
+  const uint64_t guess = uint64_t(double(n) * double(mid) / double(p.arena ? p.arena : 1));
+  const uint32_t gmax = n > NWIN ? n - NWIN : 0u;
+  const uint32_t G = uint32_t(min(guess > NWIN / 2 ? guess - NWIN / 2 : 0ull, uint64_t(gmax)));
+  uint64_t wo[4];
+  uint32_t wl[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t i = min(G + t + 256u * r, n - 1);
+    wo[r] = offs[i];
+    wl[r] = lens[i];
+  }
+  u32x4 v[U];
+#pragma unroll
+  for (uint32_t j = 0; j < U; ++j) {
+    const uintptr_t a = x0 + 16u * (j * 256u + t);
+    v[j] = load_chunk<NT>(reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool in = G + t + 256u * r < n;
+      c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg0));
+      c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg1));
+    }
+    if (lane == 0) {
+      s_cnt[w] = c0;
+      s_cnt[4 + w] = c1;
+    }
+  }
+  // 2. chunks to LDS with the row-wise wave scans of their values
+#pragma unroll
+  for (uint32_t j = 0; j < U; ++j) {
+    s_raw[j * 256u + t] = v[j];
+    const uint32_t sc = wave_incl_scan(chunk_value(v[j]));
+    s_sc[j * 256u + t] = sc;
+    if (lane == 63) {
+      s_tot[4 * j + w] = sc;
+    }
+  }
+  lds_barrier();
+  // 3. this wave's copy of the (row, wave) offsets
+  {
+    const uint32_t x = lane < 4 * U ? s_tot[lane] : 0u;
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane < 4 * U) {
+      s_woff[w][lane] = inc - x;
+    }
+  }
+  auto P = [&](uint32_t c) { return s_woff[w][c >> 6] + s_sc[c]; };
+  const uint32_t c0 = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  const uint32_t c1 = s_cnt[4] + s_cnt[5] + s_cnt[6] + s_cnt[7];
+  const uint32_t nw = min(NWIN, n - G);
+  const bool tail_ok = G + NWIN >= n;
+  const bool ok = (c0 > 0 || G == 0) && (c0 < nw || tail_ok) && (c1 > 0 || G == 0) &&
+                  (c1 < nw || tail_ok);
+
+  // 4. one segment: its part in [x0, x1) from LDS; a split segment's part
+  //    goes to its first range's word and the last arrival finishes it
+  const uint32_t want = (p.mode & FLAG_COMPLEMENT) ? 0u : 0xffffu;
+  const bool side_in = (p.mode & MODE_MASK) == MODE_TCP || p.seeds != nullptr;
+  auto emit = [&](uint32_t s, bool act, uint64_t so, uint32_t sl) {
+    SideIn side{0, 0, 0};
+    if (side_in) {
+      side = load_side(act ? s : 0u, p.seeds, p.src, p.dst, p.mode);
+    }
+    const uintptr_t sa = b + so;
+    const uintptr_t se = min(b + so + sl, aend);
+    const uintptr_t u0 = max(sa, x0), u1 = min(se, x1);
+    uint32_t sum = 0;
+    if (act && u1 > u0) {
+      const uint32_t ca = uint32_t((u0 - x0) >> 4);
+      const uint32_t ce = uint32_t((u1 - 1 - x0) >> 4);
+      const int ha = int(u0 & 15u), tb = int(((u1 - 1) & 15u) + 1u);
+      sum = ca == ce ? masked_value(s_raw[ca], ha, tb)
+                     : masked_value(s_raw[ca], ha, 16) + (P(ce - 1) - P(ca)) +
+                         masked_value(s_raw[ce], 0, tb);
+    }
+    bool done = act;
+    if (act && (sa < x0 || se > x1)) {
+      const uint64_t ra = (sa - A) / W, rz = (se - 1 - A) / W;
+      const uint32_t part = fold32(sum);
+      const unsigned long long old = atomicAdd(
+        reinterpret_cast<unsigned long long*>(p.slots + ra * SPAN3_STRIDE), (1ull << 32) | part);
+      done = (old >> 32) == rz - ra;
+      if (done) {
+        sum = uint32_t(old) + part;
+        __hip_atomic_store(p.slots + ra * SPAN3_STRIDE, uint64_t(0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const uint32_t r =
+      finish(sum, (sa & 1u) != 0, p.mode, side.seed, side.src, side.dst, sl);
+    if (done && p.out) {
+      if (p.nt_store) {
+        __builtin_nontemporal_store(uint16_t(r), p.out + s);
+      } else {
+        p.out[s] = uint16_t(r);
+      }
+    }
+    if (p.bad) {
+      const uint32_t nb =
+        __builtin_popcountll(__builtin_amdgcn_ballot_w64(done && r != want));
+      if (lane == 0 && nb) {
+        atomicAdd(p.bad + CNT_LINE * (blockIdx.x % CNT_SHARDS), nb);
+      }
+    }
+  };
+
+  uint32_t lo, hi;
+  if (ok) {
+    lo = G + c0;
+    hi = G + c1;
+  } else {
+    // rare: wave 0 searches [lo, hi) (offsets sorted)
+    if (w == 0) {
+      uint32_t L0 = 0, R0 = n, L1 = 0, R1 = n;
+      while (R0 > L0 || R1 > L1) {
+        const uint32_t st0 = (R0 - L0 + 255u) >> 8, st1 = (R1 - L1 + 255u) >> 8;
+        uint64_t o0[4], o1[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t q = lane + 64u * r;
+          o0[r] = offs[min(uint64_t(L0) + uint64_t(q) * st0, uint64_t(n - 1))];
+          o1[r] = offs[min(uint64_t(L1) + uint64_t(q) * st1, uint64_t(n - 1))];
+        }
+        uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t q = lane + 64u * r;
+          const bool in0 = uint64_t(L0) + uint64_t(q) * st0 < R0;
+          const bool in1 = uint64_t(L1) + uint64_t(q) * st1 < R1;
+          d0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in0 && o0[r] < tg0));
+          d1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in1 && o1[r] < tg1));
+        }
+        if (R0 > L0) {
+          span_narrow(L0, R0, st0, __builtin_amdgcn_readfirstlane(d0));
+        }
+        if (R1 > L1) {
+          span_narrow(L1, R1, st1, __builtin_amdgcn_readfirstlane(d1));
+        }
+      }
+      if (lane == 0) {
+        s_meta[0] = L0;
+        s_meta[1] = L1;
+      }
+    }
+    lds_barrier();
+    lo = s_meta[0];
+    hi = s_meta[1];
+  }
+  // the segments starting in the range, [lo, hi), and the one before them
+  // if it runs into the range (its start lies in an earlier range)
+  const uint32_t first = lo > 0 ? lo - 1 : 0;
+  if (ok) {
+    // each thread finishes the segments whose window entries it loaded
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t i = G + t + 256u * r;
+      bool act = i >= lo && i < hi;
+      if (lo > 0 && i == lo - 1) {
+        act = min(b + wo[r] + wl[r], aend) > x0;
+      }
+      if (__builtin_amdgcn_ballot_w64(act) != 0) {
+        emit(i, act, act ? wo[r] : 0, act ? wl[r] : 0u);
+      }
+    }
+  } else {
+    for (uint32_t s0 = first; s0 < hi; s0 += 256u) {
+      const uint32_t s = s0 + t;
+      bool act = s < hi;
+      const uint64_t so = act ? p.offs[s] : 0;
+      const uint32_t sl = act ? p.lens[s] : 0u;
+      if (s < lo) {
+        act = act && min(b + so + sl, aend) > x0;
+      }
+      emit(s, act, act ? so : 0, act ? sl : 0u);
+    }
+  }
+}
+
+template<int U, bool NT>
+hipError_t
+launch_span3_u(const SpanArgs& sp, hipStream_t stream)
+{
+  constexpr uint64_t W = 4096ull * U;
+  const uint64_t ranges = span_ranges(sp.base, sp.arena, W);
+  if (ranges > 0x7fffffffull) {
+    return hipErrorInvalidValue;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_span3_kernel<U, NT>), dim3(uint32_t(ranges)), dim3(256), 0, stream,
+                     sp);
+  return hipGetLastError();
+}
+
 template<int U, int HR, bool NT>
 hipError_t
 launch_span2_u(const SpanArgs& sp, hipStream_t stream)
@@ -2109,9 +2366,37 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
             const uint16_t* lens, const LaunchArgs& a, hipStream_t stream)
 {
   const SpanArgs sp{base, arena, offs, lens, a.seeds, a.src, a.dst, a.out, a.bad,
-                    a.n, a.mode, a.nt_store ? 1u : 0u};
+                    a.n, a.mode, a.nt_store ? 1u : 0u, nullptr};
   if (a.n == 0) {
     return hipSuccess;
+  }
+  if (a.group == 6) {
+    // split form: the stream's zeroed per-range words, held for the launch
+    std::shared_ptr<StreamState> ss;
+    hipError_t e = stream_state(stream, &ss);
+    if (e != hipSuccess) {
+      return e;
+    }
+    std::lock_guard<std::mutex> g(ss->call);
+    SpanArgs sp3 = sp;
+    e = span_slots(*ss, stream_capturing(stream),
+                   span_ranges(base, arena, 4096ull * a.unroll) * SPAN3_STRIDE, &sp3.slots);
+    if (e != hipSuccess) {
+      return e == hipErrorStreamCaptureUnsupported ? hipErrorInvalidValue : e;
+    }
+#define TCS_S3CASE(U_)                                                         \
+  if (a.unroll == U_) {                                                        \
+    return a.nontemporal ? launch_span3_u<U_, true>(sp3, stream)               \
+                         : launch_span3_u<U_, false>(sp3, stream);             \
+  }
+    TCS_S3CASE(4)
+    TCS_S3CASE(5)
+    TCS_S3CASE(6)
+    TCS_S3CASE(7)
+    TCS_S3CASE(8)
+    TCS_S3CASE(10)
+#undef TCS_S3CASE
+    return hipErrorInvalidValue;
   }
   // group = halo rows of 4 KiB read past the range (1 or 2), or 3 = none:
   // the crossing segment's wave reads exactly its tail (0 = default);

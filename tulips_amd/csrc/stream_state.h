@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -46,6 +47,17 @@ struct StreamState
   uint64_t seg_nruns = 0;
   void* seg_desc = nullptr; // 16 B per input frame
   uint64_t seg_ndesc = 0;
+
+  // SPAN split-form words (csum_kernels.hip csum_span3_kernel): one zeroed
+  // 64-bit word per arena range, zero again after every launch. The calls
+  // one capture records on this stream run in order in the graph, so they
+  // share one array (a spare, or made in relaxed capture mode), owned by the
+  // graph from then on
+  uint64_t* span_slots = nullptr;
+  uint64_t span_nslots = 0;
+  std::vector<uint64_t*> span_spare;
+  std::vector<uint64_t*> span_owned;
+  std::map<unsigned long long, std::pair<uint64_t*, uint64_t>> span_capture;
 };
 
 constexpr int SPARE_SHARDS = 16;
@@ -62,6 +74,11 @@ bool stream_capturing(hipStream_t stream);
 // the stream's direct shards, or, inside a capture, a spare set the graph
 // keeps. hipErrorStreamCaptureUnsupported when a capture finds no spare.
 hipError_t call_shards(StreamState& s, bool capturing, uint32_t** out);
+
+// The split-form span words for one call on `s` (caller holds s.call): at
+// least `need` zeroed words; inside a capture a spare array the graph keeps.
+// hipErrorStreamCaptureUnsupported when a capture would have to allocate.
+hipError_t span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out);
 
 // After a failed launch in a direct counting call: the shards may hold
 // partial sums, so the stream gets fresh zeroed ones on its next call.

@@ -136,6 +136,107 @@ call_shards(StreamState& s, bool capturing, uint32_t** out)
   return hipSuccess;
 }
 
+// Zeroed words on `device` (not stream-ordered: used only before any launch
+// can read them). Inside a capture the thread's capture mode is relaxed for
+// the allocation, so hipMalloc is allowed, and the zeroing runs on a private
+// stream that is not capturing.
+hipError_t
+zeroed_words(int device, uint64_t words, bool capturing, uint64_t** out)
+{
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  if (capturing) {
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+  }
+  void* p = nullptr;
+  hipError_t e = device_malloc(device, &p, sizeof(uint64_t) * words);
+  hipStream_t z = nullptr;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (e == hipSuccess && (e = hipSetDevice(device)) == hipSuccess) {
+    if ((e = hipStreamCreateWithFlags(&z, hipStreamNonBlocking)) == hipSuccess) {
+      e = hipMemsetAsync(p, 0, sizeof(uint64_t) * words, z);
+      const hipError_t e2 = hipStreamSynchronize(z);
+      e = e != hipSuccess ? e : e2;
+      (void)hipStreamDestroy(z);
+    }
+    (void)hipSetDevice(prev);
+  }
+  if (capturing) {
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+  }
+  if (e != hipSuccess) {
+    if (p) {
+      free_on(device, std::vector<void*>{ p });
+    }
+    return e;
+  }
+  *out = static_cast<uint64_t*>(p);
+  return hipSuccess;
+}
+
+hipError_t
+span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out)
+{
+  if (!capturing) {
+    if (need > s.span_nslots) {
+      // direct words plus spares for captures, all zeroed before use
+      const uint64_t want = need < 4096 ? 4096 : need;
+      std::vector<uint64_t*> made;
+      hipError_t e = hipSuccess;
+      for (int k = 0; k <= SPARE_SHARDS && e == hipSuccess; ++k) {
+        uint64_t* p = nullptr;
+        if ((e = zeroed_words(s.device, want, false, &p)) == hipSuccess) {
+          made.push_back(p);
+        }
+      }
+      if (e == hipSuccess) {
+        e = hipStreamSynchronize(s.stream); // the old arrays are idle
+      }
+      if (e != hipSuccess) {
+        free_on(s.device, std::vector<void*>(made.begin(), made.end()));
+        return e;
+      }
+      std::vector<void*> old(s.span_spare.begin(), s.span_spare.end());
+      old.push_back(s.span_slots);
+      free_on(s.device, old);
+      s.span_slots = made[0];
+      s.span_nslots = want;
+      s.span_spare.assign(made.begin() + 1, made.end());
+    }
+    *out = s.span_slots;
+    return hipSuccess;
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  if (hipStreamGetCaptureInfo(s.stream, &cs, &id) != hipSuccess) {
+    (void)hipGetLastError();
+    return hipErrorStreamCaptureUnsupported;
+  }
+  auto it = s.span_capture.find(id);
+  if (it != s.span_capture.end() && it->second.second >= need) {
+    *out = it->second.first;
+    return hipSuccess;
+  }
+  uint64_t* p = nullptr;
+  uint64_t size = 0;
+  if (!s.span_spare.empty() && s.span_nslots >= need) {
+    p = s.span_spare.back();
+    s.span_spare.pop_back();
+    size = s.span_nslots;
+  } else {
+    size = need < 4096 ? 4096 : need;
+    const hipError_t e = zeroed_words(s.device, size, true, &p);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return hipErrorStreamCaptureUnsupported;
+    }
+  }
+  s.span_owned.push_back(p);
+  s.span_capture[id] = std::make_pair(p, size);
+  *out = p;
+  return hipSuccess;
+}
+
 void
 drop_shards(StreamState& s, uint32_t* shards)
 {
@@ -181,6 +282,9 @@ tulips_csum_release_stream(void* stream)
     ps.push_back(s->seg_blocks);
     ps.push_back(s->seg_runs);
     ps.push_back(s->seg_desc);
+    ps.push_back(s->span_slots);
+    for (auto* p : s->span_spare) ps.push_back(p);
+    for (auto* p : s->span_owned) ps.push_back(p);
     free_on(s->device, ps);
     s->shards = nullptr;
     s->spare.clear();
@@ -189,6 +293,11 @@ tulips_csum_release_stream(void* stream)
     s->seg_blocks = s->seg_runs = nullptr;
     s->seg_desc = nullptr;
     s->seg_nruns = s->seg_ndesc = 0;
+    s->span_slots = nullptr;
+    s->span_nslots = 0;
+    s->span_spare.clear();
+    s->span_owned.clear();
+    s->span_capture.clear();
   }
   return TULIPS_STATUS_OK;
 }
