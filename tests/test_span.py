@@ -24,13 +24,13 @@ import tulips_amd  # noqa: E402
 from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
-# (chunks per lane, halo: 0 = default 2 rows, 1/2 rows, 3 = none: the
-# crossing segment's wave reads its own tail, 4/5 = boundary-slot form with
-# 2/1 rows, 6 = split form: no halo, segments split at range boundaries and
-# their parts met in per-range words)
-GEOMS = ((2, 0), (4, 0), (6, 0), (8, 0), (10, 0), (12, 0), (4, 1), (8, 1), (6, 3), (7, 3),
-         (8, 3), (4, 4), (6, 4), (8, 4), (8, 5), (10, 4), (12, 4), (4, 6), (6, 6), (8, 6),
-         (10, 6))
+# (chunks per lane, form: 0 = default = 6 = split form: no halo, segments
+# split at range boundaries and their parts met in per-range words; 1/2 rows
+# of halo, 3 = none: the crossing segment's wave reads its own tail, 4/5 =
+# boundary-slot form with 2/1 rows)
+GEOMS = ((2, 0), (4, 0), (6, 0), (8, 0), (10, 0), (12, 0), (4, 1), (8, 1), (2, 2), (6, 2),
+         (8, 2), (12, 2), (6, 3), (7, 3), (8, 3), (4, 4), (6, 4), (8, 4), (8, 5), (10, 4),
+         (12, 4), (5, 6), (7, 6))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -235,3 +235,24 @@ def test_rejects_bad_arguments():
     # n == 0 is a no-op
     assert csum.lib.tulips_csum_batch_arena(None, 0, None, None, None, None, None, None,
                                             0, 0, None) == 0
+
+
+@pytest.mark.parametrize("u", [g for g in GEOMS if g[1] in (0, 6)])
+def test_split_words_survive_contract_breaking_batch(oracle, u):
+    """The split form's per-range words are left non-zero only by a batch that
+    breaks the arena contract (overlapping segments); such residue carries an
+    older epoch and must not leak into the next, valid, batch on the stream."""
+    rng = np.random.default_rng(404 + u[0])
+    n = 20000
+    lens = rng.integers(1000, 9000, n).astype(np.uint16)
+    offs, end = in_order(rng, lens)
+    arena = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    da, dl = d(arena), d(lens)
+    bad = offs.copy()
+    bad[1::3] -= np.minimum(bad[1::3], np.uint64(6000))   # overlaps its predecessors
+    bad = np.maximum.accumulate(bad)                      # sorted, still overlapping
+    tulips_amd.batch_arena(da, d(bad), dl, arena_bytes=end, tuning=tuning(u))
+    exp = oracle.batch(arena, offs, lens, mode=MODE_RAW, nthreads=8)
+    for _ in range(3):
+        got = tulips_amd.batch_arena(da, d(offs), dl, arena_bytes=end, tuning=tuning(u))
+        np.testing.assert_array_equal(u16(got), exp)

@@ -23,7 +23,7 @@ def main():
     NB = int(os.environ.get("PROBE_NB", "8"))  # 8 copies: past the 256 MB MALL
     NMAX = 98304
     lens_all = bench.zipf_lengths(NMAX)
-    geoms = {"span8": ("span", 8), "s2_8h2": ("span", 8, 4), "s2_8h1": ("span", 8, 5),
+    geoms = {"span8": ("span", 8, 2), "split6": ("span", 6), "s2_8h2": ("span", 8, 4), "s2_8h1": ("span", 8, 5),
              "s2_6h2": ("span", 6, 4), "s2_10h2": ("span", 10, 4),
              "s3_4": ("span", 4, 6), "s3_5": ("span", 5, 6), "s3_6": ("span", 6, 6),
              "s3_7": ("span", 7, 6), "s3_8": ("span", 8, 6),

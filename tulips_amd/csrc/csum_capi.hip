@@ -138,10 +138,11 @@ tulips_csum_tcp_host(uint32_t src, uint32_t dst, uint16_t len,
 // ---------------------------------------------------------------------------
 namespace {
 
-// KIND_SPAN chunks per lane: 32 KiB per workgroup range, 8 KiB halo
-// (tools/probe_gen.py, profiles/probe_span_r02.json: ZIPF 11.7 us serial,
-// 8.7 us per launch with 4 launches in flight)
-constexpr int SPAN_DEFAULT_UNROLL = 8;
+// KIND_SPAN chunks per lane: 24 KiB per workgroup range, split form
+// (tools/probe_gen.py, profiles/probe_split_r02.txt: ZIPF 11.4-11.5 us serial
+// against 12.0-12.1 for the 8 KiB-halo form, 8.5-8.7 us per launch with 4
+// launches in flight, equal)
+constexpr int SPAN_DEFAULT_UNROLL = 6;
 
 thread_local char last_error[160] = "";
 
@@ -340,8 +341,8 @@ batch_var(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
 }
 
 // In-order arena batches (KIND_SPAN, csum_kernels.hip): the tuning's kind
-// must be DEFAULT or SPAN; unroll = chunks per lane (2, 4, 6, 8; 10 and 12
-// with 2 halo rows), group = halo rows (1, 2; 0 = 2).
+// must be DEFAULT or SPAN; unroll = chunks per lane, group = 0/6 split form,
+// 1/2 halo rows, 3 no halo, 4/5 boundary-slot form (include/tulips_csum_util.h).
 int
 batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
             const uint16_t* lengths, const uint16_t* seeds, const uint32_t* src,
@@ -370,7 +371,7 @@ batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
   a.kind = TULIPS_CSUM_KIND_SPAN;
   a.unroll = (tuning && tuning->unroll) ? tuning->unroll : SPAN_DEFAULT_UNROLL;
   a.group = (tuning && tuning->group) ? tuning->group : 0;
-  if (a.group < 0 || a.group > 6) {
+  if (!span_geometry_ok(a.unroll, a.group)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   const int32_t nt = (tuning && tuning->nontemporal >= 0) ? tuning->nontemporal : 1;
@@ -396,7 +397,7 @@ counted(void* stream, uint32_t* count, const F& launch)
     return status_of(e);
   }
   const bool capturing = stream_capturing(st);
-  std::lock_guard<std::mutex> g(ss->call);
+  std::lock_guard<std::recursive_mutex> g(ss->call);
   uint32_t* shards = nullptr;
   if ((e = call_shards(*ss, capturing, &shards)) != hipSuccess) {
     return e == hipErrorStreamCaptureUnsupported ? TULIPS_STATUS_INVALID_ARGUMENT

@@ -1172,7 +1172,8 @@ struct SpanArgs
   uint32_t n;
   uint32_t mode;
   uint32_t nt_store;
-  uint64_t* slots; // SPAN split form: one zeroed word per range (stream_state.h)
+  uint64_t* slots; // SPAN split form: one word per range (stream_state.h)
+  uint32_t epoch;  // SPAN split form: this call's tag, 1 .. 2^24 - 1
 };
 
 typedef const __attribute__((address_space(1))) uint64_t* gu64_ptr;
@@ -2016,15 +2017,37 @@ csum_span3_kernel(SpanArgs p)
     }
     bool done = act;
     if (act && (sa < x0 || se > x1)) {
-      const uint64_t ra = (sa - A) / W, rz = (se - 1 - A) / W;
+      // word = epoch << 40 | arrivals << 32 | sum of the parts so far; a
+      // word tagged with another epoch is residue of an earlier call (only
+      // a batch breaking the arena contract leaves one) and is taken over
+      const uint64_t ra = (sa - A) / W;
+      const uint32_t need = uint32_t((se - 1 - A) / W - ra);  // arrivals before the last
       const uint32_t part = fold32(sum);
-      const unsigned long long old = atomicAdd(
-        reinterpret_cast<unsigned long long*>(p.slots + ra * SPAN3_STRIDE), (1ull << 32) | part);
-      done = (old >> 32) == rz - ra;
-      if (done) {
-        sum = uint32_t(old) + part;
-        __hip_atomic_store(p.slots + ra * SPAN3_STRIDE, uint64_t(0), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t ep = uint64_t(p.epoch) << 40;
+      const uint64_t mine = ep | (1ull << 32) | part;
+      unsigned long long* wp =
+        reinterpret_cast<unsigned long long*>(p.slots + ra * SPAN3_STRIDE);
+      unsigned long long seen = atomicCAS(wp, 0ull, mine);
+      done = false;
+      // every failed exchange means another arrival changed the word: the
+      // loop ends after at most as many rounds as the segment has parts
+      for (int round = 0; seen != 0 && round < 64; ++round) {
+        unsigned long long next;
+        if ((seen >> 40) != p.epoch) {
+          next = mine;
+        } else if (uint32_t((seen >> 32) & 0xffu) == need) {
+          done = true;
+          sum = uint32_t(seen) + part;
+          __hip_atomic_store(wp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        } else {
+          next = seen + (1ull << 32) + part;
+        }
+        const unsigned long long prev = atomicCAS(wp, seen, next);
+        if (prev == seen) {
+          break;
+        }
+        seen = prev;
       }
     }
     const uint32_t r =
@@ -2361,26 +2384,50 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
   return dispatch(segs, a, stream);
 }
 
+bool
+span_geometry_ok(int u, int group)
+{
+  switch (group) {
+    case 0:
+    case 6:
+      return u == 2 || (u >= 4 && u <= 8) || u == 10 || u == 12;
+    case 1:
+      return u == 2 || u == 4 || u == 6 || u == 8;
+    case 2:
+      return u == 2 || u == 4 || u == 6 || u == 8 || u == 10 || u == 12;
+    case 3:
+      return u >= 6 && u <= 8;
+    case 4:
+      return u == 4 || u == 6 || u == 8 || u == 10 || u == 12;
+    case 5:
+      return u == 8;
+    default:
+      return false;
+  }
+}
+
 hipError_t
 launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
             const uint16_t* lens, const LaunchArgs& a, hipStream_t stream)
 {
   const SpanArgs sp{base, arena, offs, lens, a.seeds, a.src, a.dst, a.out, a.bad,
-                    a.n, a.mode, a.nt_store ? 1u : 0u, nullptr};
+                    a.n, a.mode, a.nt_store ? 1u : 0u, nullptr, 0};
   if (a.n == 0) {
     return hipSuccess;
   }
-  if (a.group == 6) {
-    // split form: the stream's zeroed per-range words, held for the launch
+  if (a.group == 0 || a.group == 6) {
+    // split form (the default): the stream's per-range words, held for the
+    // launch
     std::shared_ptr<StreamState> ss;
     hipError_t e = stream_state(stream, &ss);
     if (e != hipSuccess) {
       return e;
     }
-    std::lock_guard<std::mutex> g(ss->call);
+    std::lock_guard<std::recursive_mutex> g(ss->call);
     SpanArgs sp3 = sp;
     e = span_slots(*ss, stream_capturing(stream),
-                   span_ranges(base, arena, 4096ull * a.unroll) * SPAN3_STRIDE, &sp3.slots);
+                   span_ranges(base, arena, 4096ull * a.unroll) * SPAN3_STRIDE, &sp3.slots,
+                   &sp3.epoch);
     if (e != hipSuccess) {
       return e == hipErrorStreamCaptureUnsupported ? hipErrorInvalidValue : e;
     }
@@ -2389,12 +2436,14 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
     return a.nontemporal ? launch_span3_u<U_, true>(sp3, stream)               \
                          : launch_span3_u<U_, false>(sp3, stream);             \
   }
+    TCS_S3CASE(2)
     TCS_S3CASE(4)
     TCS_S3CASE(5)
     TCS_S3CASE(6)
     TCS_S3CASE(7)
     TCS_S3CASE(8)
     TCS_S3CASE(10)
+    TCS_S3CASE(12)
 #undef TCS_S3CASE
     return hipErrorInvalidValue;
   }
@@ -2416,7 +2465,7 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
 #undef TCS_S2CASE
     return hipErrorInvalidValue;
   }
-  const int hr = a.group == 0 ? 2 : (a.group == 3 ? 0 : a.group);
+  const int hr = a.group == 3 ? 0 : a.group;
 #define TCS_SCASE(U_, H_)                                                      \
   if (a.unroll == U_ && hr == H_) {                                            \
     return a.nontemporal ? launch_span_u<U_, H_, true>(sp, stream)             \

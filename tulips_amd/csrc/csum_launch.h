@@ -43,8 +43,12 @@ hipError_t launch_fixed(const uint8_t* base, uint64_t stride, uint32_t len,
 hipError_t launch_var(const uint8_t* base, const uint64_t* offs,
                       const uint16_t* lens, const LaunchArgs& a,
                       hipStream_t stream);
+// Whether launch_span has a kernel for (unroll, group) (checked on the CPU
+// before any HIP call).
+bool span_geometry_ok(int unroll, int group);
 // In-order arena (KIND_SPAN): segments lie in order in [base, base + arena);
-// a.unroll = chunks per lane (2, 4, 8: 8, 16, 32 KiB per workgroup).
+// a.unroll = chunks per lane (4 KiB of arena per workgroup each), a.group the
+// form (include/tulips_csum_util.h).
 hipError_t launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
                        const uint16_t* lens, const LaunchArgs& a,
                        hipStream_t stream);

@@ -366,7 +366,7 @@ launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
     return e;
   }
   const bool capturing = stream_capturing(stream);
-  std::lock_guard<std::mutex> g(ss->call);
+  std::lock_guard<std::recursive_mutex> g(ss->call);
   uint32_t* shards = nullptr;
   if ((e = call_shards(*ss, capturing, &shards)) != hipSuccess) {
     return e;

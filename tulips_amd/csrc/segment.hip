@@ -712,7 +712,7 @@ tulips_csum_segment_frames(const uint8_t* in_base, const uint64_t* in_offsets,
   }
   // the prologue and the segment kernel share the stream's workspace: queue
   // them as one sequence (stream_state.h)
-  std::lock_guard<std::mutex> g(ss->call);
+  std::lock_guard<std::recursive_mutex> g(ss->call);
   uint32_t* ws = nullptr;
   uint32_t* runs = nullptr;
   u32x4* desc = nullptr;

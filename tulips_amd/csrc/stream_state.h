@@ -33,7 +33,9 @@ struct StreamState
 {
   int device = 0;
   hipStream_t stream = nullptr;
-  std::mutex call; // held across one call's launch sequence
+  // held across one call's launch sequence (recursive: a counting call
+  // holds it around launches that take it themselves, e.g. the split span)
+  std::recursive_mutex call;
 
   // counter shards (csum_launch.h CNT_SHARDS x CNT_LINE words each)
   uint32_t* shards = nullptr;          // direct (uncaptured) calls
@@ -48,16 +50,25 @@ struct StreamState
   void* seg_desc = nullptr; // 16 B per input frame
   uint64_t seg_ndesc = 0;
 
-  // SPAN split-form words (csum_kernels.hip csum_span3_kernel): one zeroed
-  // 64-bit word per arena range, zero again after every launch. The calls
-  // one capture records on this stream run in order in the graph, so they
-  // share one array (a spare, or made in relaxed capture mode), owned by the
-  // graph from then on
+  // SPAN split-form words (csum_kernels.hip csum_span3_kernel): one 64-bit
+  // word per arena range, zero again after every launch of a batch that
+  // keeps the arena contract, and tagged with the call's epoch (24 bits) so
+  // that residue of one that does not is never added to. The calls one
+  // capture records on this stream run in order in the graph, so they share
+  // one array (a spare, or made in relaxed capture mode) and one epoch; the
+  // array is owned by the graph from then on
+  uint32_t span_epoch = 0;
   uint64_t* span_slots = nullptr;
   uint64_t span_nslots = 0;
   std::vector<uint64_t*> span_spare;
   std::vector<uint64_t*> span_owned;
-  std::map<unsigned long long, std::pair<uint64_t*, uint64_t>> span_capture;
+  struct Capture
+  {
+    uint64_t* words;
+    uint64_t size;
+    uint32_t epoch;
+  };
+  std::map<unsigned long long, Capture> span_capture;
 };
 
 constexpr int SPARE_SHARDS = 16;
@@ -76,9 +87,11 @@ bool stream_capturing(hipStream_t stream);
 hipError_t call_shards(StreamState& s, bool capturing, uint32_t** out);
 
 // The split-form span words for one call on `s` (caller holds s.call): at
-// least `need` zeroed words; inside a capture a spare array the graph keeps.
-// hipErrorStreamCaptureUnsupported when a capture would have to allocate.
-hipError_t span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out);
+// least `need` words and the call's epoch; inside a capture an array the
+// graph keeps. hipErrorStreamCaptureUnsupported when a capture's array
+// cannot be had.
+hipError_t span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out,
+                      uint32_t* epoch);
 
 // After a failed launch in a direct counting call: the shards may hold
 // partial sums, so the stream gets fresh zeroed ones on its next call.

@@ -174,8 +174,18 @@ zeroed_words(int device, uint64_t words, bool capturing, uint64_t** out)
   return hipSuccess;
 }
 
+uint32_t
+next_epoch(StreamState& s)
+{
+  s.span_epoch = (s.span_epoch + 1) & 0xffffffu;
+  if (s.span_epoch == 0) {
+    s.span_epoch = 1;
+  }
+  return s.span_epoch;
+}
+
 hipError_t
-span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out)
+span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint32_t* epoch)
 {
   if (!capturing) {
     if (need > s.span_nslots) {
@@ -204,6 +214,7 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out)
       s.span_spare.assign(made.begin() + 1, made.end());
     }
     *out = s.span_slots;
+    *epoch = next_epoch(s);
     return hipSuccess;
   }
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -213,8 +224,9 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out)
     return hipErrorStreamCaptureUnsupported;
   }
   auto it = s.span_capture.find(id);
-  if (it != s.span_capture.end() && it->second.second >= need) {
-    *out = it->second.first;
+  if (it != s.span_capture.end() && it->second.size >= need) {
+    *out = it->second.words;
+    *epoch = it->second.epoch;
     return hipSuccess;
   }
   uint64_t* p = nullptr;
@@ -232,8 +244,10 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out)
     }
   }
   s.span_owned.push_back(p);
-  s.span_capture[id] = std::make_pair(p, size);
+  const uint32_t ep = next_epoch(s);
+  s.span_capture[id] = StreamState::Capture{ p, size, ep };
   *out = p;
+  *epoch = ep;
   return hipSuccess;
 }
 
@@ -266,7 +280,7 @@ tulips_csum_release_stream(void* stream)
     }
   }
   for (auto& s : gone) {
-    std::lock_guard<std::mutex> g(s->call); // no call of this stream in flight
+    std::lock_guard<std::recursive_mutex> g(s->call); // no call of this stream in flight
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(s->device);
