@@ -70,10 +70,17 @@ tools/libcsum_genstore%.so: $(SRCS) $(HDRS)
 # Diagnostic A/B builds of the split-form span words' stride (words per
 # range: 1 = packed, 16 = one 128-byte line each; tools/ab_probe.sh).
 # Never loaded by the product.
-s3ab: tools/ab_s3s1.so tools/ab_s3s16.so
+# Cluster (consecutive ranges per XCD run) and offsets-window A/B builds:
+# tools/ab_s3c<C>w<NWIN>.so.
+s3ab: tools/ab_s3s1.so tools/ab_s3s16.so tools/ab_s3c8w1024.so tools/ab_s3c32w1024.so \
+      tools/ab_s3c8w512.so tools/ab_s3c32w512.so
 
 tools/ab_s3s%.so: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DTULIPS_SPAN3_STRIDE=$* -shared -o $@ $(SRCS)
+
+tools/ab_s3c8w1024.so tools/ab_s3c32w1024.so tools/ab_s3c8w512.so tools/ab_s3c32w512.so: $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DTULIPS_SPAN3_CLUSTER=$(word 1,$(subst w, ,$(patsubst tools/ab_s3c%.so,%,$@))) \
+	    -DTULIPS_SPAN3_NWIN=$(word 2,$(subst w, ,$(patsubst tools/ab_s3c%.so,%,$@))) -shared -o $@ $(SRCS)
 
 # Device assembly + resource usage of the kernels (for inspection).
 asm:

@@ -111,15 +111,20 @@ TCS_HD uint32_t finish(uint32_t le_partial, bool start_odd, uint32_t mode,
 // at a time): hardware block b = 8g + x maps to logical block
 // (g / C) * 8C + x * C + g % C. Blocks of a last, incomplete group of 8C map
 // to themselves. A bijection on [0, nb): results never depend on placement.
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
+template<uint32_t C>
+__device__ __forceinline__ uint32_t xcd_block_c(uint32_t b, uint32_t nb)
 {
-  constexpr uint32_t C = TULIPS_XCD_CLUSTER;
   const uint32_t full = (nb / (8u * C)) * (8u * C);
   if (C <= 1 || b >= full) {
     return b;
   }
   const uint32_t x = b & 7u, g = b >> 3;
   return (g / C) * (8u * C) + x * C + g % C;
+}
+
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
+{
+  return xcd_block_c<TULIPS_XCD_CLUSTER>(b, nb);
 }
 #endif
 

@@ -1903,6 +1903,12 @@ csum_span2_kernel(SpanArgs p)
 #define TULIPS_SPAN3_STRIDE 1
 #endif
 constexpr uint64_t SPAN3_STRIDE = TULIPS_SPAN3_STRIDE; // words per range
+#ifndef TULIPS_SPAN3_CLUSTER
+#define TULIPS_SPAN3_CLUSTER 8
+#endif
+#ifndef TULIPS_SPAN3_NWIN
+#define TULIPS_SPAN3_NWIN 1024
+#endif
 
 template<int U, bool NT>
 __global__ __launch_bounds__(256) void
@@ -1910,7 +1916,8 @@ csum_span3_kernel(SpanArgs p)
 {
   constexpr uint32_t NC = 256u * U;      // chunks per range
   constexpr uint64_t W = 16ull * NC;     // bytes per range
-  constexpr uint32_t NWIN = 1024;        // speculative window entries
+  constexpr uint32_t NWIN = TULIPS_SPAN3_NWIN; // speculative window entries
+  constexpr int RW = NWIN / 256;         // window entries per thread
   __shared__ u32x4 s_raw[NC];            // the range's chunks
   __shared__ uint32_t s_sc[NC];          // row-wise wave scans of chunk values
   __shared__ uint32_t s_tot[4 * U];      // per (row, wave) scan totals
@@ -1920,7 +1927,7 @@ csum_span3_kernel(SpanArgs p)
 
   const uint32_t t = threadIdx.x, lane = t & 63u;
   const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const uint32_t k = xcd_block(blockIdx.x, gridDim.x);
+  const uint32_t k = xcd_block_c<TULIPS_SPAN3_CLUSTER>(blockIdx.x, gridDim.x);
   const uintptr_t b = reinterpret_cast<uintptr_t>(p.base);
   const uint64_t d = b & 15u;
   const uintptr_t A = b & ~uintptr_t(15);
@@ -1939,10 +1946,10 @@ csum_span3_kernel(SpanArgs p)
   const uint64_t guess = uint64_t(double(n) * double(mid) / double(p.arena ? p.arena : 1));
   const uint32_t gmax = n > NWIN ? n - NWIN : 0u;
   const uint32_t G = uint32_t(min(guess > NWIN / 2 ? guess - NWIN / 2 : 0ull, uint64_t(gmax)));
-  uint64_t wo[4];
-  uint32_t wl[4];
+  uint64_t wo[RW];
+  uint32_t wl[RW];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < RW; ++r) {
     const uint32_t i = min(G + t + 256u * r, n - 1);
     wo[r] = offs[i];
     wl[r] = lens[i];
@@ -1957,7 +1964,7 @@ csum_span3_kernel(SpanArgs p)
   {
     uint32_t c0 = 0, c1 = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < RW; ++r) {
       const bool in = G + t + 256u * r < n;
       c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg0));
       c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg1));
@@ -2116,7 +2123,7 @@ csum_span3_kernel(SpanArgs p)
   if (ok) {
     // each thread finishes the segments whose window entries it loaded
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < RW; ++r) {
       const uint32_t i = G + t + 256u * r;
       bool act = i >= lo && i < hi;
       if (lo > 0 && i == lo - 1) {
