@@ -721,8 +721,10 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                   "pipeline": pipe_entry(zb, tp),
                   "entry": "tulips_csum_batch_arena (segments in order in one arena)",
                   "geometry": "span, split form: a workgroup per 24 KiB of arena bytes, "
-                              "no halo; a segment crossing ranges is summed in parts that "
-                              "meet in a per-range word (one returning atomic per part)",
+                              "no halo, chunk prefixes in LDS, boundary chunks loaded by "
+                              "the entry holders; a segment crossing ranges is summed in "
+                              "parts that meet in a per-range word (one returning atomic "
+                              "per part)",
                   "traffic": read_traffic("ZIPF"),
                   "parity": "ok" if fnv1a_u16(o) == zgold else "MISMATCH",
                   "read_same_bytes": {"avg_launch_us": round(tr * 1e6, 2),

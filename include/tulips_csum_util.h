@@ -31,19 +31,21 @@ extern "C" {
 #define TULIPS_CSUM_KIND_SPAN 5     /* in-order arenas only
                                        (tulips_csum_batch_arena): a workgroup
                                        per 4 KiB * `unroll` of arena bytes.
-                                       `group` 0 or 6 = split form (default,
-                                       `unroll` 2/4/5/6/7/8/10/12): a segment
-                                       crossing ranges is summed in parts that
-                                       meet in a per-range word of the
-                                       stream's state; 1/2 = segments finished
-                                       where they start, with 1/2 rows of 4 KiB
-                                       read past the range (`unroll`
-                                       2/4/6/8/10/12 for 2, 2/4/6/8 for 1);
-                                       3 = no halo, the crossing segment's
-                                       wave reads its own tail (`unroll`
-                                       6/7/8); 4/5 = boundary-slot form with
-                                       2/1 halo rows (`unroll` 4/6/8/10/12 for
-                                       4, 8 for 5) */
+                                       `group` 0 or 7 = split form (default,
+                                       `unroll` 4..8): a segment crossing
+                                       ranges is summed in parts that meet in
+                                       a per-range word of the stream's state,
+                                       only chunk prefixes in LDS; 6 = the same
+                                       with the chunks staged in LDS
+                                       (`unroll` 2/4/5/6/7/8/10/12); 1/2 =
+                                       segments finished where they start,
+                                       with 1/2 rows of 4 KiB read past the
+                                       range (`unroll` 2/4/6/8/10/12 for 2,
+                                       2/4/6/8 for 1); 3 = no halo, the
+                                       crossing segment's wave reads its own
+                                       tail (`unroll` 6/7/8); 4/5 =
+                                       boundary-slot form with 2/1 halo rows
+                                       (`unroll` 4/6/8/10/12 for 4, 8 for 5) */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning

@@ -24,13 +24,14 @@ import tulips_amd  # noqa: E402
 from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
-# (chunks per lane, form: 0 = default = 6 = split form: no halo, segments
-# split at range boundaries and their parts met in per-range words; 1/2 rows
-# of halo, 3 = none: the crossing segment's wave reads its own tail, 4/5 =
-# boundary-slot form with 2/1 rows)
-GEOMS = ((2, 0), (4, 0), (6, 0), (8, 0), (10, 0), (12, 0), (4, 1), (8, 1), (2, 2), (6, 2),
-         (8, 2), (12, 2), (6, 3), (7, 3), (8, 3), (4, 4), (6, 4), (8, 4), (8, 5), (10, 4),
-         (12, 4), (5, 6), (7, 6))
+# (chunks per lane, form: 0 = default = 7 = split form with only the chunk
+# prefixes in LDS; 6 = split form with the chunks staged in LDS (both: no
+# halo, segments split at range boundaries and their parts met in per-range
+# words); 1/2 rows of halo, 3 = none: the crossing segment's wave reads its
+# own tail, 4/5 = boundary-slot form with 2/1 rows)
+GEOMS = ((4, 0), (6, 0), (8, 0), (2, 6), (5, 6), (6, 6), (7, 6), (10, 6), (12, 6), (4, 1),
+         (8, 1), (2, 2), (6, 2), (8, 2), (12, 2), (6, 3), (7, 3), (8, 3), (4, 4), (6, 4), (8, 4),
+         (8, 5), (10, 4), (12, 4), (5, 7), (7, 7))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -237,7 +238,7 @@ def test_rejects_bad_arguments():
                                             0, 0, None) == 0
 
 
-@pytest.mark.parametrize("u", [g for g in GEOMS if g[1] in (0, 6)])
+@pytest.mark.parametrize("u", [g for g in GEOMS if g[1] in (0, 6, 7)])
 def test_split_words_survive_contract_breaking_batch(oracle, u):
     """The split form's per-range words are left non-zero only by a batch that
     breaks the arena contract (overlapping segments); such residue carries an

@@ -27,13 +27,13 @@ from collections import defaultdict
 # (kernel name fragment, grid size or None, workload label): bench.py's
 # default geometries. The ZIPF kernels are also what the host path launches
 # per staging chunk, so ZIPF is told apart by its grid: the split-form span
-# kernel has one 256-thread workgroup per 24 KiB of the 43,772,673-byte arena
+# kernel (prefix-only LDS) has one 256-thread workgroup per 24 KiB of the 43,772,673-byte arena
 # (1,782 ranges = 456,192 threads), the any-layout packed kernel 8 segments per wave
 # (8,192 waves = 524,288 threads).
 WORKLOADS = [
     ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
     ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
-    ("csum_span3_kernel<6, true>", 456192, "ZIPF"),
+    ("csum_span4_kernel<6, true>", 456192, "ZIPF"),
     ("csum_packed_kernel<8, 4, true, 1>", 524288, "ZIPF_any_layout"),  # PF = 1
     # 65,536 frames, 16 per 256-thread block (the host path's small bursts
     # launch the same kernels with smaller grids)

@@ -28,6 +28,8 @@ def main():
              "s3_4": ("span", 4, 6), "s3_5": ("span", 5, 6), "s3_6": ("span", 6, 6),
              "s3_7": ("span", 7, 6), "s3_8": ("span", 8, 6),
              "s3_10": ("span", 10, 6),
+             "s4_5": ("span", 5, 7), "s4_6": ("span", 6, 7), "s4_7": ("span", 7, 7),
+             "s4_8": ("span", 8, 7),
              "packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                         block=256, sps=2),
              }

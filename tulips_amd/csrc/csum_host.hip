@@ -42,7 +42,7 @@ constexpr uint64_t DEFAULT_CHUNK = 16ull << 20;
 constexpr uint32_t MAX_SEGS_PER_CHUNK = 1u << 20;
 constexpr int NSLOTS = 3;
 // KIND_SPAN chunks per lane for in-order staged chunks (csum_capi.hip; the
-// split form)
+// default split form)
 constexpr int SPAN_UNROLL = 6;
 // Staging-copy threads: the CPUs this process may run on, at most 16 (a GPU's
 // share of a host; 16 threads took pageable F1500 from 37 to 44 GiB/s over 8

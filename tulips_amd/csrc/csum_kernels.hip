@@ -2147,6 +2147,287 @@ csum_span3_kernel(SpanArgs p)
   }
 }
 
+// SPAN, split form without staged chunks (`group` 7): the split form's work
+// cut and per-range words, but only the chunk prefix sums live in LDS
+// (4 B per chunk instead of 20), so seven 256-thread workgroups fit a CU
+// (registers bounded to 7 waves per SIMD) and a ZIPF launch at 24 KiB ranges
+// (1,782 workgroups) is one generation. A segment's two boundary chunks are
+// loaded by the thread holding its window entry, right after the window
+// arrives and while the range's own loads (temporal, so the lines are in L2
+// or in flight) are still outstanding: the first barrier only publishes the
+// window counts. Ranges where more than 256 segments start (tiny segments;
+// one entry per thread no longer suffices) or where the window misses take
+// a slower path with metadata and boundary chunks from memory.
+template<int U, bool NT>
+__global__ __launch_bounds__(256, 7) void
+csum_span4_kernel(SpanArgs p)
+{
+  constexpr uint32_t NC = 256u * U;
+  constexpr uint64_t W = 16ull * NC;
+  constexpr uint32_t NWIN = 1024;
+  constexpr int RW = NWIN / 256;
+  __shared__ uint32_t s_sc[NC];
+  __shared__ uint32_t s_tot[4 * U];
+  __shared__ uint32_t s_woff[4][4 * U];
+  __shared__ uint32_t s_cnt[8];
+  __shared__ uint32_t s_meta[2];
+
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const uint32_t k = xcd_block(blockIdx.x, gridDim.x);
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p.base);
+  const uint64_t d = b & 15u;
+  const uintptr_t A = b & ~uintptr_t(15);
+  const uintptr_t x0 = A + uint64_t(k) * W, x1 = x0 + W;
+  const uintptr_t aend = b + p.arena;
+  const uintptr_t zero = reinterpret_cast<uintptr_t>(k_zero_chunk);
+  const uintptr_t last = p.arena ? ((aend - 1) & ~uintptr_t(15)) : zero;
+  const uint32_t n = p.n;
+  const gu64_ptr offs = reinterpret_cast<gu64_ptr>(reinterpret_cast<uintptr_t>(p.offs));
+  const gu16_ptr lens = reinterpret_cast<gu16_ptr>(reinterpret_cast<uintptr_t>(p.lens));
+  const uint64_t tg0 = k ? uint64_t(k) * W - d : 0, tg1 = uint64_t(k + 1) * W - d;
+  // a chunk of the range (or zeros), clamped into the arena
+  auto chunk_at = [&](uintptr_t a) {
+    return reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero);
+  };
+
+  // 1. the offsets window, then the range's chunks (temporal: the boundary
+  //    chunks are loaded again below)
+  const uint64_t mid = (tg0 + tg1) / 2;
+  const uint64_t guess = uint64_t(double(n) * double(mid) / double(p.arena ? p.arena : 1));
+  const uint32_t gmax = n > NWIN ? n - NWIN : 0u;
+  const uint32_t G = uint32_t(min(guess > NWIN / 2 ? guess - NWIN / 2 : 0ull, uint64_t(gmax)));
+  uint64_t wo[RW];
+  uint32_t wl[RW];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    const uint32_t i = min(G + t + 256u * r, n - 1);
+    wo[r] = offs[i];
+    wl[r] = lens[i];
+  }
+  u32x4 v[U];
+#pragma unroll
+  for (uint32_t j = 0; j < U; ++j) {
+    v[j] = load_chunk<false>(chunk_at(x0 + 16u * (j * 256u + t)));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const bool in = G + t + 256u * r < n;
+      c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg0));
+      c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg1));
+    }
+    if (lane == 0) {
+      s_cnt[w] = c0;
+      s_cnt[4 + w] = c1;
+    }
+  }
+  lds_barrier(); // (the range's loads stay in flight)
+  const uint32_t c0 = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  const uint32_t c1 = s_cnt[4] + s_cnt[5] + s_cnt[6] + s_cnt[7];
+  const uint32_t nw = min(NWIN, n - G);
+  const bool tail_ok = G + NWIN >= n;
+  const bool ok = (c0 > 0 || G == 0) && (c0 < nw || tail_ok) && (c1 > 0 || G == 0) &&
+                  (c1 < nw || tail_ok);
+  const uint32_t lo = G + c0, hi = G + c1;
+  const uint32_t first = lo > 0 ? lo - 1 : 0;
+  // fast path: at most 256 entries to finish, so each thread holds at most
+  // one of them
+  const bool fast = ok && hi - first <= 256u;
+
+  // 2. this thread's entry and its two boundary chunks, issued now
+  bool act = false;
+  uint32_t s = 0, sl = 0;
+  uint64_t so = 0;
+  if (fast) {
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const uint32_t i = G + t + 256u * r;
+      bool a = i >= lo && i < hi;
+      if (lo > 0 && i == lo - 1) {
+        a = min(b + wo[r] + wl[r], aend) > x0;
+      }
+      if (a) {
+        act = true;
+        s = i;
+        so = wo[r];
+        sl = wl[r];
+      }
+    }
+  }
+  const uintptr_t sa = b + so, se = min(b + so + sl, aend);
+  const uintptr_t u0 = max(sa, x0), u1 = min(se, x1);
+  const bool has = act && u1 > u0;
+  const uint32_t ca = has ? uint32_t((u0 - x0) >> 4) : 0u;
+  const uint32_t ce = has ? uint32_t((u1 - 1 - x0) >> 4) : 0u;
+  const u32x4 bh = load_chunk<false>(chunk_at(x0 + 16u * ca));
+  const u32x4 bt = load_chunk<false>(chunk_at(x0 + 16u * ce));
+
+  // 3. row-wise wave scans of the range's chunk values
+#pragma unroll
+  for (uint32_t j = 0; j < U; ++j) {
+    const uint32_t sc = wave_incl_scan(chunk_value(v[j]));
+    s_sc[j * 256u + t] = sc;
+    if (lane == 63) {
+      s_tot[4 * j + w] = sc;
+    }
+  }
+  lds_barrier();
+  {
+    const uint32_t x = lane < 4 * U ? s_tot[lane] : 0u;
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane < 4 * U) {
+      s_woff[w][lane] = inc - x;
+    }
+  }
+  auto P = [&](uint32_t c) { return s_woff[w][c >> 6] + s_sc[c]; };
+
+  // 4. a segment's part in the range; split segments meet in their first
+  //    range's word (as in csum_span3_kernel)
+  const uint32_t want = (p.mode & FLAG_COMPLEMENT) ? 0u : 0xffffu;
+  const bool side_in = (p.mode & MODE_MASK) == MODE_TCP || p.seeds != nullptr;
+  auto emit = [&](uint32_t s, bool act, uintptr_t sa, uintptr_t se, uint32_t sl, uint32_t sum) {
+    SideIn side{0, 0, 0};
+    if (side_in) {
+      side = load_side(act ? s : 0u, p.seeds, p.src, p.dst, p.mode);
+    }
+    bool done = act;
+    if (act && (sa < x0 || se > x1)) {
+      const uint64_t ra = (sa - A) / W;
+      const uint32_t need = uint32_t((se - 1 - A) / W - ra);
+      const uint32_t part = fold32(sum);
+      const uint64_t ep = uint64_t(p.epoch) << 40;
+      const uint64_t mine = ep | (1ull << 32) | part;
+      unsigned long long* wp =
+        reinterpret_cast<unsigned long long*>(p.slots + ra * SPAN3_STRIDE);
+      unsigned long long seen = atomicCAS(wp, 0ull, mine);
+      done = false;
+      for (int round = 0; seen != 0 && round < 64; ++round) {
+        unsigned long long next;
+        if ((seen >> 40) != p.epoch) {
+          next = mine;
+        } else if (uint32_t((seen >> 32) & 0xffu) == need) {
+          done = true;
+          sum = uint32_t(seen) + part;
+          __hip_atomic_store(wp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        } else {
+          next = seen + (1ull << 32) + part;
+        }
+        const unsigned long long prev = atomicCAS(wp, seen, next);
+        if (prev == seen) {
+          break;
+        }
+        seen = prev;
+      }
+    }
+    const uint32_t r =
+      finish(sum, (sa & 1u) != 0, p.mode, side.seed, side.src, side.dst, sl);
+    if (done && p.out) {
+      if (p.nt_store) {
+        __builtin_nontemporal_store(uint16_t(r), p.out + s);
+      } else {
+        p.out[s] = uint16_t(r);
+      }
+    }
+    if (p.bad) {
+      const uint32_t nb =
+        __builtin_popcountll(__builtin_amdgcn_ballot_w64(done && r != want));
+      if (lane == 0 && nb) {
+        atomicAdd(p.bad + CNT_LINE * (blockIdx.x % CNT_SHARDS), nb);
+      }
+    }
+  };
+  // sum of [u0, u1) from the prefix and the two boundary chunks
+  auto part_of = [&](uintptr_t u0, uintptr_t u1, uint32_t ca, uint32_t ce, const u32x4& bh,
+                     const u32x4& bt) {
+    const int ha = int(u0 & 15u), tb = int(((u1 - 1) & 15u) + 1u);
+    return ca == ce ? masked_value(bh, ha, tb)
+                    : masked_value(bh, ha, 16) + (P(ce - 1) - P(ca)) + masked_value(bt, 0, tb);
+  };
+
+  if (fast) {
+    if (__builtin_amdgcn_ballot_w64(act) != 0) {
+      emit(s, act, sa, se, sl, has ? part_of(u0, u1, ca, ce, bh, bt) : 0u);
+    }
+    return;
+  }
+  // rare: [lo, hi) from a search when the window missed; metadata and
+  // boundary chunks from memory, 256 entries per round
+  uint32_t L = lo, H = hi;
+  if (!ok) {
+    if (w == 0) {
+      uint32_t L0 = 0, R0 = n, L1 = 0, R1 = n;
+      while (R0 > L0 || R1 > L1) {
+        const uint32_t st0 = (R0 - L0 + 255u) >> 8, st1 = (R1 - L1 + 255u) >> 8;
+        uint64_t o0[4], o1[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t q = lane + 64u * r;
+          o0[r] = offs[min(uint64_t(L0) + uint64_t(q) * st0, uint64_t(n - 1))];
+          o1[r] = offs[min(uint64_t(L1) + uint64_t(q) * st1, uint64_t(n - 1))];
+        }
+        uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t q = lane + 64u * r;
+          const bool in0 = uint64_t(L0) + uint64_t(q) * st0 < R0;
+          const bool in1 = uint64_t(L1) + uint64_t(q) * st1 < R1;
+          d0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in0 && o0[r] < tg0));
+          d1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in1 && o1[r] < tg1));
+        }
+        if (R0 > L0) {
+          span_narrow(L0, R0, st0, __builtin_amdgcn_readfirstlane(d0));
+        }
+        if (R1 > L1) {
+          span_narrow(L1, R1, st1, __builtin_amdgcn_readfirstlane(d1));
+        }
+      }
+      if (lane == 0) {
+        s_meta[0] = L0;
+        s_meta[1] = L1;
+      }
+    }
+    lds_barrier();
+    L = s_meta[0];
+    H = s_meta[1];
+  }
+  for (uint32_t s0 = L > 0 ? L - 1 : 0; s0 < H; s0 += 256u) {
+    const uint32_t i = s0 + t;
+    bool a = i < H;
+    const uint64_t o = a ? p.offs[i] : 0;
+    const uint32_t l = a ? p.lens[i] : 0u;
+    const uintptr_t ia = b + o, ie = min(b + o + l, aend);
+    if (i < L) {
+      a = a && ie > x0;
+    }
+    const uintptr_t v0 = max(ia, x0), v1 = min(ie, x1);
+    const bool h = a && v1 > v0;
+    const uint32_t qa = h ? uint32_t((v0 - x0) >> 4) : 0u;
+    const uint32_t qe = h ? uint32_t((v1 - 1 - x0) >> 4) : 0u;
+    const u32x4 ch = load_chunk<false>(chunk_at(x0 + 16u * qa));
+    const u32x4 ct = load_chunk<false>(chunk_at(x0 + 16u * qe));
+    emit(i, a, a ? ia : b, a ? ie : b, a ? l : 0u, h ? part_of(v0, v1, qa, qe, ch, ct) : 0u);
+  }
+}
+
+template<int U, bool NT>
+hipError_t
+launch_span4_u(const SpanArgs& sp, hipStream_t stream)
+{
+  constexpr uint64_t W = 4096ull * U;
+  const uint64_t ranges = span_ranges(sp.base, sp.arena, W);
+  if (ranges > 0x7fffffffull) {
+    return hipErrorInvalidValue;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_span4_kernel<U, NT>), dim3(uint32_t(ranges)), dim3(256), 0, stream,
+                     sp);
+  return hipGetLastError();
+}
+
 template<int U, bool NT>
 hipError_t
 launch_span3_u(const SpanArgs& sp, hipStream_t stream)
@@ -2395,7 +2676,6 @@ bool
 span_geometry_ok(int u, int group)
 {
   switch (group) {
-    case 0:
     case 6:
       return u == 2 || (u >= 4 && u <= 8) || u == 10 || u == 12;
     case 1:
@@ -2408,6 +2688,9 @@ span_geometry_ok(int u, int group)
       return u == 4 || u == 6 || u == 8 || u == 10 || u == 12;
     case 5:
       return u == 8;
+    case 0:
+    case 7:
+      return u >= 4 && u <= 8;
     default:
       return false;
   }
@@ -2422,9 +2705,9 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
   if (a.n == 0) {
     return hipSuccess;
   }
-  if (a.group == 0 || a.group == 6) {
-    // split form (the default): the stream's per-range words, held for the
-    // launch
+  if (a.group == 0 || a.group == 6 || a.group == 7) {
+    // split forms (7, the default, and 6): the stream's per-range words,
+    // held for the launch
     std::shared_ptr<StreamState> ss;
     hipError_t e = stream_state(stream, &ss);
     if (e != hipSuccess) {
@@ -2437,6 +2720,19 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
                    &sp3.epoch);
     if (e != hipSuccess) {
       return e == hipErrorStreamCaptureUnsupported ? hipErrorInvalidValue : e;
+    }
+#define TCS_S4CASE(U_)                                                         \
+  if (a.group != 6 && a.unroll == U_) {                                        \
+    return launch_span4_u<U_, true>(sp3, stream);                              \
+  }
+    TCS_S4CASE(4)
+    TCS_S4CASE(5)
+    TCS_S4CASE(6)
+    TCS_S4CASE(7)
+    TCS_S4CASE(8)
+#undef TCS_S4CASE
+    if (a.group != 6) {
+      return hipErrorInvalidValue;
     }
 #define TCS_S3CASE(U_)                                                         \
   if (a.unroll == U_) {                                                        \
