@@ -206,6 +206,7 @@ def test_release_stream_keeps_memory_flat(oracle):
     out = torch.empty(2048 * 1024, dtype=torch.uint8, device="cuda:0")
     olen = torch.zeros(1024, dtype=torch.int16, device="cuda:0")
     first = torch.empty(17, dtype=torch.int32, device="cuda:0")
+    aout = torch.empty(n, dtype=torch.int16, device="cuda:0")
 
     def cycle():
         s = C.c_void_p()
@@ -221,6 +222,10 @@ def test_release_stream_keeps_memory_flat(oracle):
                                                    sl.data_ptr(), 16, 1460, out.data_ptr(),
                                                    2048, 1024, olen.data_ptr(),
                                                    first.data_ptr(), st) == 0
+        # an arena call (split-form span words: 17 arrays)
+        assert csum.lib.tulips_csum_batch_arena(arena.data_ptr(), n * L, offs.data_ptr(),
+                                                lens.data_ptr(), None, None, None,
+                                                aout.data_ptr(), n, MODE_INET, st) == 0
         assert csum.lib.tulips_csum_release_stream(st) == 0
         assert hip.hipStreamDestroy(s) == 0
 
@@ -232,11 +237,56 @@ def test_release_stream_keeps_memory_flat(oracle):
         cycle()
     torch.cuda.synchronize()
     free1, _ = torch.cuda.mem_get_info()
-    # unreleased, each stream would keep ~1.4 MB (17 shard sets, the scan
-    # totals, run map and descriptors): 140 MB over 100 streams
+    # unreleased, each stream would keep ~1.9 MB (17 shard sets, the scan
+    # totals, run map and descriptors, 17 span word arrays): 190 MB over 100
+    # streams
     assert free0 - free1 < 8 << 20, (free0 - free1)
     np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),
                                   counters_of(fx["expect"]))
+
+
+@pytest.mark.gpu
+def test_captured_arena_calls_own_their_words(oracle):
+    """Split-form arena calls captured on a stream with no state yet (the
+    words are made in relaxed capture mode), replayed on another stream while
+    direct arena calls of another batch run on the capture stream: both
+    exact every time."""
+    import torch
+    from tulips_amd import csum
+    rng = np.random.default_rng(77)
+    res = []
+    for n in (30000, 20000):
+        lens = rng.integers(40, 9000, n).astype(np.uint16)
+        offs = np.zeros(n, np.uint64)
+        np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+        total = int(lens.astype(np.int64).sum())
+        buf = rng.integers(0, 256, total + 16, dtype=np.uint8)
+        exp = oracle.batch(buf, offs, lens, mode=MODE_INET, nthreads=8)
+        dv = _dev(buf, offs.astype(np.int64), lens.view(np.int16))
+        res.append((n, total, dv, exp, torch.empty(n, dtype=torch.int16, device="cuda:0")))
+    cap, other = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def call(r, st):
+        n, total, (a, o, l), _, out = r
+        assert csum.lib.tulips_csum_batch_arena(a.data_ptr(), total, o.data_ptr(), l.data_ptr(),
+                                                None, None, None, out.data_ptr(), n,
+                                                MODE_INET, st) == 0
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        for _ in range(3):
+            call(res[0], cap.cuda_stream)
+    for _ in range(20):
+        res[0][4].fill_(0)
+        res[1][4].fill_(0)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(other):
+            g.replay()
+        call(res[1], cap.cuda_stream)
+        torch.cuda.synchronize()
+        for r in res:
+            np.testing.assert_array_equal(r[4].cpu().numpy().view(np.uint16), r[3])
+    del g
+    csum.release_stream(cap.cuda_stream)
 
 
 @pytest.mark.gpu
