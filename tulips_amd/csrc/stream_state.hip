@@ -136,25 +136,35 @@ call_shards(StreamState& s, bool capturing, uint32_t** out)
   return hipSuccess;
 }
 
-// Zeroed words on `device` (not stream-ordered: used only before any launch
-// can read them). Inside a capture the thread's capture mode is relaxed for
-// the allocation, so hipMalloc is allowed, and the zeroing runs on a private
-// stream that is not capturing.
+// `count` arrays of zeroed words on `device` (not stream-ordered: used only
+// before any launch can read them). Inside a capture the thread's capture
+// mode is relaxed for the allocations, so hipMalloc is allowed, and the
+// zeroing runs on a private stream that is not capturing.
 hipError_t
-zeroed_words(int device, uint64_t words, bool capturing, uint64_t** out)
+zeroed_words(int device, uint64_t words, bool capturing, int count, std::vector<uint64_t*>* out)
 {
   hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
   if (capturing) {
     (void)hipThreadExchangeStreamCaptureMode(&mode);
   }
-  void* p = nullptr;
-  hipError_t e = device_malloc(device, &p, sizeof(uint64_t) * words);
-  hipStream_t z = nullptr;
+  std::vector<void*> made;
+  hipError_t e = hipSuccess;
+  for (int k = 0; k < count && e == hipSuccess; ++k) {
+    void* p = nullptr;
+    if ((e = device_malloc(device, &p, sizeof(uint64_t) * words)) == hipSuccess) {
+      made.push_back(p);
+    }
+  }
   int prev = 0;
   (void)hipGetDevice(&prev);
   if (e == hipSuccess && (e = hipSetDevice(device)) == hipSuccess) {
+    hipStream_t z = nullptr;
     if ((e = hipStreamCreateWithFlags(&z, hipStreamNonBlocking)) == hipSuccess) {
-      e = hipMemsetAsync(p, 0, sizeof(uint64_t) * words, z);
+      for (void* p : made) {
+        if (e == hipSuccess) {
+          e = hipMemsetAsync(p, 0, sizeof(uint64_t) * words, z);
+        }
+      }
       const hipError_t e2 = hipStreamSynchronize(z);
       e = e != hipSuccess ? e : e2;
       (void)hipStreamDestroy(z);
@@ -165,12 +175,13 @@ zeroed_words(int device, uint64_t words, bool capturing, uint64_t** out)
     (void)hipThreadExchangeStreamCaptureMode(&mode);
   }
   if (e != hipSuccess) {
-    if (p) {
-      free_on(device, std::vector<void*>{ p });
-    }
+    free_on(device, made);
     return e;
   }
-  *out = static_cast<uint64_t*>(p);
+  out->clear();
+  for (void* p : made) {
+    out->push_back(static_cast<uint64_t*>(p));
+  }
   return hipSuccess;
 }
 
@@ -192,13 +203,7 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint32
       // direct words plus spares for captures, all zeroed before use
       const uint64_t want = need < 4096 ? 4096 : need;
       std::vector<uint64_t*> made;
-      hipError_t e = hipSuccess;
-      for (int k = 0; k <= SPARE_SHARDS && e == hipSuccess; ++k) {
-        uint64_t* p = nullptr;
-        if ((e = zeroed_words(s.device, want, false, &p)) == hipSuccess) {
-          made.push_back(p);
-        }
-      }
+      hipError_t e = zeroed_words(s.device, want, false, 1 + SPARE_SHARDS, &made);
       if (e == hipSuccess) {
         e = hipStreamSynchronize(s.stream); // the old arrays are idle
       }
@@ -237,11 +242,12 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint32
     size = s.span_nslots;
   } else {
     size = need < 4096 ? 4096 : need;
-    const hipError_t e = zeroed_words(s.device, size, true, &p);
-    if (e != hipSuccess) {
+    std::vector<uint64_t*> made;
+    if (zeroed_words(s.device, size, true, 1, &made) != hipSuccess) {
       (void)hipGetLastError();
       return hipErrorStreamCaptureUnsupported;
     }
+    p = made[0];
   }
   s.span_owned.push_back(p);
   const uint32_t ep = next_epoch(s);
