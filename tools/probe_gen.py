@@ -29,7 +29,7 @@ def main():
              "s3_7": ("span", 7, 6), "s3_8": ("span", 8, 6),
              "s3_10": ("span", 10, 6),
              "s4_5": ("span", 5, 7), "s4_6": ("span", 6, 7), "s4_7": ("span", 7, 7),
-             "s4_8": ("span", 8, 7),
+             "s4_8": ("span", 8, 7), "s4_6t": ("span", 6, 7, 0), "s4_8t": ("span", 8, 7, 0),
              "packed8x4pf": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                         block=256, sps=2),
              }
@@ -53,7 +53,8 @@ def main():
                 continue
             if isinstance(t, tuple):
                 t = csum.Tuning(kind=csum.KIND_SPAN, unroll=t[1],
-                                group=t[2] if len(t) > 2 else 0, nontemporal=1)
+                                group=t[2] if len(t) > 2 else 0,
+                                nontemporal=t[3] if len(t) > 3 else 1)
 
                 def fn(i, sh, t=t):
                     b = i % NB
