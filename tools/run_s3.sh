@@ -1,6 +1,6 @@
 #!/bin/bash
 # Split-form span kernel session (under gpurun): the arena parity suite, then
-# the s3 stride A/B probe (tools/ab_probe.sh).
+# the s3 stride A/B probe (tools/ab_probe.sh; `make s3ab` first).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

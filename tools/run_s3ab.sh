@@ -1,6 +1,6 @@
 #!/bin/bash
 # Split-form span A/B (under gpurun): parity of the most different variant,
-# then tools/ab_probe.sh over AB_ORDER.
+# then tools/ab_probe.sh over AB_ORDER (`make s3ab` first).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
