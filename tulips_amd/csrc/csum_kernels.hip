@@ -1909,6 +1909,9 @@ constexpr uint64_t SPAN3_STRIDE = TULIPS_SPAN3_STRIDE; // words per range
 #ifndef TULIPS_SPAN3_NWIN
 #define TULIPS_SPAN3_NWIN 1024
 #endif
+#ifndef TULIPS_SPAN4_NWIN
+#define TULIPS_SPAN4_NWIN 1024
+#endif
 
 template<int U, bool NT>
 __global__ __launch_bounds__(256) void
@@ -2164,7 +2167,7 @@ csum_span4_kernel(SpanArgs p)
 {
   constexpr uint32_t NC = 256u * U;
   constexpr uint64_t W = 16ull * NC;
-  constexpr uint32_t NWIN = 1024;
+  constexpr uint32_t NWIN = TULIPS_SPAN4_NWIN; // speculative window entries
   constexpr int RW = NWIN / 256;
   __shared__ uint32_t s_sc[NC];
   __shared__ uint32_t s_tot[4 * U];
