@@ -11,57 +11,37 @@
 extern "C" {
 #endif
 
-/* Kernel families (tulips_csum_tuning.kind). */
+/* Kernel families (tulips_csum_tuning.kind). Kinds 2 and 4 (hybrid,
+   workgroup-balanced) and the other span forms are measured variants kept
+   outside the library (tools/variants/); the library rejects them. */
 #define TULIPS_CSUM_KIND_DEFAULT 0
-#define TULIPS_CSUM_KIND_SUBGROUP 1 /* `group` lanes (16/32/64) per segment */
-#define TULIPS_CSUM_KIND_HYBRID 2   /* variable only: `group`-lane subgroups
-                                       (8/16/32) for short segments, `sps`
-                                       of them in flight per subgroup; whole
-                                       wave for long ones */
+#define TULIPS_CSUM_KIND_SUBGROUP 1 /* `group` lanes (16/32/64) per segment,
+                                       `unroll` chunks per lane in flight
+                                       (16/32: 2/4/8; 64: 4/8/12) */
 #define TULIPS_CSUM_KIND_PACKED 3   /* variable only: one wave per `group`
-                                       segments (8/16/32/64), their chunks
-                                       packed end to end, `unroll` 64-chunk
-                                       windows in flight (2/4/8) */
-#define TULIPS_CSUM_KIND_BALANCED 4 /* variable only: a workgroup of `block`/64
-                                       waves (4 or 8) owns 8 segments per wave;
-                                       the workgroup's chunks are packed end to
-                                       end and split evenly over its waves,
-                                       `unroll` windows (2/4) per batch,
-                                       double-buffered; `group` must be 8 */
+                                       segments (8/16), their chunks packed
+                                       end to end, `unroll` 64-chunk windows
+                                       per batch (2/4), double-buffered
+                                       (`sps` 2) */
 #define TULIPS_CSUM_KIND_SPAN 5     /* in-order arenas only
                                        (tulips_csum_batch_arena): a workgroup
-                                       per 4 KiB * `unroll` of arena bytes.
-                                       `group` 0 or 7 = split form (default,
-                                       `unroll` 4..8): a segment crossing
-                                       ranges is summed in parts that meet in
-                                       a per-range word of the stream's state,
-                                       only chunk prefixes in LDS; 6 = the same
-                                       with the chunks staged in LDS
-                                       (`unroll` 2/4/5/6/7/8/10/12); 1/2 =
-                                       segments finished where they start,
-                                       with 1/2 rows of 4 KiB read past the
-                                       range (`unroll` 2/4/6/8/10/12 for 2,
-                                       2/4/6/8 for 1); 3 = no halo, the
-                                       crossing segment's wave reads its own
-                                       tail (`unroll` 6/7/8); 4/5 =
-                                       boundary-slot form with 2/1 halo rows
-                                       (`unroll` 4/6/8/10/12 for 4, 8 for 5) */
+                                       per 4 KiB * `unroll` (4..8) of arena
+                                       bytes; a segment crossing ranges is
+                                       summed in parts that meet in a
+                                       per-range word of the stream's state.
+                                       `group` 0 (or 7: the same form) */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning
 {
   int32_t kind;        /* TULIPS_CSUM_KIND_* */
   int32_t group;       /* see kind */
-  int32_t unroll;      /* 16-byte chunks in flight per lane: 2, 4 or 8 */
+  int32_t unroll;      /* see kind */
   int32_t nontemporal; /* bit 0: nt loads, bit 1: nt result stores; -1 = default */
   uint32_t max_blocks; /* grid cap; 0 = default */
   int32_t block;       /* threads per workgroup: 256, 512 or 1024; 0 = default */
-  int32_t sps;         /* HYBRID: short segments per subgroup issued together
-                          (1, 2, 4); PACKED: 1 = one batch of windows at a
-                          time, 2 = double-buffered, 3 = double-buffered with
-                          the next group's metadata prefetched (grid-stride;
-                          pays with max_blocks below one group per wave);
-                          0 = default */
+  int32_t sps;         /* PACKED: 2 = double-buffered windows (the only
+                          form; 0 = default) */
 } tulips_csum_tuning;
 
 /* The geometry tulips_csum_batch_fixed / tulips_csum_batch would pick. */

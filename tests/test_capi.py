@@ -172,7 +172,8 @@ def test_batch_validation_without_gpu():
     for kind, unroll, halo in ((csum.KIND_PACKED, 4, 0), (csum.KIND_SPAN, 3, 0),
                                (csum.KIND_SPAN, 10, 1), (csum.KIND_SPAN, 8, 9), (csum.KIND_SPAN, 2, 0),
                                (csum.KIND_SPAN, 2, 4), (csum.KIND_SPAN, 9, 6),
-                               (csum.KIND_SPAN, 13, 0)):
+                               (csum.KIND_SPAN, 13, 0), (csum.KIND_SPAN, 6, 6),
+                               (csum.KIND_SPAN, 8, 2), (csum.KIND_SPAN, 6, 3)):
         t = csum.Tuning(kind=kind, unroll=unroll, group=halo)
         assert lib.tulips_csum_batch_arena_tuned(FAKE, 16, FAKE, FAKE, None, None, None, FAKE,
                                                  4, 0, C.byref(t), None) == 1, (kind, unroll)
@@ -197,16 +198,19 @@ def test_default_tuning():
     assert t.group in (16, 32, 64) and t.unroll in (2, 4, 8)
     t = csum.default_tuning(0, variable=True)
     assert t.kind == csum.KIND_PACKED and t.group == 8 and t.unroll == 4 and t.sps == 2
-    # hybrid and packed geometries are for variable-length batches only
-    for kind in (csum.KIND_HYBRID, csum.KIND_PACKED):
+    # packed geometries are for variable-length batches only; kinds 2 and 4
+    # (hybrid, workgroup-balanced) live in tools/variants, not the library
+    for kind in (2, 4, csum.KIND_PACKED):
         bad = csum.Tuning(kind=kind, group=16, unroll=4, nontemporal=1)
         assert csum.lib.tulips_csum_batch_fixed_tuned(FAKE, 1500, 1500, None, None, None,
                                                       FAKE, 4, 0, C.byref(bad), None) == 1
-    for kind, g, u, s in ((csum.KIND_HYBRID, 16, 3, 1), (csum.KIND_HYBRID, 16, 8, 2),
-                          (csum.KIND_PACKED, 8, 8, 1), (csum.KIND_PACKED, 5, 4, 1),
-                          (csum.KIND_PACKED, 64, 2, 1), (csum.KIND_PACKED, 16, 4, 5),
-                          (csum.KIND_HYBRID, 12, 4, 1), (csum.KIND_SUBGROUP, 8, 4, 0),
-                          (csum.KIND_SUBGROUP, 16, 4, 2), (7, 16, 4, 0)):
+    for kind, g, u, s in ((2, 16, 2, 1), (2, 8, 4, 2), (4, 8, 4, 2),
+                          (csum.KIND_PACKED, 8, 8, 2), (csum.KIND_PACKED, 5, 4, 2),
+                          (csum.KIND_PACKED, 64, 4, 2), (csum.KIND_PACKED, 16, 4, 5),
+                          (csum.KIND_PACKED, 8, 4, 1), (csum.KIND_PACKED, 8, 4, 3),
+                          (csum.KIND_PACKED, 8, 4, 4), (csum.KIND_SUBGROUP, 8, 4, 0),
+                          (csum.KIND_SUBGROUP, 16, 4, 2), (csum.KIND_SUBGROUP, 32, 3, 0),
+                          (7, 16, 4, 0)):
         bad = csum.Tuning(kind=kind, group=g, unroll=u, nontemporal=1, sps=s)
         assert csum.lib.tulips_csum_batch_tuned(FAKE, FAKE, FAKE, None, None, None, FAKE, 4,
                                                 0, C.byref(bad), None) == 1

@@ -20,23 +20,16 @@ from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
 
-SUB, HYB, PCK = csum.KIND_SUBGROUP, csum.KIND_HYBRID, csum.KIND_PACKED
+SUB, PCK = csum.KIND_SUBGROUP, csum.KIND_PACKED
+# The shipped geometries (include/tulips_csum_util.h). The library's defaults
+# pick SUBGROUP 16x4 / 32x4 / 64x8 / 64x12 by fixed length and PACKED 8x4
+# (double-buffered) for variable lengths at any offsets.
 # (kind, group, unroll, nontemporal bits, sps)
-GEOMETRIES = [(SUB, g, u, nt, 0) for g in (16, 32, 64) for u in (2, 4, 8) for nt in (0, 1, 3)]
-GEOMETRIES += [(SUB, g, u, 1, 0) for (g, u) in ((16, 6), (32, 3), (64, 9), (64, 12))]
-# hybrid short/long variable-length kernel, with 1/2/4 short segments in flight
-GEOMETRIES += [(HYB, 8, 4, 1, 1), (HYB, 8, 4, 1, 2), (HYB, 8, 4, 0, 4), (HYB, 8, 8, 0, 1),
-               (HYB, 16, 2, 0, 1), (HYB, 16, 2, 1, 2), (HYB, 16, 2, 1, 4),
-               (HYB, 16, 4, 1, 1), (HYB, 16, 4, 3, 2), (HYB, 16, 8, 1, 1), (HYB, 32, 4, 0, 1)]
-# packed kernel: `group` segments per wave, `unroll` 64-chunk windows in flight
-PACKED = [(4, 4), (6, 4), (8, 2), (8, 4), (12, 4), (16, 2), (16, 4), (16, 8), (32, 4), (32, 8), (64, 4), (64, 8)]
-GEOMETRIES += [(PCK, s, u, nt, 1) for (s, u) in PACKED for nt in (0, 1)]
-# ... and with the double-buffered window loop (sps=2)
-GEOMETRIES += [(PCK, s, u, 1, 2) for (s, u) in PACKED]
-# ... and with the next group's metadata prefetched (sps=3)
-GEOMETRIES += [(PCK, s, u, 1, 3) for (s, u) in PACKED]
-# ... and with lane-parallel cursors (sps=4)
-GEOMETRIES += [(PCK, s, u, 1, 4) for (s, u) in PACKED if s in (4, 8, 16, 32) and u in (2, 4)]
+SUBGROUP = [(16, 2), (16, 4), (16, 8), (32, 2), (32, 4), (32, 8), (64, 4), (64, 8), (64, 12)]
+GEOMETRIES = [(SUB, g, u, nt, 0) for (g, u) in SUBGROUP for nt in (0, 1, 3)]
+# packed kernel: `group` segments per wave, `unroll` 64-chunk windows per batch
+PACKED = [(8, 2), (8, 4), (16, 2), (16, 4)]
+GEOMETRIES += [(PCK, s, u, nt, 2) for (s, u) in PACKED for nt in (0, 1)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -169,9 +162,8 @@ def test_zipf_digest(golden, oracle, name):
     if b["mode"] == "tcp":
         kw = dict(src=d(np.full(n, ip4(10, 1, 0, 1), np.uint32)),
                   dst=d(np.full(n, ip4(10, 1, 0, 2), np.uint32)), mode=MODE_TCP)
-    geoms = [None] + [(SUB, g, 1) for g in (16, 32, 64)] + [(HYB, g, 1) for g in (8, 16, 32)]
-    geoms += [(HYB, 8, 2), (HYB, 8, 4), (HYB, 16, 2)]
-    geoms += [(PCK, s_, 1, u_) for (s_, u_) in PACKED]
+    geoms = [None] + [(SUB, g, 1) for g in (16, 32, 64)]
+    geoms += [(PCK, s_, 2, u_) for (s_, u_) in PACKED]
     for geo in geoms:
         t = None if geo is None else csum.Tuning(kind=geo[0], group=geo[1],
                                                  unroll=geo[3] if len(geo) > 3 else 4,
@@ -220,12 +212,11 @@ def test_random_vs_oracle_all_alignments(oracle):
 
 @pytest.mark.parametrize("geo", PACKED)
 def test_packed_random_vs_oracle(oracle, geo):
-    """PACKED kernel: segments laid end to end in one chunk space per wave.
-    Lengths mix empty, 1..63 B, Zipf-like and up to 65,535 B; any alignment;
-    runs of empty segments at wave starts/ends; n not a multiple of the wave's
-    segment count; grid-stride (max_blocks) on and off; single- and
-    double-buffered window loops (sps 1/2), the latter with the next
-    group's metadata prefetched (sps 3, several groups per wave when capped)."""
+    """PACKED kernel: segments laid end to end in one chunk space per wave,
+    double-buffered windows. Lengths mix empty, 1..63 B, Zipf-like and up to
+    65,535 B; any alignment; runs of empty segments at wave starts/ends; n not
+    a multiple of the wave's segment count; grid-stride (max_blocks) on and
+    off, several groups per wave when capped."""
     s_, u_ = geo
     rng = np.random.default_rng(1000 + s_ * 10 + u_)
     arena = rng.integers(0, 256, 2 << 20, dtype=np.uint8)
@@ -253,10 +244,7 @@ def test_packed_random_vs_oracle(oracle, geo):
     for mode in (MODE_RAW, MODE_TCP | FLAG_COMPLEMENT):
         exp = oracle.batch(arena, offs, lens, seeds=seeds, src=src, dst=dst, mode=mode,
                            nthreads=8)
-        cases = [(0, 1), (5, 1), (0, 2), (5, 2), (0, 3), (5, 3), (37, 3)]
-        if s_ in (4, 8, 16, 32) and u_ in (2, 4):      # lane-parallel cursors (sps 4)
-            cases += [(0, 4), (5, 4), (37, 4)]
-        for max_blocks, sps in cases:
+        for max_blocks, sps in ((0, 2), (5, 2), (37, 2)):
             t = csum.Tuning(kind=PCK, group=s_, unroll=u_, nontemporal=1,
                             max_blocks=max_blocks, sps=sps)
             got = tulips_amd.batch(da, do, dl, seeds=ds_, src=dsrc, dst=ddst, mode=mode,
@@ -388,68 +376,3 @@ def test_empty_batch_is_noop():
     lens = torch.empty(0, dtype=torch.uint16, device=DEV)
     out = tulips_amd.batch(arena, offs, lens)
     assert out.numel() == 0
-
-
-# -- workgroup-balanced variable-length kernel (TULIPS_CSUM_KIND_BALANCED) ----
-BALANCED = [(256, 2, 2), (256, 4, 2), (512, 2, 2), (512, 4, 2), (256, 4, 1), (256, 6, 1),
-            (512, 4, 1), (512, 6, 1)]
-
-
-@pytest.mark.parametrize("geo", BALANCED)
-def test_balanced_random_vs_oracle(oracle, golden, geo):
-    """BALANCED kernel: a workgroup's segments packed end to end and its chunk
-    space split evenly over its waves, partials meeting in LDS. Same mix as the
-    packed test (empty, tiny, long up to 65,535 B, any alignment, all-zero /
-    all-0xFF bytes), n not a multiple of the workgroup's 8 x waves segments,
-    grid-stride (max_blocks) on and off; plus the adversarial fixture and the
-    reference's ZIPF digest."""
-    blk, u_, sps = geo
-    BAL = csum.KIND_BALANCED
-    rng = np.random.default_rng(7000 + blk + u_)
-    arena = rng.integers(0, 256, 2 << 20, dtype=np.uint8)
-    arena[:4096] = 0
-    arena[4096:8192] = 0xFF
-    n = 20000 + 5
-    lens = rng.integers(0, 3000, n).astype(np.uint16)
-    lens[rng.random(n) < 0.15] = 0
-    lens[:100] = 0                          # whole workgroups of empty segments
-    lens[rng.integers(0, n, 60)] = rng.integers(60000, 65536, 60)
-    lens[rng.integers(0, n, 300)] = rng.integers(1, 64, 300)
-    lens[4000:4064] = 65535                 # a workgroup of maximal segments
-    offs = np.array([rng.integers(0, len(arena) - int(L)) for L in lens], dtype=np.uint64)
-    zero_idx = rng.integers(0, n, 200)
-    lens[zero_idx] = np.minimum(lens[zero_idx], 2000)
-    offs[zero_idx] = rng.integers(0, 4096 - 2000, 200)
-    seeds = rng.integers(0, 65536, n, dtype=np.uint16)
-    seeds[zero_idx[:100]] = 0
-    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
-    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
-    da, do, dl = d(arena), d(offs), d(lens)
-    ds_, dsrc, ddst = d(seeds), d(src), d(dst)
-    for mode in (MODE_RAW, MODE_INET, MODE_TCP | FLAG_COMPLEMENT):
-        exp = oracle.batch(arena, offs, lens, seeds=seeds, src=src, dst=dst, mode=mode,
-                           nthreads=8)
-        for max_blocks in (0, 3, 37):
-            t = csum.Tuning(kind=BAL, group=8, unroll=u_, nontemporal=1, block=blk,
-                            max_blocks=max_blocks, sps=sps)
-            got = tulips_amd.batch(da, do, dl, seeds=ds_, src=dsrc, dst=ddst, mode=mode,
-                                   tuning=t)
-            np.testing.assert_array_equal(u16(got), exp, err_msg=f"{hex(mode)} {max_blocks}")
-    adv = golden.adversarial()
-    t = csum.Tuning(kind=BAL, group=8, unroll=u_, nontemporal=1, block=blk, sps=sps)
-    out = tulips_amd.batch(d(adv["arena"]), d(adv["offsets"]), d(adv["lengths"]),
-                           src=d(adv["src"]), dst=d(adv["dst"]), mode=MODE_TCP, tuning=t)
-    np.testing.assert_array_equal(u16(out), adv["expect_tcp"])
-    g = golden.digests()["batches"]["ZIPF"]
-    lz = oracle.zipf_lengths(65536)
-    oz = np.concatenate([[0], np.cumsum(lz[:-1], dtype=np.uint64)]).astype(np.uint64)
-    az = oracle.splitmix_bytes(int(lz.astype(np.int64).sum()) + 64)
-    out = tulips_amd.batch(d(az), d(oz), d(lz), tuning=t)
-    assert f"{oracle.fnv1a_u16(u16(out)):016x}" == g["fnv1a64"]
-
-
-def test_balanced_rejects_bad_geometry():
-    t = csum.Tuning(kind=csum.KIND_BALANCED, group=16, unroll=2, block=256)
-    assert csum.lib.tulips_csum_batch_tuned(1, 1, 1, None, None, None, 1, 4, 0, t, None) == 1
-    t = csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=8, block=256)
-    assert csum.lib.tulips_csum_batch_tuned(1, 1, 1, None, None, None, 1, 4, 0, t, None) == 1

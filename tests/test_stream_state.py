@@ -290,6 +290,57 @@ def test_captured_arena_calls_own_their_words(oracle):
 
 
 @pytest.mark.gpu
+def test_captured_contract_breaking_replay_does_not_spoil_the_next(oracle):
+    """one captured arena call replayed first over a batch
+    that breaks the arena contract (overlapping segments) and then, with the
+    same buffers refilled, over valid batches. The split words carry the
+    launch's dispatch id, which differs per replay, so the bad replay's
+    residue is taken over, never added to: every valid replay is exact."""
+    import torch
+    from tulips_amd import csum
+    rng = np.random.default_rng(4040)
+    n = 20000
+    lens = rng.integers(1000, 9000, n).astype(np.uint16)
+    offs = np.zeros(n, np.uint64)
+    np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+    total = int(lens.astype(np.int64).sum())
+    buf = rng.integers(0, 256, total + 16, dtype=np.uint8)
+    exp = oracle.batch(buf, offs, lens, mode=MODE_INET, nthreads=8)
+    bad = offs.copy()
+    bad[1::3] -= np.minimum(bad[1::3], np.uint64(6000))     # overlaps its predecessors
+    bad = np.maximum.accumulate(bad)
+    a, o, l = _dev(buf, offs.astype(np.int64), lens.view(np.int16))
+    good_o = o.clone()
+    bad_o = torch.from_numpy(bad.astype(np.int64)).to("cuda:0")
+    out = torch.empty(n, dtype=torch.int16, device="cuda:0")
+    cap = torch.cuda.Stream()
+    # words made before the capture (direct call on the stream)
+    assert csum.lib.tulips_csum_batch_arena(a.data_ptr(), total, o.data_ptr(), l.data_ptr(),
+                                            None, None, None, out.data_ptr(), n, MODE_INET,
+                                            cap.cuda_stream) == 0
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        assert csum.lib.tulips_csum_batch_arena(a.data_ptr(), total, o.data_ptr(),
+                                                l.data_ptr(), None, None, None,
+                                                out.data_ptr(), n, MODE_INET,
+                                                cap.cuda_stream) == 0
+    for rnd in range(3):
+        o.copy_(bad_o)
+        g.replay()
+        torch.cuda.synchronize()
+        o.copy_(good_o)
+        for _ in range(2):
+            out.fill_(0)
+            g.replay()
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), exp,
+                                          err_msg=f"round {rnd}")
+    del g
+    csum.release_stream(cap.cuda_stream)
+
+
+@pytest.mark.gpu
 def test_zero_frames_zero_the_counters():
     import torch
     from tulips_amd import csum

@@ -184,31 +184,13 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
 {
   switch (kind) {
     case TULIPS_CSUM_KIND_SUBGROUP:
-      return spw == 1 && (((group == 16 || group == 32 || group == 64) &&
+      return spw == 1 && (((group == 16 || group == 32) &&
                            (unroll == 2 || unroll == 4 || unroll == 8)) ||
-                          (group == 16 && unroll == 6) || (group == 32 && unroll == 3) ||
-                          (group == 64 && (unroll == 9 || unroll == 12)));
-    case TULIPS_CSUM_KIND_HYBRID:
-      return variable &&
-             ((group == 8 && unroll == 4 && (spw == 1 || spw == 2 || spw == 4)) ||
-              (group == 8 && unroll == 8 && spw == 1) ||
-              (group == 16 && unroll == 2 && (spw == 1 || spw == 2 || spw == 4)) ||
-              (group == 16 && unroll == 4 && (spw == 1 || spw == 2)) ||
-              (group == 16 && unroll == 8 && spw == 1) ||
-              (group == 32 && unroll == 4 && spw == 1));
-    case TULIPS_CSUM_KIND_BALANCED:
-      return variable && (group == 8 || group == 0) &&
-             (unroll == 2 || unroll == 4 || unroll == 6) && (spw == 1 || spw == 2);
+                          (group == 64 && (unroll == 4 || unroll == 8 || unroll == 12)));
     case TULIPS_CSUM_KIND_PACKED:
-      if (spw == 4) { // lane-parallel cursors: up to 32 segments, 2 or 4 windows
-        return variable && (group == 4 || group == 8 || group == 16 || group == 32) &&
-               (unroll == 2 || unroll == 4);
-      }
-      return variable && (spw == 1 || spw == 2 || spw == 3) &&
-             (((group == 4 || group == 6 || group == 12) && unroll == 4) ||
-              ((group == 8) && (unroll == 2 || unroll == 4)) ||
-              ((group == 16) && (unroll == 2 || unroll == 4 || unroll == 8)) ||
-              ((group == 32 || group == 64) && (unroll == 4 || unroll == 8)));
+      // double-buffered windows only (sps 2)
+      return variable && spw == 2 && (group == 8 || group == 16) &&
+             (unroll == 2 || unroll == 4);
     default:
       return false;
   }
@@ -341,8 +323,8 @@ batch_var(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
 }
 
 // In-order arena batches (KIND_SPAN, csum_kernels.hip): the tuning's kind
-// must be DEFAULT or SPAN; unroll = chunks per lane, group = 0/6 split form,
-// 1/2 halo rows, 3 no halo, 4/5 boundary-slot form (include/tulips_csum_util.h).
+// must be DEFAULT or SPAN; unroll = chunks per lane (4 KiB of arena per
+// workgroup each), group 0 (or 7, the same form; include/tulips_csum_util.h).
 int
 batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
             const uint16_t* lengths, const uint16_t* seeds, const uint32_t* src,
@@ -377,9 +359,6 @@ batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
   const int32_t nt = (tuning && tuning->nontemporal >= 0) ? tuning->nontemporal : 1;
   a.nontemporal = (nt & 1) != 0;
   a.nt_store = (nt & 2) != 0;
-  if (a.unroll < 2 || a.unroll > 12) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
   return status_of(
     launch_span(base, arena, offsets, lengths, a, static_cast<hipStream_t>(stream)));
 }

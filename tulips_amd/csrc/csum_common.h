@@ -99,9 +99,6 @@ TCS_HD uint32_t finish(uint32_t le_partial, bool start_odd, uint32_t mode,
 }
 
 #if defined(__HIPCC__)
-#ifndef TULIPS_XCD_CLUSTER
-#define TULIPS_XCD_CLUSTER 8
-#endif
 // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
 // one; MI355X_MICROARCH.md, "Workgroup dispatch, XCD placement"), each with
 // its own L2. Consecutive blocks take consecutive segments, and segments
@@ -124,7 +121,7 @@ __device__ __forceinline__ uint32_t xcd_block_c(uint32_t b, uint32_t nb)
 
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
 {
-  return xcd_block_c<TULIPS_XCD_CLUSTER>(b, nb);
+  return xcd_block_c<8>(b, nb);
 }
 #endif
 

@@ -243,12 +243,7 @@ store_field(uintptr_t a, uint32_t v)
   typedef __attribute__((address_space(1))) uint8_t* gbyte_wptr;
   typedef __attribute__((address_space(1))) uint16_t* gshort_wptr;
   if ((a & 1) == 0) {
-#if defined(TULIPS_GEN_STORE) && TULIPS_GEN_STORE == 4
-    // diagnostic build: streaming (nt) field stores
-    __builtin_nontemporal_store(uint16_t(v), reinterpret_cast<gshort_wptr>(a));
-#else
     *reinterpret_cast<gshort_wptr>(a) = uint16_t(v);
-#endif
   } else {
     reinterpret_cast<gbyte_wptr>(a)[0] = uint8_t(v & 0xff);
     reinterpret_cast<gbyte_wptr>(a)[1] = uint8_t(v >> 8);
@@ -289,13 +284,7 @@ load_frame(uintptr_t fa, uint32_t flen, int lane, FrameChunks<G, U>& fc)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int cc = min(lane + u * G, lim);
-#if defined(TULIPS_GEN_STORE) && TULIPS_GEN_STORE == 3
-    // diagnostic build: the header's slot loaded temporal (kept in L2 for
-    // the field stores)
-    fc.v[u] = (NT && u > 0) ? __builtin_nontemporal_load(p + cc) : p[cc];
-#else
     fc.v[u] = NT ? __builtin_nontemporal_load(p + cc) : p[cc];
-#endif
   }
 }
 

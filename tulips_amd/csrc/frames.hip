@@ -58,22 +58,14 @@ using namespace frame;
 // the best of tools/probe_frames.py's sweep on 1514 B frames
 // (profiles/probe_frames_r01.json).
 // Minimum waves per SIMD the register allocator must leave room for
-// (0 = no bound; diagnostic A/B builds override them). Generation: 94 -> 80
-// VGPRs, 5 -> 6 waves/SIMD, no spill; 3 alternations on one box
-// (profiles/ab_r01.txt): 21.2-22.0 -> 20.8-21.4 us serial, 19.4-19.7 ->
-// 18.7-19.0 us on 4 branches. Validation at 7 waves spills 12 B and is slower.
-#ifndef TULIPS_FRAME_VAL_WAVES
-#define TULIPS_FRAME_VAL_WAVES 0
-#endif
-#ifndef TULIPS_FRAME_GEN_WAVES
-#define TULIPS_FRAME_GEN_WAVES 6
-#endif
-#ifndef TULIPS_GEN_STORE
-#define TULIPS_GEN_STORE 0
-#endif
+// (0 = no bound). Generation: 94 -> 80 VGPRs, 5 -> 6 waves/SIMD, no spill;
+// 3 alternations on one box (profiles/ab_r01.txt): 21.2-22.0 -> 20.8-21.4 us
+// serial, 19.4-19.7 -> 18.7-19.0 us on 4 branches. Validation at 7 waves
+// spills 12 B and is slower.
+constexpr int FRAME_VAL_WAVES = 0, FRAME_GEN_WAVES = 6;
 
 template<bool GENERATE, int FG, int FU, bool NT>
-__global__ __launch_bounds__(1024, GENERATE ? TULIPS_FRAME_GEN_WAVES : TULIPS_FRAME_VAL_WAVES) void
+__global__ __launch_bounds__(1024, GENERATE ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
 frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ shards,
@@ -118,71 +110,6 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
     const uint32_t l4_part = sub_sum<FG>(fold64(
       do_l4 ? range_sum<FG, FU, NT>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen))
             : 0));
-#if TULIPS_GEN_STORE == 1 || TULIPS_GEN_STORE == 2
-    if (GENERATE) {
-      // diagnostic builds (tools/probe_genstore.py): the fields written back
-      // inside whole 16-byte chunks (1) or the frame's whole first 64-byte
-      // line (2) by the lanes that hold those chunks
-      uint32_t ipv = 0, tcv = 0;
-      if (h.ipv4) {
-        const uint32_t p =
-          fold32(ip_part) + (0xffffu - field_contrib(fa + 24, h.ipck0, h.ipck1));
-        ipv = ~finish(p, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20) & 0xffffu;
-      }
-      if (do_l4) {
-        const uint32_t p =
-          fold32(l4_part) + (0xffffu - field_contrib(fa + 50, h.tcpck0, h.tcpck1));
-        tcv = ~finish(p, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst, h.tcplen) &
-              0xffffu;
-      }
-      u32x4 c = fc.v[0];
-      bool touched = false;
-      auto patch = [&](int pos, uint32_t byte) {
-        if ((pos >> 4) == lane) {
-          const int q = pos & 15, dw = q >> 2, sh = 8 * (q & 3);
-          const uint32_t m = ~(0xffu << sh), bv = (byte & 0xffu) << sh;
-          if (dw == 0) c.x = (c.x & m) | bv;
-          else if (dw == 1) c.y = (c.y & m) | bv;
-          else if (dw == 2) c.z = (c.z & m) | bv;
-          else c.w = (c.w & m) | bv;
-          touched = true;
-        }
-      };
-      if (h.ipv4) {
-        patch(h0 + 24, ipv);
-        patch(h0 + 25, ipv >> 8);
-      }
-      if (do_l4) {
-        patch(h0 + 50, tcv);
-        patch(h0 + 51, tcv >> 8);
-      }
-      const bool inside = lane * 16 >= h0 && lane * 16 + 16 <= h0 + int(flen);
-      const bool line = TULIPS_GEN_STORE == 2 && h0 == 0 && (fa & 63) == 0 && flen >= 64 &&
-                        lane < 4 && (h.ipv4 || do_l4);
-      typedef __attribute__((address_space(1))) u32x4* gchunk_wptr;
-      if ((touched && inside) || line) {
-        *reinterpret_cast<gchunk_wptr>(fc.a0 + 16u * lane) = c;
-      } else if (touched) {
-        // the chunk holds bytes past the frame: byte stores
-        typedef __attribute__((address_space(1))) uint8_t* gbyte_wptr;
-        if (h.ipv4 && ((h0 + 24) >> 4) == lane) {
-          store_field(fa + 24, ipv);
-        }
-        if (do_l4 && ((h0 + 50) >> 4) == lane) {
-          store_field(fa + 50, tcv);
-        }
-        (void)sizeof(gbyte_wptr);
-      }
-      if (lane == 0) {
-        if (fields) {
-          fields[f] = (h.ipv4 ? ipv : 0u) | ((do_l4 ? tcv : 0u) << 16);
-        }
-        if (flags) {
-          flags[f] = uint8_t(frame_flags(h, h.ipv4, do_l4));
-        }
-      }
-    } else
-#endif
     if (lane == 0) {
       if (GENERATE) {
         uint32_t written = 0;

@@ -181,22 +181,15 @@ load_chunk(uintptr_t q)
   return *reinterpret_cast<gchunk_ptr>(q);
 }
 
-#ifndef TULIPS_SEG_NT_STORE
-#define TULIPS_SEG_NT_STORE 1
-#endif
 // Output chunks are written once and read next by the NIC, not by this GPU:
 // nontemporal stores stream them out instead of leaving ~68 MB per call dirty
 // in L2 for the kernel boundary to write back (per call 41.0 -> 31.5 us in
 // bench.py's serial chain, 30.0 -> 23.4 us on 4 branches; the kernel's own
-// duration is unchanged). TULIPS_SEG_NT_STORE=0 builds the plain stores.
+// duration is unchanged).
 __device__ __forceinline__ void
 store_chunk(uintptr_t a, u32x4 v)
 {
-  if constexpr (TULIPS_SEG_NT_STORE) {
-    __builtin_nontemporal_store(v, reinterpret_cast<gchunk_wptr>(a));
-  } else {
-    *reinterpret_cast<gchunk_wptr>(a) = v;
-  }
+  __builtin_nontemporal_store(v, reinterpret_cast<gchunk_wptr>(a));
 }
 
 // Bytes x .. x+15 of a source: two consecutive aligned chunks a, b and the

@@ -50,14 +50,14 @@ struct StreamState
   void* seg_desc = nullptr; // 16 B per input frame
   uint64_t seg_ndesc = 0;
 
-  // SPAN split-form words (csum_kernels.hip csum_span3_kernel): one 64-bit
+  // SPAN split-form words (csum_kernels.hip csum_span_kernel): one 64-bit
   // word per arena range, zero again after every launch of a batch that
-  // keeps the arena contract, and tagged with the call's epoch (24 bits) so
+  // keeps the arena contract, and tagged with the launch's dispatch id so
   // that residue of one that does not is never added to. The calls one
   // capture records on this stream run in order in the graph, so they share
-  // one array (a spare, or made in relaxed capture mode) and one epoch; the
-  // array is owned by the graph from then on
-  uint32_t span_epoch = 0;
+  // one array (a spare, or made in relaxed capture mode), owned by the graph
+  // from then on and salted apart from other arrays
+  uint32_t span_salt = 0;
   uint64_t* span_slots = nullptr;
   uint64_t span_nslots = 0;
   std::vector<uint64_t*> span_spare;
@@ -66,7 +66,7 @@ struct StreamState
   {
     uint64_t* words;
     uint64_t size;
-    uint32_t epoch;
+    uint32_t salt;
   };
   std::map<unsigned long long, Capture> span_capture;
 };
@@ -87,11 +87,11 @@ bool stream_capturing(hipStream_t stream);
 hipError_t call_shards(StreamState& s, bool capturing, uint32_t** out);
 
 // The split-form span words for one call on `s` (caller holds s.call): at
-// least `need` words and the call's epoch; inside a capture an array the
-// graph keeps. hipErrorStreamCaptureUnsupported when a capture's array
-// cannot be had.
+// least `need` words (their count in *nslots) and the array's tag salt;
+// inside a capture an array the graph keeps.
+// hipErrorStreamCaptureUnsupported when a capture's array cannot be had.
 hipError_t span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out,
-                      uint32_t* epoch);
+                      uint64_t* nslots, uint32_t* salt);
 
 // After a failed launch in a direct counting call: the shards may hold
 // partial sums, so the stream gets fresh zeroed ones on its next call.

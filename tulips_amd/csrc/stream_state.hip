@@ -185,18 +185,9 @@ zeroed_words(int device, uint64_t words, bool capturing, int count, std::vector<
   return hipSuccess;
 }
 
-uint32_t
-next_epoch(StreamState& s)
-{
-  s.span_epoch = (s.span_epoch + 1) & 0xffffffu;
-  if (s.span_epoch == 0) {
-    s.span_epoch = 1;
-  }
-  return s.span_epoch;
-}
-
 hipError_t
-span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint32_t* epoch)
+span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64_t* nslots,
+           uint32_t* salt)
 {
   if (!capturing) {
     if (need > s.span_nslots) {
@@ -219,7 +210,8 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint32
       s.span_spare.assign(made.begin() + 1, made.end());
     }
     *out = s.span_slots;
-    *epoch = next_epoch(s);
+    *nslots = s.span_nslots;
+    *salt = 0;
     return hipSuccess;
   }
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -228,10 +220,15 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint32
     (void)hipGetLastError();
     return hipErrorStreamCaptureUnsupported;
   }
+  // only the capture in progress on this stream can add calls to its array
+  for (auto it = s.span_capture.begin(); it != s.span_capture.end();) {
+    it = it->first == id ? std::next(it) : s.span_capture.erase(it);
+  }
   auto it = s.span_capture.find(id);
   if (it != s.span_capture.end() && it->second.size >= need) {
     *out = it->second.words;
-    *epoch = it->second.epoch;
+    *nslots = it->second.size;
+    *salt = it->second.salt;
     return hipSuccess;
   }
   uint64_t* p = nullptr;
@@ -250,10 +247,14 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint32
     p = made[0];
   }
   s.span_owned.push_back(p);
-  const uint32_t ep = next_epoch(s);
-  s.span_capture[id] = StreamState::Capture{ p, size, ep };
+  // a graph may be replayed on other streams (other hardware queues, whose
+  // dispatch ids overlap this one's): a salt per captured array keeps such
+  // replays' tags apart
+  s.span_salt = s.span_salt * 0x9E3779B1u + 0x7F4A7C15u;
+  s.span_capture[id] = StreamState::Capture{ p, size, s.span_salt };
   *out = p;
-  *epoch = ep;
+  *nslots = size;
+  *salt = s.span_salt;
   return hipSuccess;
 }
 

@@ -58,19 +58,19 @@ def _check(rc: int, what: str) -> None:
     raise CsumError(rc, f"{what} [{detail}]" if detail else what)
 
 
-KIND_DEFAULT, KIND_SUBGROUP, KIND_HYBRID, KIND_PACKED, KIND_BALANCED = 0, 1, 2, 3, 4
+KIND_DEFAULT, KIND_SUBGROUP, KIND_PACKED = 0, 1, 3
 KIND_SPAN = 5
 
 
 class Tuning(C.Structure):
     """tulips_csum_tuning (include/tulips_csum_util.h).
 
-    kind SUBGROUP: `group` lanes (16/32/64) per segment; HYBRID (variable
-    only): `group`-lane subgroups (8/16/32), `sps` short segments in flight
-    per subgroup, whole wave for long segments; PACKED (variable only): one
-    wave per `group` segments (4..64), their chunks packed end to end,
-    `unroll` 64-chunk windows in flight. A positive `group` with kind left at
-    DEFAULT means SUBGROUP.
+    kind SUBGROUP: `group` lanes (16/32/64) per segment, `unroll` chunks per
+    lane in flight; PACKED (variable only): one wave per `group` segments
+    (8/16), their chunks packed end to end, `unroll` 64-chunk windows per
+    double-buffered batch; SPAN (in-order arenas only): `unroll` 4..8 chunks
+    per lane (4 KiB of arena per workgroup each). A positive `group` with
+    kind left at DEFAULT means SUBGROUP.
     """
     _fields_ = [("kind", C.c_int32), ("group", C.c_int32), ("unroll", C.c_int32),
                 ("nontemporal", C.c_int32), ("max_blocks", C.c_uint32),
