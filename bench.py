@@ -886,6 +886,31 @@ def frame_extras(torch, csum, dev, timer):
         alg, t, kernel="frame_kernel<GENERATE, 16 lanes x 6 chunks per frame>",
         workload="65,536 x 1514 B TCP frames per launch, 2 KiB slots, 8 bursts rotated",
         pipeline=pipe_entry(alg, tp), traffic=read_traffic("frames_generate_F1514"))
+    # compact-field generation: the same two values per frame, returned as
+    # one u32 instead of patched in place (frames only read); algorithmic
+    # bytes = the frames read + 4 B written per frame. Parity: the values
+    # equal the fields the in-place generation wrote (bytes 24-25, 50-51)
+    fields = torch.empty(nb * nf, dtype=torch.int32, device=dev)
+    gfl = lib.tulips_csum_generate_fields
+
+    def ffld(i, st):
+        b = i % nb
+        gfl(ar.data_ptr() + b * burst, offs.data_ptr(), lens.data_ptr(), nf,
+            fields.data_ptr() + b * nf * 4, None, st)
+    for i in range(nb):
+        ffld(i, torch.cuda.current_stream().cuda_stream)
+    t = timer(ffld, 64)
+    tp = timer(ffld, 64, branches=PIPE)
+    fv = v.view(nb * nf, slot)
+    want = (fv[:, 24].int() | (fv[:, 25].int() << 8) | (fv[:, 50].int() << 16) |
+            (fv[:, 51].int() << 24))
+    ok = bool((fields == want).all().item())
+    ex["frames_generate_fields_F1514"] = rate_entry(
+        alg + 4 * nf, t, kernel="frame_kernel<FIELDS, 16 lanes x 6 chunks per frame>",
+        workload="same frames: tulips_csum_generate_fields, one u32 per frame out",
+        pipeline=pipe_entry(alg + 4 * nf, tp), parity="ok" if ok else "MISMATCH",
+        traffic=read_traffic("frames_generate_fields_F1514"))
+    del fields, fv, want
     t = timer(fval, 64)
     tp = timer(fval, 64, branches=PIPE)
     ok = bool((flags == 0x0F).all().item())

@@ -277,6 +277,22 @@ int tulips_csum_generate_frames(uint8_t* base, const uint64_t* offsets,
                                 uint8_t* flags, void* stream);
 
 /*
+ * Compact-field generation: the two values tulips_csum_generate_frames would
+ * write, returned instead of patched into the frames (which are only read):
+ * fields[i] = IPv4 header checksum field (low 16 bits) | TCP checksum field
+ * (high 16 bits), each as the uint16 a little-endian load of the header word
+ * gives (so `*(uint16_t*)(frame + 24) = fields[i] & 0xffff` stores it), 0
+ * where flags[i] (may be NULL; bits as for generate) reports nothing
+ * written. For callers that patch headers when they post the TX descriptor
+ * (src/stack/ipv4/Producer.cpp:79-82, src/stack/tcpv4/Send.cpp:441-449): 4
+ * bytes written per frame instead of one partial 64-byte line. `fields` is
+ * a device array of n uint32.
+ */
+int tulips_csum_generate_fields(const uint8_t* base, const uint64_t* offsets,
+                                const uint16_t* lengths, uint32_t n, uint32_t* fields,
+                                uint8_t* flags, void* stream);
+
+/*
  * Segmentation offload (what src/transport/ofed/Device.cpp:688-772 asks of
  * the NIC with IBV_WR_TSO; header length per stack::utils::headerLength,
  * src/stack/Utils.cpp:67-84). Frame i = in_base[in_offsets[i]..][..

@@ -328,6 +328,61 @@ def test_gpu_generate_mutated_and_jumbo(oracle):
         assert bytes(got[int(offs[i]):int(offs[i]) + len(w)]) == w, i
 
 
+def fields_of(arena, offs, lens, flags):
+    """The compact fields a generated arena carries: IPv4 field (frame bytes
+    24-25 as a little-endian u16) low, TCP field (50-51) high, 0 where the
+    flags say nothing was written."""
+    out = np.zeros(len(offs), np.uint32)
+    for i, (o, ln) in enumerate(zip(offs.astype(np.int64), lens.astype(np.int64))):
+        v = 0
+        if flags[i] & IP_OK:
+            v |= int(arena[o + 24]) | int(arena[o + 25]) << 8
+        if flags[i] & L4_OK:
+            v |= (int(arena[o + 50]) | int(arena[o + 51]) << 8) << 16
+        out[i] = v
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 1, 6, 15])
+def test_gpu_generate_fields_matches_oracle(oracle, shift):
+    """tulips_csum_generate_fields: the values orc_generate_frames writes
+    (pinned to the reference-generated frames above), the frames untouched;
+    fixture frames plus mutations, at several base alignments."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(700 + shift)
+    for arena0 in (scramble_fields(fx, rng), mutate(fx, rng, 3000)):
+        src = np.concatenate([np.zeros(shift, np.uint8), arena0])
+        offs = fx["offsets"] + np.uint64(shift)
+        exp_arena, exp_flags = oracle.generate_frames(src, offs, fx["lengths"])
+        a, o, l = _dev(src, offs.astype(np.int64), fx["lengths"].view(np.int16))
+        fields, fl = csum.generate_fields(a, o, l)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(fl.cpu().numpy(), exp_flags)
+        np.testing.assert_array_equal(fields.cpu().numpy().view(np.uint32),
+                                      fields_of(exp_arena, offs, fx["lengths"], exp_flags))
+        assert np.array_equal(a.cpu().numpy(), src)          # read only
+    good = np.nonzero(fx["expect"] == (IPV4 | IP_OK | TCP | L4_OK))[0]
+    # on the reference-built frames the fields are the reference's own bytes
+    a, o, l = _dev(fx["arena"], fx["offsets"].astype(np.int64), fx["lengths"].view(np.int16))
+    fields, fl = csum.generate_fields(a, o, l, want_flags=False)
+    torch.cuda.synchronize()
+    got = fields.cpu().numpy().view(np.uint32)
+    ref = fields_of(fx["arena"], fx["offsets"], fx["lengths"],
+                    np.full(len(fx["offsets"]), IP_OK | L4_OK, np.uint8))
+    np.testing.assert_array_equal(got[good], ref[good])
+
+
+def test_generate_fields_arguments_without_gpu():
+    from tulips_amd import csum
+    f = csum.lib.tulips_csum_generate_fields
+    assert f(None, None, None, 0, None, None, None) == 0       # n == 0: no-op
+    assert f(None, 1, 1, 4, 1, None, None) == 1
+    assert f(1, 1, 1, 4, None, None, None) == 1               # fields required
+
+
 FRAME_GEOMETRIES = [(16, 4), (16, 6), (16, 8), (8, 8), (8, 16), (32, 4), (64, 2)]
 
 

@@ -69,6 +69,12 @@ hipError_t launch_generate(uint8_t* base, const uint64_t* offs,
                            const uint16_t* lens, uint32_t n, uint8_t* flags,
                            hipStream_t stream, const FrameLaunch& fl = {},
                            uint32_t* fields = nullptr);
+// compact generation: fields[i] only (IPv4 field low 16 bits, TCP high),
+// frames not modified
+hipError_t launch_generate_fields(const uint8_t* base, const uint64_t* offs,
+                                  const uint16_t* lens, uint32_t n, uint32_t* fields,
+                                  uint8_t* flags, hipStream_t stream,
+                                  const FrameLaunch& fl = {});
 hipError_t launch_frames(const uint8_t* base, const uint64_t* offs,
                          const uint16_t* lens, uint32_t n, uint8_t* flags,
                          uint32_t* counters, hipStream_t stream,

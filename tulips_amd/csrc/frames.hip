@@ -64,13 +64,19 @@ using namespace frame;
 // spills 12 B and is slower.
 constexpr int FRAME_VAL_WAVES = 0, FRAME_GEN_WAVES = 6;
 
-template<bool GENERATE, int FG, int FU, bool NT>
-__global__ __launch_bounds__(1024, GENERATE ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
+// OP: 0 = validate (flags, counters), 1 = generate in place (the two
+// checksum fields patched into the frame; `fields` optionally gets a copy),
+// 2 = generate compact fields only (frames untouched, one u32 per frame).
+enum { OP_VALIDATE = 0, OP_GENERATE = 1, OP_FIELDS = 2 };
+
+template<int OP, int FG, int FU, bool NT>
+__global__ __launch_bounds__(1024, OP != OP_VALIDATE ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
 frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ shards,
              uint32_t* __restrict__ fields)
 {
+  constexpr bool GENERATE = OP != OP_VALIDATE;
   const int lane64 = threadIdx.x & 63;
   const int lane = lane64 & (FG - 1);
   const int sub0 = lane64 - lane; // first lane of this subgroup
@@ -117,7 +123,9 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
           const uint32_t p =
             fold32(ip_part) + (0xffffu - field_contrib(fa + 24, h.ipck0, h.ipck1));
           const uint32_t r = finish(p, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20);
-          store_field(fa + 24, ~r & 0xffffu);
+          if constexpr (OP == OP_GENERATE) {
+            store_field(fa + 24, ~r & 0xffffu);
+          }
           written = ~r & 0xffffu;
         }
         if (do_l4) {
@@ -125,12 +133,16 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
             fold32(l4_part) + (0xffffu - field_contrib(fa + 50, h.tcpck0, h.tcpck1));
           const uint32_t r =
             finish(p, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst, h.tcplen);
-          store_field(fa + 50, ~r & 0xffffu);
+          if constexpr (OP == OP_GENERATE) {
+            store_field(fa + 50, ~r & 0xffffu);
+          }
           written |= (~r & 0xffffu) << 16;
         }
         if (fields) {
-          // the two field values as stored (little-endian u16s) for a host
-          // copy of the frames (tulips_csum_generate_frames_host)
+          // the two field values as stored (the u16s a little-endian load of
+          // the header words gives): what tulips_csum_generate_frames_host
+          // patches into the host copy, and tulips_csum_generate_fields'
+          // whole output
           fields[f] = written;
         }
         if (flags) {
@@ -204,7 +216,7 @@ frame_counters_finalize(uint32_t* __restrict__ shards, uint32_t* __restrict__ co
 
 constexpr int DEFAULT_G = 16, DEFAULT_U = 6;
 
-template<bool GENERATE, int G, int U, bool NT>
+template<int OP, int G, int U, bool NT>
 hipError_t
 launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
            uint8_t* flags, uint32_t* counters, uint32_t* fields, const FrameLaunch& fl,
@@ -218,12 +230,12 @@ launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n
     blocks = cap;
   }
   (void)hipGetLastError();
-  hipLaunchKernelGGL((frame_kernel<GENERATE, G, U, NT>), dim3(uint32_t(blocks)),
+  hipLaunchKernelGGL((frame_kernel<OP, G, U, NT>), dim3(uint32_t(blocks)),
                      dim3(block), 0, stream, base, offs, lens, n, flags, counters, fields);
   return hipGetLastError();
 }
 
-template<bool GENERATE>
+template<int OP>
 hipError_t
 dispatch(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
          uint8_t* flags, uint32_t* counters, uint32_t* fields, const FrameLaunch& fl,
@@ -233,11 +245,10 @@ dispatch(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
   const bool nt = fl.nontemporal != 0;
 #define TCS_F(G, U)                                                            \
   if (g == G && u == U) {                                                      \
-    return nt ? launch_one<GENERATE, G, U, true>(base, offs, lens, n, flags,    \
-                                                 counters, fields, fl, stream) \
-              : launch_one<GENERATE, G, U, false>(base, offs, lens, n, flags,   \
-                                                  counters, fields, fl,        \
-                                                  stream);                     \
+    return nt ? launch_one<OP, G, U, true>(base, offs, lens, n, flags, counters, \
+                                           fields, fl, stream)                 \
+              : launch_one<OP, G, U, false>(base, offs, lens, n, flags, counters,\
+                                            fields, fl, stream);               \
   }
   TCS_F(16, 4)
   TCS_F(16, 6)
@@ -284,8 +295,8 @@ launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
                     : hipSuccess;
   }
   if (!counters) {
-    return dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n, flags, nullptr,
-                           nullptr, fl, stream);
+    return dispatch<OP_VALIDATE>(const_cast<uint8_t*>(base), offs, lens, n, flags, nullptr,
+                                 nullptr, fl, stream);
   }
   std::shared_ptr<StreamState> ss;
   hipError_t e = stream_state(stream, &ss);
@@ -298,8 +309,8 @@ launch_frames(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
   if ((e = call_shards(*ss, capturing, &shards)) != hipSuccess) {
     return e;
   }
-  e = dispatch<false>(const_cast<uint8_t*>(base), offs, lens, n, flags, shards, nullptr,
-                      fl, stream);
+  e = dispatch<OP_VALIDATE>(const_cast<uint8_t*>(base), offs, lens, n, flags, shards,
+                            nullptr, fl, stream);
   if (e == hipSuccess) {
     e = launch_counters_finalize(shards, counters, 4, stream);
   }
@@ -317,7 +328,19 @@ launch_generate(uint8_t* base, const uint64_t* offs, const uint16_t* lens,
   if (n == 0) {
     return hipSuccess;
   }
-  return dispatch<true>(base, offs, lens, n, flags, nullptr, fields, fl, stream);
+  return dispatch<OP_GENERATE>(base, offs, lens, n, flags, nullptr, fields, fl, stream);
+}
+
+hipError_t
+launch_generate_fields(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
+                       uint32_t n, uint32_t* fields, uint8_t* flags, hipStream_t stream,
+                       const FrameLaunch& fl)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  return dispatch<OP_FIELDS>(const_cast<uint8_t*>(base), offs, lens, n, flags, nullptr,
+                             fields, fl, stream);
 }
 
 } // namespace tulips_amd
@@ -362,12 +385,28 @@ tulips_csum_generate_frames(uint8_t* base, const uint64_t* offsets,
 }
 
 extern "C" int
+tulips_csum_generate_fields(const uint8_t* base, const uint64_t* offsets,
+                            const uint16_t* lengths, uint32_t n, uint32_t* fields,
+                            uint8_t* flags, void* stream)
+{
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths || !fields) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  const hipError_t e = tulips_amd::launch_generate_fields(
+    base, offsets, lengths, n, fields, flags, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
+}
+
+extern "C" int
 tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
                          const uint16_t* lengths, uint32_t n, uint8_t* flags,
                          uint32_t* counters, const tulips_csum_tuning* tuning,
                          void* stream)
 {
-  if ((op != 0 && op != 1) || !tuning ||
+  if ((op != 0 && op != 1 && op != 2) || !tuning ||
       !tulips_amd::frame_geometry_ok(tuning->group, tuning->unroll,
                                      uint32_t(tuning->block < 0 ? 0 : tuning->block))) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
@@ -375,7 +414,8 @@ tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
   if (n == 0 && !(op == 0 && counters)) {
     return TULIPS_STATUS_OK;
   }
-  if (n && (!base || !offsets || !lengths || (op == 0 && !flags && !counters))) {
+  if (n && (!base || !offsets || !lengths || (op == 0 && !flags && !counters) ||
+            (op == 2 && !counters))) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   tulips_amd::FrameLaunch fl;
@@ -388,6 +428,9 @@ tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
   hipError_t e;
   if (op == 0) {
     e = tulips_amd::launch_frames(base, offsets, lengths, n, flags, counters, st, fl);
+  } else if (op == 2) {
+    // `counters` carries the n-entry fields array
+    e = tulips_amd::launch_generate_fields(base, offsets, lengths, n, counters, flags, st, fl);
   } else {
     e = tulips_amd::launch_generate(base, offsets, lengths, n, flags, st, fl);
   }

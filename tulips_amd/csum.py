@@ -135,6 +135,7 @@ _SIGNATURES = {
     "tulips_csum_host_free": (C.c_int, [_vp]),
     "tulips_csum_validate_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     "tulips_csum_generate_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp]),
+    "tulips_csum_generate_fields": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     "tulips_csum_segment_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp,
                                              C.c_uint64, C.c_uint32, _vp, _vp, _vp]),
     "tulips_csum_frames_tuned": (C.c_int, [C.c_int, _vp, _vp, _vp, C.c_uint32, _vp, _vp,
@@ -665,6 +666,27 @@ def generate_frames(arena, offsets, lengths, *, flags=None, want_flags: bool = T
                                            _addr(flags), _stream(stream)),
            "tulips_csum_generate_frames")
     return flags
+
+
+def generate_fields(arena, offsets, lengths, *, fields=None, flags=None,
+                    want_flags: bool = True, stream=None):
+    """The two checksum field values generate_frames would write, returned
+    as uint32 per frame (IPv4 field low 16 bits, TCP field high; each the
+    uint16 a little-endian load of the header word gives); the frames are
+    only read. Returns (fields, flags)."""
+    import torch
+    n = int(offsets.numel())
+    if int(lengths.numel()) != n:
+        raise ValueError("offsets/lengths size mismatch")
+    _check_sizes(n, fields=fields, flags=flags)
+    if fields is None:
+        fields = torch.empty(n, dtype=torch.int32, device=arena.device)
+    if flags is None and want_flags:
+        flags = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    _check(lib.tulips_csum_generate_fields(_addr(arena), _addr(offsets), _addr(lengths), n,
+                                           _addr(fields), _addr(flags), _stream(stream)),
+           "tulips_csum_generate_fields")
+    return fields, flags
 
 
 def segment_frames(arena, offsets, lengths, mss: int, *, stride: int = 2048,
