@@ -198,6 +198,34 @@ int tulips_csum_mctx_validate_frames_host(tulips_csum_mctx* ctx,
                                           const uint64_t* offsets,
                                           const uint16_t* lengths, uint32_t n,
                                           uint8_t* flags, uint32_t* counters);
+/*
+ * Device-resident batches over the context's devices ("data
+ * starts on GPU 0"): every array is a device pointer on the device of
+ * `stream` (the source). The batch is cut into contiguous byte-balanced
+ * pieces, a run of pieces per listed device; each other device pulls its
+ * pieces over xGMI (hipMemcpyPeerAsync on its own copy stream, ~32 MiB
+ * pieces so copies overlap its kernels), checksums them, and sends the
+ * results back into `out` (on the source device, segment order). The first
+ * listed entry on the source device computes its share in place. Ordered
+ * after the work already queued on `stream`; `stream` waits for all results
+ * before its later work (the call returns before they are done). The arena
+ * form requires an in-order arena (tulips_csum_batch_arena's contract) and
+ * blocks until its cut plan is read back (one small D2H after the stream's
+ * earlier work). Not capturable (InvalidArgument inside a stream capture).
+ * Semantics per segment as tulips_csum_batch_fixed / tulips_csum_batch_arena.
+ * tulips_csum_mctx_shard_bounds reports the segment range each device got.
+ */
+int tulips_csum_mctx_batch_fixed_device(tulips_csum_mctx* ctx, const uint8_t* base,
+                                        uint64_t stride, uint32_t length,
+                                        const uint16_t* seeds, const uint32_t* src,
+                                        const uint32_t* dst, uint16_t* out, uint32_t n,
+                                        uint32_t mode, void* stream);
+int tulips_csum_mctx_batch_arena_device(tulips_csum_mctx* ctx, const uint8_t* base,
+                                        uint64_t arena_bytes, const uint64_t* offsets,
+                                        const uint16_t* lengths, const uint16_t* seeds,
+                                        const uint32_t* src, const uint32_t* dst,
+                                        uint16_t* out, uint32_t n, uint32_t mode,
+                                        void* stream);
 /* The shard bounds (ndevices + 1 entries) of the context's last call. */
 int tulips_csum_mctx_shard_bounds(const tulips_csum_mctx* ctx, uint32_t* bounds);
 

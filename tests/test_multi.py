@@ -114,3 +114,124 @@ def test_mctx_validate_frames_and_counters(oracle):
         fl, cnt = m.validate_frames(arena, fx["offsets"], fx["lengths"], with_counters=True)
     np.testing.assert_array_equal(fl, exp)
     np.testing.assert_array_equal(cnt, counters_of(exp))
+
+
+# -- device-resident batches over several devices (tulips_csum_mctx_batch_*_device)
+def test_mctx_device_arguments_without_gpu():
+    from tulips_amd import csum
+    lib = csum.lib
+    F = 16
+    assert lib.tulips_csum_mctx_batch_fixed_device(None, F, 1500, 1500, None, None, None, F,
+                                                   4, 0, None) == 1
+    assert lib.tulips_csum_mctx_batch_arena_device(None, F, 16, F, F, None, None, None, F,
+                                                   4, 0, None) == 1
+    # n == 0 with a context is a no-op; without one it is an argument error
+    assert lib.tulips_csum_mctx_batch_fixed_device(None, None, 0, 0, None, None, None, None,
+                                                   0, 0, None) == 1
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndev", [1, 2, 4])
+def test_mctx_device_arena_zipf_digests(oracle, ndev):
+    """The golden ZIPF arena resident on GPU 0, spread over `ndev` logical
+    devices (all GPU 0 on the test box: entry 0 works in place, the others
+    pull their pieces with peer copies into their own buffers and send the
+    results home): ZIPF and ZIPF-tcp digests, byte-balanced bounds."""
+    import torch
+    from tulips_amd import csum
+    from oracle import ip4
+    g = golden()
+    lens = oracle.zipf_lengths(65536)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.astype(np.int64).sum())
+    arena = torch.empty(total + 64, dtype=torch.uint8, device="cuda:0")
+    csum.fill_splitmix(arena, total)
+    do, dl = _dev(offs.view(np.int64)), _dev(lens)
+    src = _dev(np.full(65536, ip4(10, 1, 0, 1), np.uint32))
+    dst = _dev(np.full(65536, ip4(10, 1, 0, 2), np.uint32))
+    with csum.MultiContext([0] * ndev) as m:
+        for rep in range(2):                       # buffers reused by a second call
+            out = m.batch_arena_device(arena, do, dl, arena_bytes=total)
+            torch.cuda.synchronize()
+            assert f"{oracle.fnv1a_u16(out.cpu().numpy().view(np.uint16)):016x}" == \
+                g["ZIPF"]["fnv1a64"], rep
+        b = m.bounds()
+        out = m.batch_arena_device(arena, do, dl, arena_bytes=total, src=src, dst=dst,
+                                   mode=2)
+        torch.cuda.synchronize()
+        assert f"{oracle.fnv1a_u16(out.cpu().numpy().view(np.uint16)):016x}" == \
+            g["ZIPF-tcp"]["fnv1a64"]
+    assert b[0] == 0 and b[-1] == 65536 and np.all(np.diff(b.astype(np.int64)) >= 0)
+    share = np.add.reduceat(lens.astype(np.int64), b[:-1].astype(np.int64)) if ndev > 1 else \
+        np.array([total])
+    assert np.all(np.abs(share - total / ndev) <= 2 * int(lens.max())), share
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndev", [3, 5])
+def test_mctx_device_arena_random_layouts(oracle, ndev):
+    """In-order arena with gaps, empty / tiny / 65,535-byte segments, an odd
+    base, seeds; and a later call on the same context with a smaller batch
+    (stale buffers must not leak)."""
+    import torch
+    from tulips_amd import csum
+    rng = np.random.default_rng(8800 + ndev)
+    for n in (150000, 9000):
+        lens = rng.integers(0, 3000, n).astype(np.uint16)
+        lens[rng.random(n) < 0.1] = 0
+        lens[rng.integers(0, n, 30)] = 65535
+        gaps = np.where(rng.random(n) < 0.3, rng.integers(0, 300, n), 0).astype(np.uint64)
+        ends = np.cumsum(lens.astype(np.uint64) + gaps)
+        offs = (ends - lens.astype(np.uint64)).astype(np.uint64)
+        total = int(ends[-1])
+        buf = rng.integers(0, 256, total + 67, dtype=np.uint8)
+        seeds = rng.integers(0, 65536, n, dtype=np.uint16)
+        exp = oracle.batch(buf[3:3 + total], offs, lens, seeds=seeds, mode=1, nthreads=8)
+        dbuf = _dev(buf)
+        with csum.MultiContext([0] * ndev) as m:
+            out = m.batch_arena_device(dbuf[3:], _dev(offs.view(np.int64)), _dev(lens),
+                                       arena_bytes=total, seeds=_dev(seeds), mode=1)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), exp)
+
+
+@pytest.mark.gpu
+def test_mctx_device_fixed_m8_from_gpu0(oracle):
+    """configs[4]: the whole M8x1500 batch (8,388,608 x 1500 B = 12.6 GB)
+    resident on GPU 0, spread over 8 logical devices: every shard digest and
+    the full-batch digest equal the reference's, the bounds are the shard
+    boundaries. Then F1500-tcp through 3 logical devices."""
+    import torch
+    from tulips_amd import csum
+    from oracle import ip4
+    g = golden()
+    gold = g["M8x1500"]
+    n, seg = 8 << 20, 1500
+    arena = torch.empty(n * seg + 64, dtype=torch.uint8, device="cuda:0")
+    csum.fill_splitmix(arena, n * seg)
+    with csum.MultiContext([0] * 8) as m:
+        out = m.batch_fixed_device(arena, seg, seg, n)
+        torch.cuda.synchronize()
+        b = m.bounds()
+    o = out.cpu().numpy().view(np.uint16)
+    assert list(b) == [k * (n // 8) for k in range(9)]
+    for k in range(8):
+        assert f"{oracle.fnv1a_u16(o[k * (n // 8):(k + 1) * (n // 8)]):016x}" == \
+            gold["shards"][k]["fnv1a64"], k
+    assert f"{oracle.fnv1a_u16(o):016x}" == gold["fnv1a64"]
+    del arena, out
+    bt = g["F1500-tcp"]
+    nt = bt["n"]
+    arena = torch.empty(nt * 1500 + 64, dtype=torch.uint8, device="cuda:0")
+    csum.fill_splitmix(arena, nt * 1500)
+    src = _dev(np.full(nt, ip4(10, 1, 0, 1), np.uint32))
+    dst = _dev(np.full(nt, ip4(10, 1, 0, 2), np.uint32))
+    with csum.MultiContext([0] * 3) as m:
+        out = m.batch_fixed_device(arena, 1500, 1500, nt, src=src, dst=dst, mode=2)
+        torch.cuda.synchronize()
+    assert f"{oracle.fnv1a_u16(out.cpu().numpy().view(np.uint16)):016x}" == bt["fnv1a64"]

@@ -295,6 +295,7 @@ struct SpanArgs
   uint64_t* slots; // split form: one 64-bit word per range (stream_state.h)
   uint64_t nslots; // words in `slots`
   uint32_t salt;   // xor-ed into the split words' tag (per word array)
+  uint64_t bias;   // segment i starts at base + offs[i] - bias
 };
 
 typedef const __attribute__((address_space(1))) uint64_t* gu64_ptr;

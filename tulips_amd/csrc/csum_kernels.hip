@@ -344,7 +344,7 @@ csum_span_kernel(SpanArgs p)
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
     const uint32_t i = min(G + t + 256u * r, n - 1);
-    wo[r] = offs[i];
+    wo[r] = offs[i] - p.bias;
     wl[r] = lens[i];
   }
   u32x4 v[U];
@@ -523,8 +523,8 @@ csum_span_kernel(SpanArgs p)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const uint32_t q = lane + 64u * r;
-          o0[r] = offs[min(uint64_t(L0) + uint64_t(q) * st0, uint64_t(n - 1))];
-          o1[r] = offs[min(uint64_t(L1) + uint64_t(q) * st1, uint64_t(n - 1))];
+          o0[r] = offs[min(uint64_t(L0) + uint64_t(q) * st0, uint64_t(n - 1))] - p.bias;
+          o1[r] = offs[min(uint64_t(L1) + uint64_t(q) * st1, uint64_t(n - 1))] - p.bias;
         }
         uint32_t d0 = 0, d1 = 0;
 #pragma unroll
@@ -554,7 +554,7 @@ csum_span_kernel(SpanArgs p)
   for (uint32_t s0 = L > 0 ? L - 1 : 0; s0 < H; s0 += 256u) {
     const uint32_t i = s0 + t;
     bool a = i < H;
-    const uint64_t o = a ? p.offs[i] : 0;
+    const uint64_t o = a ? p.offs[i] - p.bias : 0;
     const uint32_t l = a ? p.lens[i] : 0u;
     const uintptr_t ia = b + o, ie = min(b + o + l, aend);
     if (i < L) {
@@ -671,7 +671,7 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
     return hipSuccess;
   }
   SpanArgs sp{base, arena, offs, lens, a.seeds, a.src, a.dst, a.out, a.bad,
-              a.n, a.mode, a.nt_store ? 1u : 0u, nullptr, 0, 0};
+              a.n, a.mode, a.nt_store ? 1u : 0u, nullptr, 0, 0, a.offs_bias};
   // the stream's per-range words, held for the launch
   std::shared_ptr<StreamState> ss;
   hipError_t e = stream_state(stream, &ss);

@@ -24,7 +24,8 @@ struct LaunchArgs
   bool nt_store;         // nt (streaming) result stores
   uint32_t max_blocks;   // grid cap (0 = one subgroup per segment)
   int block;             // threads per workgroup: 256, 512, 1024 (0 = 256)
-  int spw;               // hybrid: short segments per subgroup in flight
+  int spw;               // packed: 2 = double-buffered windows
+  uint64_t offs_bias;    // span: segment i starts at base + offs[i] - offs_bias
 };
 
 // Counter shards: CNT_SHARDS zeroed 128-B lines per (device,

@@ -11,6 +11,19 @@
 // results land in the caller's array in segment order. The reference's
 // analogue is NIC multi-queue flow spreading
 // (src/transport/ena/RedirectionTable.cpp:74-98).
+//
+// Device-resident batches (tulips_csum_mctx_batch_{fixed,arena}_device,
+// SURVEY.md §8e "data starts on GPU 0"): the batch lives in the HBM of the
+// caller's stream's device. It is cut into contiguous pieces (byte-balanced;
+// for an arena the cut is found on the device by a binary search of the
+// offsets), a run of pieces per listed device. A peer pulls each piece over
+// xGMI (hipMemcpyPeerAsync on its own copy stream: the peer's DMA engines
+// read the source HBM directly), its compute stream checksums piece p while
+// piece p + 1 is in flight, and the piece's results go back to the source
+// device's `out` in segment order. The first listed entry on the source
+// device computes its pieces in place. Everything is stream-ordered after
+// the work already queued on the caller's stream, and that stream waits for
+// every result before its later work.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -24,6 +37,7 @@
 #include <vector>
 
 #include "../../include/tulips_csum.h"
+#include "csum_launch.h"
 
 namespace tulips_amd {
 int pack_threads();
@@ -103,12 +117,38 @@ private:
 
 } // namespace
 
+namespace {
+
+// Per listed device: what a device-resident call needs on that device
+// (made on first use, grown on demand).
+struct DevSlot
+{
+  int device = 0;
+  hipStream_t copy = nullptr, comp = nullptr;
+  std::vector<hipEvent_t> ev;   // per piece: copied
+  hipEvent_t done = nullptr;    // this call's work on the device finished
+  bool used = false;            // `done` recorded by an earlier call
+  uint8_t* buf = nullptr;       // the device's pieces, source layout
+  uint64_t buf_bytes = 0;
+  uint8_t* meta = nullptr;      // offsets, lengths, side inputs of its pieces
+  uint64_t meta_bytes = 0;
+  uint16_t* out = nullptr;      // its results before they go home
+  uint64_t out_n = 0;
+};
+
+} // namespace
+
 struct tulips_csum_mctx
 {
   std::vector<int> devices;
   std::vector<tulips_csum_ctx*> ctx;
   Workers* workers = nullptr;
   std::vector<uint32_t> bounds;
+  std::vector<DevSlot> slots;   // device-resident calls
+  uint64_t* plan_host = nullptr; // pinned: the arena cut plan read back
+  uint64_t* plan_dev = nullptr;  // on the last source device
+  int plan_device = -1;
+  uint32_t plan_cap = 0;
 };
 
 extern "C" {
@@ -187,6 +227,34 @@ tulips_csum_mctx_destroy(tulips_csum_mctx* m)
   for (auto* c : m->ctx) {
     tulips_csum_ctx_destroy(c);
   }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (auto& d : m->slots) {
+    (void)hipSetDevice(d.device);
+    for (hipStream_t st : { d.copy, d.comp }) {
+      if (st) {
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+      }
+    }
+    for (hipEvent_t e : d.ev) {
+      (void)hipEventDestroy(e);
+    }
+    if (d.done) {
+      (void)hipEventDestroy(d.done);
+    }
+    (void)hipFree(d.buf);
+    (void)hipFree(d.meta);
+    (void)hipFree(d.out);
+  }
+  if (m->plan_dev) {
+    (void)hipSetDevice(m->plan_device);
+    (void)hipFree(m->plan_dev);
+  }
+  if (m->plan_host) {
+    (void)hipHostFree(m->plan_host);
+  }
+  (void)hipSetDevice(prev);
   delete m;
   return TULIPS_STATUS_OK;
 }
@@ -290,6 +358,506 @@ tulips_csum_mctx_validate_frames_host(tulips_csum_mctx* m, const uint8_t* base,
     }
   }
   return rc;
+}
+
+} // extern "C"
+
+// ---------------------------------------------------------------------------
+// Device-resident batches over several devices.
+// ---------------------------------------------------------------------------
+namespace {
+
+using tulips_amd::LaunchArgs;
+
+// Piece p: segments [i0, i1) whose bytes lie in [lo, hi) of the source arena.
+struct Piece
+{
+  uint64_t i0, i1, lo, hi;
+};
+
+// Thread j: piece j of an in-order arena cut at j * arena / P (the first
+// segment starting at or after the cut opens the piece), as {i0, i1, lo, hi}.
+__global__ __launch_bounds__(64) void
+arena_plan_kernel(const uint64_t* __restrict__ offs, const uint16_t* __restrict__ lens,
+                  uint32_t n, uint64_t arena, uint32_t P, uint64_t* __restrict__ plan)
+{
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P) {
+    return;
+  }
+  auto lower = [&](uint64_t cut) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (offs[mid] < cut) {
+        lo = mid + 1;
+      } else {
+        hi = mid;
+      }
+    }
+    return lo;
+  };
+  // cuts as (arena / P) * j + (arena % P) * j / P: no 64-bit overflow
+  auto cut = [&](uint64_t k) { return (arena / P) * k + ((arena % P) * k) / P; };
+  const uint32_t i0 = j == 0 ? 0u : lower(cut(j));
+  const uint32_t i1 = j + 1 == P ? n : lower(cut(j + 1));
+  uint64_t lo = 0, hi = 0;
+  if (i1 > i0) {
+    lo = offs[i0];
+    hi = offs[i1 - 1] + lens[i1 - 1];
+    hi = hi > arena ? arena : hi;
+    lo = lo > hi ? hi : lo;
+  }
+  plan[4 * j + 0] = i0;
+  plan[4 * j + 1] = i1;
+  plan[4 * j + 2] = lo;
+  plan[4 * j + 3] = hi;
+}
+
+struct DevGuard
+{
+  int prev = 0;
+  DevGuard() { (void)hipGetDevice(&prev); }
+  ~DevGuard() { (void)hipSetDevice(prev); }
+};
+
+int
+status_of(hipError_t e)
+{
+  return e == hipSuccess             ? TULIPS_STATUS_OK
+         : e == hipErrorOutOfMemory  ? TULIPS_STATUS_NO_MORE_RESOURCES
+         : e == hipErrorInvalidValue ? TULIPS_STATUS_INVALID_ARGUMENT
+                                     : TULIPS_STATUS_HARDWARE_ERROR;
+}
+
+#define TCS_TRY(x)                                                             \
+  do {                                                                         \
+    const hipError_t e_ = (x);                                                 \
+    if (e_ != hipSuccess) {                                                    \
+      return e_;                                                               \
+    }                                                                          \
+  } while (0)
+
+// Streams, events, peer access (made once per context).
+hipError_t
+ensure_slots(tulips_csum_mctx* m)
+{
+  if (!m->slots.empty()) {
+    return hipSuccess;
+  }
+  std::vector<DevSlot> slots(m->devices.size());
+  for (size_t k = 0; k < slots.size(); ++k) {
+    DevSlot& d = slots[k];
+    d.device = m->devices[k];
+    TCS_TRY(hipSetDevice(d.device));
+    TCS_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    TCS_TRY(hipStreamCreateWithFlags(&d.comp, hipStreamNonBlocking));
+    TCS_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+    // peers read every other listed device's HBM over xGMI
+    for (int o : m->devices) {
+      int can = 0;
+      if (o != d.device && hipDeviceCanAccessPeer(&can, d.device, o) == hipSuccess && can) {
+        const hipError_t e = hipDeviceEnablePeerAccess(o, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+          return e;
+        }
+        (void)hipGetLastError();
+      }
+    }
+  }
+  m->slots = std::move(slots);
+  return hipSuccess;
+}
+
+// Grow `*p` (device memory on `dev`) to at least `bytes`; the slot's streams
+// are idle first.
+hipError_t
+grow(DevSlot& d, void** p, uint64_t* have, uint64_t bytes)
+{
+  if (bytes <= *have) {
+    return hipSuccess;
+  }
+  TCS_TRY(hipSetDevice(d.device));
+  TCS_TRY(hipStreamSynchronize(d.copy));
+  TCS_TRY(hipStreamSynchronize(d.comp));
+  (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  TCS_TRY(hipMalloc(p, bytes));
+  *have = bytes;
+  return hipSuccess;
+}
+
+hipError_t
+ensure_events(DevSlot& d, size_t n)
+{
+  TCS_TRY(hipSetDevice(d.device));
+  while (d.ev.size() < n) {
+    hipEvent_t e = nullptr;
+    TCS_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    d.ev.push_back(e);
+  }
+  return hipSuccess;
+}
+
+// What one call spreads: the source arrays and how a piece is checksummed.
+struct Job
+{
+  int src_dev;
+  const uint8_t* base;
+  bool arena;                 // else fixed stride
+  uint64_t stride;            // fixed
+  uint32_t length;            // fixed
+  uint64_t arena_bytes;       // arena
+  const uint64_t* offsets;    // arena
+  const uint16_t* lengths;    // arena
+  const uint16_t* seeds;
+  const uint32_t* src;
+  const uint32_t* dst;
+  uint16_t* out;
+  uint32_t mode;
+};
+
+// Checksum piece `pc` whose bytes [pc.lo, pc.hi) sit at `local` (the byte
+// at source offset pc.lo), its arrays at the given device pointers, results
+// to `out` (on the same device as everything else).
+hipError_t
+run_piece(const Job& J, const Piece& pc, const uint8_t* local, const uint64_t* offs,
+          const uint16_t* lens, const uint16_t* seeds, const uint32_t* src,
+          const uint32_t* dst, uint16_t* out, hipStream_t st)
+{
+  const uint32_t cnt = uint32_t(pc.i1 - pc.i0);
+  if (!J.arena) {
+    const int rc = tulips_csum_batch_fixed(local, J.stride, J.length, seeds, src, dst, out, cnt,
+                                           J.mode, st);
+    return rc == TULIPS_STATUS_OK ? hipSuccess
+           : rc == TULIPS_STATUS_INVALID_ARGUMENT ? hipErrorInvalidValue
+                                                  : hipErrorLaunchFailure;
+  }
+  LaunchArgs a{};
+  a.seeds = seeds;
+  a.src = src;
+  a.dst = dst;
+  a.out = out;
+  a.n = cnt;
+  a.mode = J.mode;
+  a.kind = 5; // TULIPS_CSUM_KIND_SPAN
+  a.unroll = 6;
+  a.group = 0;
+  a.nontemporal = true;
+  a.offs_bias = pc.lo;
+  return tulips_amd::launch_span(local, pc.hi - pc.lo, offs, lens, a, st);
+}
+
+hipError_t
+spread_device(tulips_csum_mctx* m, const Job& J, const std::vector<Piece>& pieces,
+              uint32_t per_dev, hipStream_t caller)
+{
+  const size_t nd = m->slots.size();
+  DevGuard guard;
+  TCS_TRY(hipSetDevice(J.src_dev));
+  hipEvent_t start = nullptr;
+  TCS_TRY(hipEventCreateWithFlags(&start, hipEventDisableTiming));
+  hipError_t e = hipEventRecord(start, caller);
+  // the first listed entry on the source device works in place
+  size_t home = nd;
+  for (size_t k = 0; k < nd; ++k) {
+    if (m->slots[k].device == J.src_dev) {
+      home = k;
+      break;
+    }
+  }
+  const bool mtcp = (J.mode & 0xffu) == 2u;
+  for (size_t k = 0; k < nd && e == hipSuccess; ++k) {
+    DevSlot& d = m->slots[k];
+    const size_t p0 = k * per_dev, p1 = std::min(pieces.size(), p0 + per_dev);
+    m->bounds[k] = p0 < pieces.size() ? uint32_t(pieces[p0].i0) : uint32_t(pieces.back().i1);
+    if (p0 >= p1) {
+      continue;
+    }
+    // this device's run of pieces: segments [s0, s1), bytes from A (16-aligned)
+    uint64_t s0 = pieces[p0].i0, s1 = pieces[p1 - 1].i1;
+    if (s1 <= s0) {
+      continue;
+    }
+    if (k == home) {
+      if ((e = hipSetDevice(d.device)) != hipSuccess ||
+          (e = hipStreamWaitEvent(d.comp, start, 0)) != hipSuccess) {
+        break;
+      }
+      for (size_t p = p0; p < p1 && e == hipSuccess; ++p) {
+        const Piece& pc = pieces[p];
+        if (pc.i1 > pc.i0) {
+          e = run_piece(J, pc, J.base + pc.lo, J.arena ? J.offsets + pc.i0 : nullptr,
+                        J.arena ? J.lengths + pc.i0 : nullptr,
+                        (J.seeds && !mtcp) ? J.seeds + pc.i0 : nullptr,
+                        mtcp ? J.src + pc.i0 : nullptr, mtcp ? J.dst + pc.i0 : nullptr,
+                        J.out + pc.i0, d.comp);
+        }
+      }
+      if (e == hipSuccess) {
+        e = hipEventRecord(d.done, d.comp);
+        d.used = true;
+      }
+      continue;
+    }
+    const uint64_t A = pieces[p0].lo & ~uint64_t(15);
+    uint64_t Z = A;
+    for (size_t p = p0; p < p1; ++p) {
+      Z = std::max(Z, pieces[p].hi);
+    }
+    const uint64_t nseg = s1 - s0;
+    // metadata layout: offsets (8 B), lengths (2 B), seeds (2 B), src, dst (4 B)
+    const uint64_t m_off = 0, m_len = m_off + (J.arena ? 8 * nseg : 0);
+    const uint64_t m_seed = (m_len + (J.arena ? 2 * nseg : 0) + 15) & ~uint64_t(15);
+    const bool seeded = J.seeds && !mtcp;
+    const uint64_t m_src = (m_seed + (seeded ? 2 * nseg : 0) + 15) & ~uint64_t(15);
+    const uint64_t m_dst = m_src + (mtcp ? 4 * nseg : 0);
+    const uint64_t m_end = m_dst + (mtcp ? 4 * nseg : 0) + 16;
+    if ((e = grow(d, reinterpret_cast<void**>(&d.buf), &d.buf_bytes, Z - A + 64)) != hipSuccess ||
+        (e = grow(d, reinterpret_cast<void**>(&d.meta), &d.meta_bytes, m_end)) != hipSuccess) {
+      break;
+    }
+    uint64_t out_have = d.out_n * 2;
+    if ((e = grow(d, reinterpret_cast<void**>(&d.out), &out_have, 2 * nseg + 16)) != hipSuccess ||
+        (e = ensure_events(d, p1 - p0)) != hipSuccess) {
+      break;
+    }
+    d.out_n = out_have / 2;
+    if ((e = hipSetDevice(d.device)) != hipSuccess) {
+      break;
+    }
+    // after the caller's earlier work, and after this slot's previous call
+    // stopped reading its buffers
+    if ((e = hipStreamWaitEvent(d.copy, start, 0)) != hipSuccess ||
+        (d.used && (e = hipStreamWaitEvent(d.copy, d.done, 0)) != hipSuccess)) {
+      break;
+    }
+    const uint64_t* moffs = reinterpret_cast<const uint64_t*>(d.meta + m_off);
+    const uint16_t* mlens = reinterpret_cast<const uint16_t*>(d.meta + m_len);
+    const uint16_t* mseeds = reinterpret_cast<const uint16_t*>(d.meta + m_seed);
+    const uint32_t* msrc = reinterpret_cast<const uint32_t*>(d.meta + m_src);
+    const uint32_t* mdst = reinterpret_cast<const uint32_t*>(d.meta + m_dst);
+    for (size_t p = p0; p < p1 && e == hipSuccess; ++p) {
+      const Piece& pc = pieces[p];
+      if (pc.i1 <= pc.i0) {
+        continue;
+      }
+      const uint64_t c = pc.i1 - pc.i0, r = pc.i0 - s0;
+      const uint64_t a0 = pc.lo & ~uint64_t(15);
+      auto pull = [&](const void* from, uint8_t* to, uint64_t bytes) {
+        return bytes ? hipMemcpyPeerAsync(to, d.device, from, J.src_dev, bytes, d.copy)
+                     : hipSuccess;
+      };
+      e = pull(J.base + a0, d.buf + (a0 - A), pc.hi - a0);
+      if (e == hipSuccess && J.arena) {
+        e = pull(J.offsets + pc.i0, d.meta + m_off + 8 * r, 8 * c);
+        if (e == hipSuccess) {
+          e = pull(J.lengths + pc.i0, d.meta + m_len + 2 * r, 2 * c);
+        }
+      }
+      if (e == hipSuccess && seeded) {
+        e = pull(J.seeds + pc.i0, d.meta + m_seed + 2 * r, 2 * c);
+      }
+      if (e == hipSuccess && mtcp) {
+        e = pull(J.src + pc.i0, d.meta + m_src + 4 * r, 4 * c);
+        if (e == hipSuccess) {
+          e = pull(J.dst + pc.i0, d.meta + m_dst + 4 * r, 4 * c);
+        }
+      }
+      hipEvent_t ev = d.ev[p - p0];
+      if (e == hipSuccess && (e = hipEventRecord(ev, d.copy)) == hipSuccess &&
+          (e = hipStreamWaitEvent(d.comp, ev, 0)) == hipSuccess) {
+        e = run_piece(J, pc, d.buf + (pc.lo - A), J.arena ? moffs + r : nullptr,
+                      J.arena ? mlens + r : nullptr, seeded ? mseeds + r : nullptr,
+                      mtcp ? msrc + r : nullptr, mtcp ? mdst + r : nullptr, d.out + r,
+                      d.comp);
+      }
+      if (e == hipSuccess) {
+        e = hipMemcpyPeerAsync(J.out + pc.i0, J.src_dev, d.out + r, d.device, 2 * c, d.comp);
+      }
+    }
+    if (e == hipSuccess) {
+      e = hipEventRecord(d.done, d.comp);
+      d.used = true;
+    }
+  }
+  m->bounds[nd] = pieces.empty() ? 0u : uint32_t(pieces.back().i1);
+  // the caller's stream continues once every device's results are home
+  if (e == hipSuccess && (e = hipSetDevice(J.src_dev)) == hipSuccess) {
+    for (size_t k = 0; k < nd && e == hipSuccess; ++k) {
+      if (m->slots[k].used) {
+        e = hipStreamWaitEvent(caller, m->slots[k].done, 0);
+      }
+    }
+  }
+  (void)hipEventDestroy(start);
+  return e;
+}
+
+// Pieces per device: about 32 MiB each (so copies and kernels overlap), at
+// least one, at most 64.
+uint32_t
+pieces_per_device(uint64_t bytes, size_t nd)
+{
+  const uint64_t per = bytes / (nd ? nd : 1);
+  const uint64_t c = (per + (32ull << 20) - 1) >> 25;
+  return uint32_t(std::min<uint64_t>(64, std::max<uint64_t>(1, c)));
+}
+
+int
+check_common(tulips_csum_mctx* m, void* stream, const uint16_t* out, uint32_t mode,
+             const uint32_t* src, const uint32_t* dst, int* src_dev)
+{
+  if (!m || !out) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if ((mode & ~0x1ffu) != 0 || (mode & 0xffu) > 2 || ((mode & 0xffu) == 2 && (!src || !dst))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return TULIPS_STATUS_INVALID_ARGUMENT; // the cut plan needs the host
+  }
+  hipDevice_t d = 0;
+  if (hipStreamGetDevice(st, &d) != hipSuccess) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  *src_dev = int(d);
+  return TULIPS_STATUS_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int
+tulips_csum_mctx_batch_fixed_device(tulips_csum_mctx* m, const uint8_t* base, uint64_t stride,
+                                    uint32_t length, const uint16_t* seeds,
+                                    const uint32_t* src, const uint32_t* dst, uint16_t* out,
+                                    uint32_t n, uint32_t mode, void* stream)
+{
+  if (n == 0) {
+    return m ? TULIPS_STATUS_OK : TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  int sdev = 0;
+  int rc = check_common(m, stream, out, mode, src, dst, &sdev);
+  if (rc != TULIPS_STATUS_OK) {
+    return rc;
+  }
+  if (!base || length > TULIPS_CSUM_MAX_SEGMENT) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  Job J{};
+  J.src_dev = sdev;
+  J.base = base;
+  J.stride = stride;
+  J.length = length;
+  J.seeds = seeds;
+  J.src = src;
+  J.dst = dst;
+  J.out = out;
+  J.mode = mode;
+  DevGuard guard;
+  hipError_t e = ensure_slots(m);
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  // equal segment counts = equal bytes
+  const size_t nd = m->slots.size();
+  const uint32_t C = pieces_per_device(uint64_t(n) * stride, nd);
+  const uint64_t P = uint64_t(C) * nd;
+  std::vector<Piece> pieces(P);
+  for (uint64_t p = 0; p < P; ++p) {
+    Piece& pc = pieces[p];
+    pc.i0 = uint64_t(n) * p / P;
+    pc.i1 = uint64_t(n) * (p + 1) / P;
+    pc.lo = pc.i0 * stride;
+    pc.hi = pc.i1 > pc.i0 ? (pc.i1 - 1) * stride + length : pc.lo;
+  }
+  return status_of(spread_device(m, J, pieces, C, static_cast<hipStream_t>(stream)));
+}
+
+int
+tulips_csum_mctx_batch_arena_device(tulips_csum_mctx* m, const uint8_t* base,
+                                    uint64_t arena_bytes, const uint64_t* offsets,
+                                    const uint16_t* lengths, const uint16_t* seeds,
+                                    const uint32_t* src, const uint32_t* dst, uint16_t* out,
+                                    uint32_t n, uint32_t mode, void* stream)
+{
+  if (n == 0) {
+    return m ? TULIPS_STATUS_OK : TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  int sdev = 0;
+  int rc = check_common(m, stream, out, mode, src, dst, &sdev);
+  if (rc != TULIPS_STATUS_OK) {
+    return rc;
+  }
+  if ((!base && arena_bytes) || !offsets || !lengths) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  Job J{};
+  J.src_dev = sdev;
+  J.base = base;
+  J.arena = true;
+  J.arena_bytes = arena_bytes;
+  J.offsets = offsets;
+  J.lengths = lengths;
+  J.seeds = seeds;
+  J.src = src;
+  J.dst = dst;
+  J.out = out;
+  J.mode = mode;
+  DevGuard guard;
+  hipError_t e = ensure_slots(m);
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  const size_t nd = m->slots.size();
+  const uint32_t C = pieces_per_device(arena_bytes, nd);
+  const uint32_t P = uint32_t(C * nd);
+  // the cut plan: found on the source device, read back (one small D2H)
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if ((e = hipSetDevice(sdev)) != hipSuccess) {
+    return status_of(e);
+  }
+  if (m->plan_device != sdev || m->plan_cap < P) {
+    if (m->plan_dev) {
+      DevGuard g2;
+      (void)hipSetDevice(m->plan_device);
+      (void)hipDeviceSynchronize();
+      (void)hipFree(m->plan_dev);
+      m->plan_dev = nullptr;
+    }
+    if (m->plan_host) {
+      (void)hipHostFree(m->plan_host);
+      m->plan_host = nullptr;
+    }
+    m->plan_cap = 0;
+    if ((e = hipMalloc(&m->plan_dev, 32ull * P)) != hipSuccess ||
+        (e = hipHostMalloc(&m->plan_host, 32ull * P, 0)) != hipSuccess) {
+      return status_of(e);
+    }
+    m->plan_device = sdev;
+    m->plan_cap = P;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(arena_plan_kernel, dim3((P + 63) / 64), dim3(64), 0, st, offsets, lengths,
+                     n, arena_bytes, P, m->plan_dev);
+  if ((e = hipGetLastError()) != hipSuccess ||
+      (e = hipMemcpyAsync(m->plan_host, m->plan_dev, 32ull * P, hipMemcpyDeviceToHost, st)) !=
+        hipSuccess ||
+      (e = hipStreamSynchronize(st)) != hipSuccess) {
+    return status_of(e);
+  }
+  std::vector<Piece> pieces(P);
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint64_t* q = m->plan_host + 4 * p;
+    pieces[p] = Piece{ q[0], q[1], q[2], q[3] };
+  }
+  return status_of(spread_device(m, J, pieces, C, st));
 }
 
 } // extern "C"

@@ -151,6 +151,12 @@ _SIGNATURES = {
     "tulips_csum_mctx_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32,
                                                         _vp, _vp]),
     "tulips_csum_mctx_shard_bounds": (C.c_int, [_vp, _vp]),
+    "tulips_csum_mctx_batch_fixed_device": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint32, _vp,
+                                                      _vp, _vp, _vp, C.c_uint32, C.c_uint32,
+                                                      _vp]),
+    "tulips_csum_mctx_batch_arena_device": (C.c_int, [_vp, _vp, C.c_uint64, _vp, _vp, _vp,
+                                                      _vp, _vp, _vp, C.c_uint32, C.c_uint32,
+                                                      _vp]),
     "tulips_csum_generate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp]),
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
@@ -590,6 +596,36 @@ class MultiContext(HostContext):
             cnt.ctypes.data if with_counters else None),
             "tulips_csum_mctx_validate_frames_host")
         return (flags, cnt) if with_counters else flags
+
+    def batch_fixed_device(self, arena, stride: int, length: int, n: int, *, seeds=None,
+                           src=None, dst=None, mode: int = RAW, out=None, stream=None,
+                           base_offset: int = 0):
+        """Device-resident fixed-stride batch on `stream`'s device, spread
+        over the context's devices (tulips_csum_mctx_batch_fixed_device)."""
+        _check_sizes(n, seeds=seeds, src=src, dst=dst, out=out)
+        if out is None:
+            out = _alloc_out(n, arena)
+        _check(lib.tulips_csum_mctx_batch_fixed_device(
+            self._h, _addr(arena) + base_offset, stride, length, _addr(seeds), _addr(src),
+            _addr(dst), _addr(out), n, mode, _stream(stream)),
+            "tulips_csum_mctx_batch_fixed_device")
+        return out
+
+    def batch_arena_device(self, arena, offsets, lengths, *, arena_bytes=None, seeds=None,
+                           src=None, dst=None, mode: int = RAW, out=None, stream=None):
+        """Device-resident in-order arena on `stream`'s device, spread over the
+        context's devices (tulips_csum_mctx_batch_arena_device)."""
+        n = int(offsets.numel())
+        if int(lengths.numel()) != n:
+            raise ValueError("offsets/lengths size mismatch")
+        _check_sizes(n, seeds=seeds, src=src, dst=dst, out=out)
+        if out is None:
+            out = _alloc_out(n, offsets)
+        _check(lib.tulips_csum_mctx_batch_arena_device(
+            self._h, _addr(arena), _arena_bytes(arena, arena_bytes), _addr(offsets),
+            _addr(lengths), _addr(seeds), _addr(src), _addr(dst), _addr(out), n, mode,
+            _stream(stream)), "tulips_csum_mctx_batch_arena_device")
+        return out
 
     def generate_frames(self, *a, **k):
         raise NotImplementedError("use HostContext for generation")
