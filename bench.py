@@ -320,6 +320,7 @@ def main():
             "streams": args.streams if graph is not None else 1,
         },
         "parity": parity,
+        "dist": dist_info(torch, dist, world, local, args),
         "shard_digests": shard_digests,
         "exchange": exchange,
         "multi_gpu": multi,
@@ -365,6 +366,24 @@ def main():
         print(json.dumps(result), flush=True)
 
 
+def dist_info(torch, dist, world, local, args):
+    """What the process group saw: its size and backend, and each rank's
+    device (index and PCI bus id), so a reader can confirm N ranks on N
+    distinct GPUs."""
+    from tulips_amd.shard import gather_strings
+    props = torch.cuda.get_device_properties(local)
+    me = {"device": local, "name": props.name,
+          "pci_bus_id": getattr(props, "pci_bus_id", None),
+          "pci_device_id": getattr(props, "pci_device_id", None)}
+    if world == 1 or not dist.is_initialized():
+        return {"world_size": 1, "backend": None, "ranks": [me]}
+    ranks = [json.loads(x) for x in gather_strings(json.dumps(me), dist)]
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+            "one_device_rehearsal": bool(args.one_device),
+            "distinct_devices": len({(r["device"], r["pci_bus_id"]) for r in ranks}),
+            "ranks": ranks}
+
+
 def exchange_sequential(torch, dist, cdev, outs, total_bytes, t_max, shard_digests, rank,
                         world):
     """The K steps' results gathered to every rank after the compute - 16
@@ -400,6 +419,8 @@ def multi_rank_legs(torch, dist, csum, dev, cdev, stream, arena, outs, rank, wor
     # (under gloo, the one-GPU rehearsal, the collectives take the same CUDA
     # tensors through host memory)
     res = {"backend": args.dist_backend}
+    res["library_scatter_from_gpu0"] = _leg(mctx_device_leg, torch, dist, csum, cdev, rank,
+                                            world, args)
     res["exchange_overlapped"] = _leg(exchange_overlapped, torch, dist, csum, cdev,
                                       stream, arena, rank, world, args, shard_digests)
     res["scatter_from_gpu0"] = _leg(scatter_leg, torch, dist, csum, dev, cdev, arena,
@@ -407,6 +428,61 @@ def multi_rank_legs(torch, dist, csum, dev, cdev, stream, arena, outs, rank, wor
     res["zipf_byte_balanced"] = _leg(zipf_sharded_leg, torch, dist, csum, dev, cdev, stream,
                                      rank, world)
     return res
+
+
+def mctx_device_leg(torch, dist, csum, cdev, rank, world, args):
+    """configs[4] with the data starting on GPU 0, through the LIBRARY
+    (tulips_csum_mctx_batch_fixed_device): rank 0 holds the
+    whole world x 1,048,576 x 1500 B batch (at N = 8: M8x1500, 12.6 GB) in
+    GPU 0's HBM and spreads it over every GPU of the node from one process -
+    each peer pulls its ~32 MiB pieces over xGMI while checksumming the
+    previous ones, results come back to GPU 0 in segment order. The other
+    ranks wait at a barrier. Timed end to end on GPU 0's stream (best of 3;
+    exchange-inclusive). Parity: every shard's digest equals the reference's
+    M8 shard digest, and at N = 8 the whole batch's digest equals M8x1500's."""
+    from tulips_amd.shard import SHARD_SEGMENTS, gather_strings
+    devs = [0] * world if args.one_device else list(range(world))
+    res = {}
+    if rank == 0:
+        n = world * SHARD_SEGMENTS
+        d0 = torch.device("cuda", 0)
+        with torch.cuda.device(d0):
+            arena = torch.empty(n * SEG + 64, dtype=torch.uint8, device=d0)
+            csum.fill_splitmix(arena, n * SEG, seed=DATA_SEED)
+            out = torch.empty(n, dtype=torch.uint16, device=d0)
+            st = torch.cuda.current_stream(d0)
+            with csum.MultiContext(devs, chunk_bytes=1 << 20) as m:
+                m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)   # buffers made
+                st.synchronize()
+                best = None
+                for _ in range(3):
+                    st.synchronize()
+                    t0 = time.perf_counter()
+                    m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)
+                    st.synchronize()
+                    t = time.perf_counter() - t0
+                    best = t if best is None else min(best, t)
+                bounds = m.bounds().tolist()
+            o = out.cpu().numpy().view(np.uint16)
+        gold = golden_digests().get("M8x1500", {})
+        shards = gold.get("shards", [])
+        ok = all(fnv1a_u16(o[k * SHARD_SEGMENTS:(k + 1) * SHARD_SEGMENTS]) ==
+                 shards[k]["fnv1a64"] for k in range(min(world, len(shards))))
+        if world == 8:
+            ok = ok and fnv1a_u16(o) == gold.get("fnv1a64")
+        nbytes = float(n) * SEG
+        res = {"entry": "tulips_csum_mctx_batch_fixed_device (one process, devices "
+                        f"{devs})",
+               "workload": f"{n:,} x 1500 B resident on GPU 0 ({nbytes / 1e9:.2f} GB)",
+               "bytes_pulled_by_peers": int(nbytes * (world - 1) / world),
+               "ms": round(best * 1e3, 3),
+               "value_exchange_inclusive_GiBps": round(nbytes / best / GIB, 2),
+               "shard_bounds": bounds,
+               "parity": "ok" if ok else "MISMATCH"}
+        del arena, out
+    dist.barrier()
+    import json as _json
+    return _json.loads(gather_strings(_json.dumps(res), dist)[0])
 
 
 def exchange_overlapped(torch, dist, csum, cdev, stream, arena, rank, world, args,

@@ -362,6 +362,27 @@ int tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
                                      const uint16_t* lengths, uint32_t n,
                                      uint8_t* flags, uint32_t* counters);
 
+/*
+ * Low-latency form of tulips_csum_validate_frames_host for small poll
+ * bursts (the reference is a latency stack: docs/topics/Test-and-
+ * Performance.md:12-15, its OFED poll drains whatever CQ batch is ready,
+ * src/transport/ofed/Device.cpp:505-545). A workgroup stays resident on the
+ * context's device and polls a doorbell in page-locked host memory; each
+ * call copies the burst's offsets/lengths into that mailbox, rings it, and
+ * spins until the flags are back. Frames in page-locked memory (one
+ * hipHostMalloc / hipHostRegister allocation, e.g. a transport's staging
+ * arena) are read in place over PCIe: no staging copy, no DMA, no launch.
+ * Frames in pageable memory are first packed into the context's 2 MiB
+ * page-locked staging. Bursts of more than TULIPS_CSUM_ZC_MAX_FRAMES frames,
+ * or pageable bursts past 2 MiB, take tulips_csum_validate_frames_host. Same
+ * flags and counters. The server leaves the GPU after 100 ms without a burst
+ * (the next call restarts it) and when the context is destroyed.
+ */
+#define TULIPS_CSUM_ZC_MAX_FRAMES 1024u
+int tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,
+                                   const uint64_t* offsets, const uint16_t* lengths,
+                                   uint32_t n, uint8_t* flags, uint32_t* counters);
+
 /* In-place checksum generation for host-resident frames (what a transport's
  * send path would offload, src/transport/ofed/Device.cpp:756): the frames
  * travel through the context's pinned pipeline, the GPU computes both fields

@@ -73,6 +73,9 @@ public:
   };
 
   static constexpr uint32_t DEFAULT_BURST = 1024;
+  // bursts up to this size take the low-latency server (measured on MI355X:
+  // DESIGN.md §5 "Latency per poll burst")
+  static constexpr uint32_t DEFAULT_LOWLAT = 256;
 
   struct Config
   {
@@ -82,6 +85,10 @@ public:
     bool tx = false;                // transmit: checksums generated on the GPU
     uint32_t tx_burst = 64;         // transmit: frames per GPU batch
     uint32_t tso = 0;               // > 0: TSO with send buffers of this size
+    // receive: bursts of at most this many frames go through the resident
+    // low-latency server (tulips_csum_validate_frames_zc: frames read in
+    // place from the pinned staging arena, no copies or launch); 0 = never
+    uint32_t lowlat = DEFAULT_LOWLAT;
   };
 
   static Ref allocate(system::Logger& log, transport::Device::Ref device,
@@ -203,6 +210,7 @@ private:
   bool m_tx;
   uint32_t m_tx_burst;
   uint32_t m_tso;
+  uint32_t m_lowlat;
   std::vector<Pending> m_pending;
   std::unordered_set<uint8_t*> m_own;        // our TSO send buffers
   std::vector<uint8_t*> m_free;              // ... not handed out

@@ -251,6 +251,82 @@ def test_gpu_host_context(oracle, pinned):
     np.testing.assert_array_equal(cnt, counters_of(exp))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [True, False])
+def test_gpu_zero_copy_bursts(oracle, pinned):
+    """tulips_csum_validate_frames_zc (the resident server, zc_mailbox.h):
+    bursts of 1..1024 fixture frames (mutated) read in place from one
+    page-locked arena, or packed from pageable memory, against the oracle;
+    the arena rewritten between rounds (no stale bytes may survive in GPU
+    caches); a burst past TULIPS_CSUM_ZC_MAX_FRAMES takes the staged path;
+    counters; an idle gap longer than the server's 100 ms timeout (it exits
+    and is restarted)."""
+    import time
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(77 if pinned else 78)
+    buf = torch.empty(len(fx["arena"]), dtype=torch.uint8)
+    if pinned:
+        buf = buf.pin_memory()
+    arena = buf.numpy()
+    n = len(fx["offsets"])
+    with csum.HostContext(0, chunk_bytes=1 << 17) as ctx:
+        for rnd in range(3):
+            arena[:] = mutate(fx, rng, 1500)
+            exp = oracle.validate_frames(arena, fx["offsets"], fx["lengths"])
+            i = 0
+            for b in (1, 1, 7, 64, 200, 1024, 1, 1025, 3):
+                if i + b > n:
+                    i = 0
+                o, ln = fx["offsets"][i:i + b], fx["lengths"][i:i + b]
+                got, cnt = ctx.validate_frames(arena, o, ln, with_counters=True,
+                                               low_latency=True)
+                np.testing.assert_array_equal(got, exp[i:i + b], err_msg=f"{rnd} {b}")
+                np.testing.assert_array_equal(cnt, counters_of(exp[i:i + b]))
+                i += b
+            if rnd == 1:
+                time.sleep(0.25)               # past the server's idle timeout
+        # every frame of the fixture, one burst each
+        for k in range(0, n, 97):
+            got = ctx.validate_frames(arena, fx["offsets"][k:k + 1], fx["lengths"][k:k + 1],
+                                      low_latency=True)
+            assert got[0] == exp[k], k
+
+
+@pytest.mark.gpu
+def test_gpu_zero_copy_two_contexts_and_destroy_while_serving(oracle):
+    """Two contexts with live servers on one GPU, calls interleaved, a staged
+    (non-zc) batch on one of them in between; destroying a context stops its
+    server (the call returns, the other keeps serving)."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    arena = torch.from_numpy(mutate(fx, np.random.default_rng(5), 900)).pin_memory().numpy()
+    exp = oracle.validate_frames(arena, fx["offsets"], fx["lengths"])
+    a = csum.HostContext(0)
+    with csum.HostContext(0) as b:
+        for k in range(0, 2000, 50):
+            sl = slice(k, k + 50)
+            for ctx in (a, b):
+                got = ctx.validate_frames(arena, fx["offsets"][sl], fx["lengths"][sl],
+                                          low_latency=True)
+                np.testing.assert_array_equal(got, exp[sl])
+            if k == 500:
+                got = a.validate_frames(arena, fx["offsets"], fx["lengths"])
+                np.testing.assert_array_equal(got, exp)
+        a.close()
+        got = b.validate_frames(arena, fx["offsets"][:64], fx["lengths"][:64], low_latency=True)
+        np.testing.assert_array_equal(got, exp[:64])
+
+
+def test_zero_copy_arguments_without_gpu():
+    from tulips_amd import csum
+    f = csum.lib.tulips_csum_validate_frames_zc
+    assert f(None, 1, 1, 1, 4, 1, None) == 1                 # no context
+    assert f(None, None, None, None, 0, None, None) == 1
+
+
 # ------------------------------------------------- send-side generation -----
 def scramble_fields(fx, rng):
     """The fixture arena with both checksum fields of every frame overwritten

@@ -369,6 +369,45 @@ def test_host_context_path(golden, oracle, pinned):
     assert f"{oracle.fnv1a_u16(out):016x}" == golden.digests()["batches"]["ZIPF-tcp"]["fnv1a64"]
 
 
+def test_host_context_span_straddling_two_pinned_blocks(oracle):
+    """a chunk's segments in two separate page-locked
+    allocations (offsets relative to the first, reaching into the second).
+    Their hull is not one allocation, so the context must pack them rather
+    than DMA the hull (which would read memory between the blocks); results
+    equal the oracle's either way. Also blocks allocated back to back, so the
+    hull is small enough for the direct path."""
+    import ctypes as C
+    lib = csum.lib
+    rng = np.random.default_rng(606)
+    size = 1 << 20
+    ptrs = []
+    try:
+        for _ in range(4):
+            p = C.c_void_p()
+            assert lib.tulips_csum_host_alloc(size, C.byref(p)) == 0
+            ptrs.append(p.value)
+        for a, b in ((ptrs[0], ptrs[1]), (ptrs[2], ptrs[3])):
+            va = np.ctypeslib.as_array((C.c_uint8 * size).from_address(a))
+            vb = np.ctypeslib.as_array((C.c_uint8 * size).from_address(b))
+            va[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            vb[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            n = 400
+            lens = rng.integers(1, 3000, n).astype(np.uint16)
+            at = rng.integers(0, size - 3000, n).astype(np.uint64)
+            in_b = np.arange(n) >= n // 2
+            offs = np.where(in_b, (at + np.uint64((b - a) % 2**64)) % np.uint64(2**64), at)
+            offs = offs.astype(np.uint64)
+            exp = np.array([oracle.checksum(0, (vb if in_b[i] else va)
+                                            [int(at[i]):int(at[i]) + int(lens[i])].tobytes())
+                            for i in range(n)], np.uint16)
+            with csum.HostContext(0) as ctx:
+                got = ctx.batch(a, offs, lens)
+            np.testing.assert_array_equal(got, exp)
+    finally:
+        for p in ptrs:
+            lib.tulips_csum_host_free(C.c_void_p(p))
+
+
 def test_empty_batch_is_noop():
     arena = torch.zeros(16, dtype=torch.uint8, device=DEV)
     offs = torch.zeros(0, dtype=torch.int64, device=DEV)

@@ -13,10 +13,13 @@
 //
 // When the caller's arena is already pinned (hipHostMalloc/hipHostRegister,
 // as a registered NIC ring would be) and a chunk's segments lie in a compact
-// span, the span is DMA'd straight from the caller's memory (no CPU copy).
+// span inside ONE page-locked allocation, the span is DMA'd straight from the
+// caller's memory (no CPU copy); any other span is packed.
 #include <hip/hip_runtime.h>
 #include <sched.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -31,6 +34,9 @@
 #include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
+#include "zc_mailbox.h"
+
+#include <chrono>
 
 using namespace tulips_amd;
 
@@ -180,16 +186,54 @@ status_of(hipError_t e)
                                   : TULIPS_STATUS_HARDWARE_ERROR;
 }
 
-bool
-is_pinned(const void* p)
+// The page-locked allocation holding `p`, as [lo, hi) (empty when `p` is not
+// in page-locked host memory): a span may be DMA'd straight from the
+// caller only when it lies inside one such allocation.
+struct PinnedRange
 {
+  uintptr_t lo = 0, hi = 0;
+  bool holds(uintptr_t a, uintptr_t b) const { return lo <= a && a <= b && b <= hi; }
+};
+
+PinnedRange
+pinned_range(const void* p)
+{
+  PinnedRange r;
   hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess || attr.type != hipMemoryTypeHost) {
     (void)hipGetLastError();
-    return false;
+    return r;
   }
-  return attr.type == hipMemoryTypeHost;
+  void* start = nullptr;
+  size_t size = 0;
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) !=
+        hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) !=
+        hipSuccess) {
+    (void)hipGetLastError();
+    return r;
+  }
+  r.lo = reinterpret_cast<uintptr_t>(start);
+  r.hi = r.lo + size;
+  return r;
 }
+
+// Low-latency receive validation (zc_mailbox.h), made on first use.
+struct ZcState
+{
+  ZcMailbox* mb = nullptr;       // page-locked, host-coherent, GPU-mapped
+  uint8_t* staging = nullptr;    // page-locked: bursts from pageable memory
+  hipStream_t stream = nullptr;  // the server's stream (its own hardware queue)
+  bool resident = false;         // resident server (else one launch per burst)
+  bool launched = false;
+  uint64_t seq = 0;
+  uintptr_t mb_dev = 0, staging_dev = 0;  // their device addresses
+  PinnedRange pin;               // last page-locked allocation seen
+  uintptr_t pin_dev = 0;         // device address of pin.lo
+  std::chrono::steady_clock::time_point last{};
+};
 
 } // namespace
 
@@ -197,6 +241,7 @@ struct tulips_csum_ctx
 {
   explicit tulips_csum_ctx(int threads) : pool(threads) {}
   int device = 0;
+  ZcState zc;
   uint64_t chunk = DEFAULT_CHUNK;
   Slot slots[NSLOTS];
   PackPool pool;
@@ -358,6 +403,26 @@ pack(PackPool& pool, Slot& s, const uint8_t* base, const uint64_t* offsets,
   });
 }
 
+// Stop the context's validation server and free its mailbox.
+void
+zc_release(ZcState& z)
+{
+  if (z.mb && z.launched) {
+    __atomic_store_n(&z.mb->stop, 1ull, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(z.stream);
+  }
+  if (z.mb) {
+    (void)hipHostFree(z.mb);
+  }
+  if (z.staging) {
+    (void)hipHostFree(z.staging);
+  }
+  if (z.stream) {
+    (void)hipStreamDestroy(z.stream);
+  }
+  z = ZcState();
+}
+
 } // namespace
 
 namespace tulips_amd {
@@ -432,6 +497,7 @@ tulips_csum_ctx_destroy(tulips_csum_ctx* ctx)
   int prev = 0;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(ctx->device);
+  zc_release(ctx->zc);
   for (auto& s : ctx->slots) {
     free_slot(s);
   }
@@ -458,7 +524,7 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
   if (e != hipSuccess) {
     return status_of(e);
   }
-  const bool pinned = is_pinned(base);
+  const PinnedRange pinned = pinned_range(base);
   int slot = 0;
   uint32_t i = 0;
   while (i < n && e == hipSuccess) {
@@ -485,7 +551,9 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
     uint64_t hbytes;
     // packed staging is in order by construction (tulips_csum_batch_arena)
     bool arena_ok = true;
-    if (pinned && hi > lo && hi - lo <= ctx->chunk && hi - lo <= 2 * bytes) {
+    const uintptr_t b0 = reinterpret_cast<uintptr_t>(base);
+    if (hi > lo && hi - lo <= ctx->chunk && hi - lo <= 2 * bytes &&
+        pinned.holds(b0 + lo, b0 + hi)) {
       arena_ok = in_order;
       // Direct DMA of the caller's span; offsets rebased onto it.
       for (uint32_t k = 0; k < cnt; ++k) {
@@ -660,6 +728,245 @@ tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
 }
 
 } // extern "C"
+
+namespace {
+
+hipError_t
+zc_setup(tulips_csum_ctx* ctx)
+{
+  ZcState& z = ctx->zc;
+  if (z.mb) {
+    return hipSuccess;
+  }
+  hipError_t e;
+  void* mb = nullptr;
+  void* st = nullptr;
+  if ((e = hipHostMalloc(&mb, sizeof(ZcMailbox), hipHostMallocCoherent | hipHostMallocMapped)) !=
+      hipSuccess) {
+    return e;
+  }
+  memset(mb, 0, sizeof(ZcMailbox));
+  z.mb = static_cast<ZcMailbox*>(mb);
+  if ((e = hipHostMalloc(&st, ZC_STAGING, hipHostMallocMapped)) != hipSuccess) {
+    zc_release(z);
+    return e;
+  }
+  z.staging = static_cast<uint8_t*>(st);
+  void* d = nullptr;
+  if ((e = hipHostGetDevicePointer(&d, mb, 0)) != hipSuccess) {
+    zc_release(z);
+    return e;
+  }
+  z.mb_dev = reinterpret_cast<uintptr_t>(d);
+  if ((e = hipHostGetDevicePointer(&d, st, 0)) != hipSuccess) {
+    zc_release(z);
+    return e;
+  }
+  z.staging_dev = reinterpret_cast<uintptr_t>(d);
+  // a CU-masked stream gets a hardware queue of its own (HIP never pools
+  // it with other streams), so the resident server cannot hold up work
+  // queued on any other stream of the process
+  int cus = 0;
+  if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device)) !=
+      hipSuccess) {
+    zc_release(z);
+    return e;
+  }
+  std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0xffffffffu);
+  const char* mode = getenv("TULIPS_ZC_MODE");
+  z.resident = mode && strcmp(mode, "resident") == 0;
+  const char* plain = getenv("TULIPS_ZC_PLAIN_STREAM");
+  if ((e = (!z.resident || (plain && plain[0] == '1'))
+             ? hipStreamCreateWithFlags(&z.stream, hipStreamNonBlocking)
+             : hipExtStreamCreateWithCUMask(&z.stream, uint32_t(mask.size()), mask.data())) !=
+      hipSuccess) {
+    z.stream = nullptr;
+    zc_release(z);
+    return e;
+  }
+  return hipSuccess;
+}
+
+// One burst through the resident server; returns NOT_APPLICABLE when the
+// burst must take the staged path (too many frames, or pageable frames
+// that do not fit the zc staging).
+constexpr int ZC_NOT_APPLICABLE = -1;
+
+int
+zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
+            const uint16_t* lengths, uint32_t n, uint8_t* flags, uint32_t* counters)
+{
+  if (n > ZC_MAX_FRAMES) {
+    return ZC_NOT_APPLICABLE;
+  }
+  uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    lo = std::min<uint64_t>(lo, offsets[k]);
+    hi = std::max<uint64_t>(hi, offsets[k] + lengths[k]);
+    bytes += lengths[k];
+  }
+  hipError_t e = zc_setup(ctx);
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  ZcState& z = ctx->zc;
+  ZcMailbox* mb = z.mb;
+  const uintptr_t b0 = reinterpret_cast<uintptr_t>(base);
+  if (hi > lo && !z.pin.holds(b0 + lo, b0 + hi)) {
+    z.pin = pinned_range(base + lo);
+    z.pin_dev = 0;
+    void* d = nullptr;
+    if (z.pin.hi > z.pin.lo &&
+        hipHostGetDevicePointer(&d, reinterpret_cast<void*>(z.pin.lo), 0) == hipSuccess) {
+      z.pin_dev = reinterpret_cast<uintptr_t>(d);
+    } else {
+      (void)hipGetLastError();
+      z.pin = PinnedRange();
+    }
+  }
+  uint64_t dbase;
+  bool staged = false;
+  if (hi <= lo || z.pin.holds(b0 + lo, b0 + hi)) {
+    // frames read in place over PCIe
+    dbase = z.pin_dev + (b0 - z.pin.lo);
+  } else if (bytes <= ZC_STAGING) {
+    uint64_t at = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+      memcpy(z.staging + at, base + offsets[k], lengths[k]);
+      mb->offs[k] = at;
+      at += lengths[k];
+    }
+    dbase = z.staging_dev;
+    staged = true;
+    lo = 0;
+    hi = at;
+  } else {
+    return ZC_NOT_APPLICABLE;
+  }
+  const uint64_t seq = ++z.seq;
+  ZcArgs args{};
+  args.base = dbase;
+  args.seq = seq;
+  args.n = n;
+  // a launch per burst carries a small burst's descriptors in its arguments
+  const bool inl = !z.resident && n <= ZC_ARG_FRAMES && hi - (hi > lo ? lo : 0) < (1ull << 32);
+  if (inl) {
+    const uint64_t l0 = hi > lo ? lo : 0;
+    args.base = dbase + l0;
+    args.inline_n = n;
+    for (uint32_t k = 0; k < n; ++k) {
+      args.off[k] = uint32_t((staged ? mb->offs[k] : offsets[k]) - l0);
+      args.len[k] = lengths[k];
+    }
+  } else {
+    if (!staged) {
+      memcpy(mb->offs, offsets, size_t(n) * 8);
+    }
+    memcpy(mb->lens, lengths, size_t(n) * 2);
+    mb->base = dbase;
+    mb->n = n;
+  }
+  __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
+  // (re)start the server: first use, or it may have timed out since the
+  // last burst (it idles out after 100 ms; checked from 50 ms on)
+  const auto now = std::chrono::steady_clock::now();
+  if (!z.resident) {
+    // one workgroup per burst: serves request `seq` and exits
+    if ((e = launch_zc_server(reinterpret_cast<ZcMailbox*>(z.mb_dev), &args, z.stream)) !=
+        hipSuccess) {
+      return status_of(e);
+    }
+    z.launched = true;
+  }
+  auto relaunch = [&]() -> hipError_t {
+    const hipError_t q = z.launched ? hipStreamQuery(z.stream) : hipSuccess;
+    if (!z.resident) {
+      return q == hipErrorNotReady ? hipSuccess : q; // an error ends the wait
+    }
+    if (q == hipErrorNotReady) {
+      return hipSuccess; // still serving
+    }
+    if (q != hipSuccess) {
+      return q;
+    }
+    const hipError_t r =
+      launch_zc_server(reinterpret_cast<ZcMailbox*>(z.mb_dev), nullptr, z.stream);
+    z.launched = r == hipSuccess;
+    return r;
+  };
+  if (z.resident && (!z.launched || now - z.last > std::chrono::milliseconds(50))) {
+    if ((e = relaunch()) != hipSuccess) {
+      return status_of(e);
+    }
+  }
+  for (uint64_t k = 1;; ++k) {
+    if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) {
+      break;
+    }
+    __builtin_ia32_pause();
+    if ((k & 4095) == 0) {
+      // the server may have exited between our check and the doorbell
+      if ((e = relaunch()) != hipSuccess) {
+        return status_of(e);
+      }
+      if (std::chrono::steady_clock::now() - now > std::chrono::seconds(2)) {
+        fprintf(stderr,
+                "tulips_csum_validate_frames_zc: no answer in 2 s (seq %llu done %llu "
+                "seen %llu beat %llu stage %llu launched %d query %d base %llx mb %p/%llx "
+                "pin %llx-%llx dev %llx b0 %llx n %u)\n",
+                (unsigned long long)seq, (unsigned long long)mb->done,
+                (unsigned long long)mb->seen, (unsigned long long)mb->beat,
+                (unsigned long long)0, int(z.launched),
+                int(hipStreamQuery(z.stream)), (unsigned long long)dbase, (void*)mb,
+                (unsigned long long)z.mb_dev, (unsigned long long)z.pin.lo,
+                (unsigned long long)z.pin.hi, (unsigned long long)z.pin_dev,
+                (unsigned long long)b0, n);
+        return TULIPS_STATUS_HARDWARE_ERROR;
+      }
+    }
+  }
+  z.last = std::chrono::steady_clock::now();
+  memcpy(flags, mb->flags, n);
+  if (counters) {
+    for (int k = 0; k < 4; ++k) {
+      counters[k] = mb->counters[k];
+    }
+  }
+  return TULIPS_STATUS_OK;
+}
+
+} // namespace
+
+extern "C" int
+tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,
+                               const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
+                               uint8_t* flags, uint32_t* counters)
+{
+  if (!ctx) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (counters) {
+    memset(counters, 0, 4 * sizeof(uint32_t));
+  }
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths || !flags) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  const hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  int rc = zc_validate(ctx, base, offsets, lengths, n, flags, counters);
+  (void)hipSetDevice(prev);
+  if (rc == ZC_NOT_APPLICABLE) {
+    rc = tulips_csum_validate_frames_host(ctx, base, offsets, lengths, n, flags, counters);
+  }
+  return rc;
+}
 
 namespace {
 

@@ -81,6 +81,13 @@ hipError_t launch_frames(const uint8_t* base, const uint64_t* offs,
                          uint32_t* counters, hipStream_t stream,
                          const FrameLaunch& fl = {});
 
+// the low-latency validation server (zc_mailbox.h) on `stream`: one
+// resident workgroup until mb->stop or an idle timeout, or (oneshot = a
+// posted request's seq) one workgroup that serves that request and exits
+struct ZcMailbox;
+struct ZcArgs;
+hipError_t launch_zc_server(ZcMailbox* mb, const ZcArgs* oneshot, hipStream_t stream);
+
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                 uint64_t byte_off, hipStream_t stream);
 hipError_t launch_stream_read(const uint8_t* p, uint64_t nbytes,

@@ -34,6 +34,7 @@
 #include "csum_launch.h"
 #include "frame_common.h"
 #include "stream_state.h"
+#include "zc_mailbox.h"
 
 namespace tulips_amd {
 namespace {
@@ -191,6 +192,136 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
   }
 }
 
+// ---- low-latency receive validation (zc_mailbox.h) --------------------------
+//
+// One workgroup of 64 16-lane subgroups serves the context's mailbox. Every
+// subgroup validates frames f, f + 64, ... of a request exactly as
+// frame_kernel<VALIDATE> does, reading them from the caller's page-locked
+// arena over PCIe; the flags and counters go back into the mailbox before
+// `done` is published with a system-scope release. RESIDENT: wave 0 polls
+// the doorbell (system-scope acquire loads) and the workgroup serves one
+// request after another until `stop` or ZC_IDLE_TICKS without one (every
+// wave leaves through the same barrier); otherwise the workgroup serves the
+// request `seq` (already posted) and exits. Control flow around the
+// barriers is wave-uniform (readfirstlane), so every wave takes every
+// barrier.
+template<bool RESIDENT>
+__global__ __launch_bounds__(1024) void
+zc_server_kernel(ZcMailbox* mb, ZcArgs args)
+{
+  const uint64_t seq0 = args.seq;
+  constexpr int FG = 16, FU = 6;
+  __shared__ uint64_t s_seq;
+  __shared__ uint32_t s_exit;
+  __shared__ uint32_t s_cnt[4];
+  const int lane64 = threadIdx.x & 63;
+  const int lane = lane64 & (FG - 1);
+  const int sub0 = lane64 - lane;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t sub = threadIdx.x / FG, nsub = blockDim.x / FG;
+  uint64_t served = RESIDENT ? __hip_atomic_load(&mb->done, __ATOMIC_ACQUIRE,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM)
+                             : 0;
+  for (;;) {
+    if (wave == 0) {
+      uint64_t seq = seq0;
+      uint32_t ex = 0;
+      if (RESIDENT) {
+        // the whole wave polls the same word (one request per load)
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t polls = 1;; ++polls) {
+          const uint64_t v =
+            __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+          seq = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(v >> 32))) << 32) |
+                __builtin_amdgcn_readfirstlane(uint32_t(v));
+          if ((polls & 1023u) == 0 && lane64 == 0) {
+            __hip_atomic_store(&mb->beat, uint64_t(polls >> 10), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&mb->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          if (seq != served) {
+            break;
+          }
+          const uint32_t stop = __builtin_amdgcn_readfirstlane(uint32_t(
+            __hip_atomic_load(&mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
+          if (stop != 0 || __builtin_amdgcn_s_memrealtime() - t0 > ZC_IDLE_TICKS) {
+            ex = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (lane64 == 0) {
+        s_seq = seq;
+        s_exit = ex;
+        s_cnt[0] = s_cnt[1] = s_cnt[2] = s_cnt[3] = 0;
+      }
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(s_exit) != 0) {
+      break;
+    }
+    // every wave sees the request and the frames as the host left them
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint64_t seq = s_seq;
+    const bool inl = !RESIDENT && args.inline_n != 0;
+    const uintptr_t base = inl ? uintptr_t(args.base)
+                               : uintptr_t(__hip_atomic_load(&mb->base, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_SYSTEM));
+    const uint32_t n =
+      inl ? min(args.inline_n, ZC_ARG_FRAMES)
+          : min(__hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                ZC_MAX_FRAMES);
+    for (uint32_t f = sub; f < n; f += nsub) {
+      const uintptr_t fa = base + (inl ? uint64_t(args.off[f]) : mb->offs[f]);
+      const uint32_t flen = inl ? uint32_t(args.len[f]) : uint32_t(mb->lens[f]);
+      FrameChunks<FG, FU> fc;
+      load_frame<FG, FU, false>(fa, flen, lane, fc);
+      const Header h = frame_header(fc, flen, sub0);
+      const int h0 = fc.h0;
+      const bool do_l4 = h.tcp && !h.trunc;
+      const uint32_t ip_part = sub_sum<FG>(
+        fold64(h.ipv4 ? range_sum<FG, FU, false>(fc, lane, h0 + 14, h0 + 34) : 0));
+      const uint32_t l4_part = sub_sum<FG>(fold64(
+        do_l4 ? range_sum<FG, FU, false>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen)) : 0));
+      if (lane == 0) {
+        const bool ip_ok = h.ipv4 && finish(ip_part, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0,
+                                            20) == 0xffffu;
+        const bool l4_ok = do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src,
+                                           h.dst, h.tcplen) == 0xffffu;
+        mb->flags[f] = uint8_t(frame_flags(h, ip_ok, l4_ok));
+        if (h.ipv4) {
+          atomicAdd(&s_cnt[0], 1u);
+          if (!ip_ok) {
+            atomicAdd(&s_cnt[1], 1u);
+          }
+        }
+        if (h.tcp) {
+          atomicAdd(&s_cnt[2], 1u);
+          if (!l4_ok) {
+            atomicAdd(&s_cnt[3], 1u);
+          }
+        }
+      }
+    }
+    // this wave's flag stores reach the host before `done` does
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int k = 0; k < 4; ++k) {
+        __hip_atomic_store(&mb->counters[k], s_cnt[k], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __hip_atomic_store(&mb->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (!RESIDENT) {
+      break;
+    }
+    served = seq;
+    __syncthreads(); // s_seq / s_cnt are rewritten by the next poll
+  }
+}
+
 // Sums the shards into the caller's counters and zeroes them for the next
 // call on this stream (atomic exchange: read and cleared where the adds
 // landed).
@@ -271,6 +402,22 @@ frame_geometry_ok(int group, int unroll, uint32_t block)
                    (g == 8 && (u == 8 || u == 16)) || (g == 32 && u == 4) ||
                    (g == 64 && u == 2);
   return geo && (block == 0 || block == 256 || block == 512 || block == 1024);
+}
+
+hipError_t
+launch_zc_server(ZcMailbox* mb, const ZcArgs* oneshot, hipStream_t stream)
+{
+  (void)hipGetLastError();
+  if (oneshot) {
+    // a burst of up to 64 frames needs 4 waves, not 16
+    const uint32_t threads =
+      oneshot->inline_n ? min(1024u, 64u * ((oneshot->inline_n + 3) / 4)) : 1024u;
+    hipLaunchKernelGGL(zc_server_kernel<false>, dim3(1), dim3(threads), 0, stream, mb,
+                       *oneshot);
+  } else {
+    hipLaunchKernelGGL(zc_server_kernel<true>, dim3(1), dim3(1024), 0, stream, mb, ZcArgs{});
+  }
+  return hipGetLastError();
 }
 
 hipError_t

@@ -158,6 +158,7 @@ _SIGNATURES = {
                                                       _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                       _vp]),
     "tulips_csum_generate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp]),
+    "tulips_csum_validate_frames_zc": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp, _vp]),
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
 }
@@ -467,8 +468,10 @@ class HostContext:
         return out
 
     def validate_frames(self, arena, offsets, lengths, *, flags=None,
-                        with_counters: bool = False):
-        """Host-resident frames -> uint8 FRAME_* flags (and the 4 counters)."""
+                        with_counters: bool = False, low_latency: bool = False):
+        """Host-resident frames -> uint8 FRAME_* flags (and the 4 counters).
+        low_latency: tulips_csum_validate_frames_zc (resident server, frames
+        read in place when page-locked)."""
         import numpy as np
         ar = arena if isinstance(arena, int) else _host(arena, np.uint8)
         base = ar if isinstance(ar, int) else ar.ptr
@@ -480,10 +483,12 @@ class HostContext:
         if flags is None:
             flags = np.empty(n, dtype=np.uint8)
         cnt = np.zeros(4, dtype=np.uint32)
-        rc = lib.tulips_csum_validate_frames_host(
-            self._h, base, off.ptr, ln.ptr, n, flags.ctypes.data,
-            cnt.ctypes.data if with_counters else None)
-        _check(rc, "tulips_csum_validate_frames_host")
+        fn = lib.tulips_csum_validate_frames_zc if low_latency else \
+            lib.tulips_csum_validate_frames_host
+        rc = fn(self._h, base, off.ptr, ln.ptr, n, flags.ctypes.data,
+                cnt.ctypes.data if with_counters else None)
+        _check(rc, "tulips_csum_validate_frames_zc" if low_latency else
+               "tulips_csum_validate_frames_host")
         return (flags, cnt) if with_counters else flags
 
     def generate_frames(self, arena, offsets, lengths):
