@@ -226,6 +226,28 @@ int tulips_csum_mctx_batch_arena_device(tulips_csum_mctx* ctx, const uint8_t* ba
                                         const uint32_t* src, const uint32_t* dst,
                                         uint16_t* out, uint32_t n, uint32_t mode,
                                         void* stream);
+/*
+ * Flow-affine receive validation ("enables flow-affine GPU
+ * sharding"), the GPU analogue of NIC RSS queues with an indirection table
+ * (src/transport/ena/RedirectionTable.cpp:74-98): every option-less
+ * IPv4/TCP frame's 4-tuple (saddr | daddr | sport | dport, as
+ * tulips_rss_toeplitz_batch takes it) is hashed with the `key_len`-byte
+ * Toeplitz key from `init` on the context's first device, and the frame is
+ * validated on device table[hash % table_len] (entries index the context's
+ * devices); frames without such a tuple go to table[0]. All frames of one
+ * flow therefore land on one device, in arrival order. `flags` (and the
+ * summed `counters`) come back in arrival order; `device_of` (host uint16[n],
+ * may be NULL) receives each frame's device index. All arrays are host
+ * arrays; blocks until done. tulips_csum_mctx_shard_bounds then reports the
+ * prefix sums of the per-device frame counts.
+ */
+int tulips_csum_mctx_validate_frames_rss_host(tulips_csum_mctx* ctx, const uint8_t* base,
+                                              const uint64_t* offsets,
+                                              const uint16_t* lengths, uint32_t n,
+                                              const uint8_t* key, size_t key_len,
+                                              uint32_t init, const uint16_t* table,
+                                              uint32_t table_len, uint8_t* flags,
+                                              uint32_t* counters, uint16_t* device_of);
 /* The shard bounds (ndevices + 1 entries) of the context's last call. */
 int tulips_csum_mctx_shard_bounds(const tulips_csum_mctx* ctx, uint32_t* bounds);
 

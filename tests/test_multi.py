@@ -4,6 +4,7 @@ csum_multi.hip). On the one-GPU test box every shard maps to device 0 —
 independent contexts and pipelines on one card — which exercises the split,
 the per-device workers and the in-order result assembly; the digests are the
 reference's (tests/golden/digests.json: ZIPF, the M8x1500 shards)."""
+import ctypes as C
 import json
 import os
 
@@ -235,3 +236,70 @@ def test_mctx_device_fixed_m8_from_gpu0(oracle):
         out = m.batch_fixed_device(arena, 1500, 1500, nt, src=src, dst=dst, mode=2)
         torch.cuda.synchronize()
     assert f"{oracle.fnv1a_u16(out.cpu().numpy().view(np.uint16)):016x}" == bt["fnv1a64"]
+
+
+# -- flow-affine validation (tulips_csum_mctx_validate_frames_rss_host) -------
+def _rss_frames(oracle, rng, fx_rss, reps=2):
+    """One well-formed TCP frame per rss.npz tuple (addresses and ports set
+    to the fixture's, checksums generated by the oracle), `reps` frames per
+    flow interleaved with each other, plus non-TCP frames."""
+    from test_frames import make_frame
+    frames, flow = [], []
+    ntup = len(fx_rss["saddr"])
+    order = np.concatenate([rng.permutation(ntup) for _ in range(reps)])
+    for j in order:
+        f = bytearray(make_frame(oracle, rng, int(rng.integers(0, 600))))
+        f[26:30] = int(fx_rss["saddr"][j]).to_bytes(4, "little")
+        f[30:34] = int(fx_rss["daddr"][j]).to_bytes(4, "little")
+        f[34:36] = int(fx_rss["sport"][j]).to_bytes(2, "big")
+        f[36:38] = int(fx_rss["dport"][j]).to_bytes(2, "big")
+        frames.append(bytes(f))
+        flow.append(int(j))
+    for _ in range(50):                                    # ARP-like, not IPv4
+        frames.append(b"\xff" * 12 + b"\x08\x06" + bytes(46))
+        flow.append(-1)
+    from test_frames import pack
+    arena, offs, lens = pack(frames, rng)
+    arena = arena.copy()
+    gen, _ = oracle.generate_frames(arena, offs, lens)     # fresh checksums
+    return gen, offs, lens, np.array(flow)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_i,init,ndev", [(0, 0, 4), (9, 0xFFFFFFFF, 3), (7, 0, 2)])
+def test_mctx_rss_flow_affine_matches_reference_hashes(oracle, key_i, init, ndev):
+    """Each frame lands on table[reference hash % len] (the reference's own
+    toeplitz over the same tuples, tests/golden/rss.npz), every frame of a
+    flow on the same device, flags identical to one device's, counters
+    summed; non-TCP frames go to table[0]."""
+    from test_rss import rss_fixture
+    from tulips_amd import csum
+    fx = rss_fixture()
+    key = fx[f"key_{key_i}"].tobytes()
+    exp_hash = fx[f"expect_{key_i}_{'init0' if init == 0 else 'initff'}"]
+    rng = np.random.default_rng(key_i * 7 + ndev)
+    arena, offs, lens, flow = _rss_frames(oracle, rng, fx)
+    table = (np.arange(128) * 7 % ndev).astype(np.uint16)
+    table[0] = ndev - 1
+    exp_flags = oracle.validate_frames(arena, offs, lens)
+    with csum.MultiContext([0] * ndev, chunk_bytes=1 << 20) as m:
+        flags, dev, cnt = m.validate_frames_rss(arena, offs, lens, key, table, init=init,
+                                                with_counters=True)
+        b = m.bounds()
+    np.testing.assert_array_equal(flags, exp_flags)
+    from test_frames import counters_of
+    np.testing.assert_array_equal(cnt, counters_of(exp_flags))
+    tcp = flow >= 0
+    want = table[exp_hash[flow[tcp]].astype(np.int64) % len(table)]
+    np.testing.assert_array_equal(dev[tcp], want)
+    assert np.all(dev[~tcp] == table[0])
+    for j in np.unique(flow[tcp])[:200]:
+        assert len(set(dev[flow == j].tolist())) == 1
+    assert list(np.diff(b)) == [int((dev == k).sum()) for k in range(ndev)]
+
+
+def test_mctx_rss_arguments_without_gpu():
+    from tulips_amd import csum
+    f = csum.lib.tulips_csum_mctx_validate_frames_rss_host
+    key = (C.c_uint8 * 40)()
+    assert f(None, 1, 1, 1, 1, key, 40, 0, 1, 1, 1, None, None) == 1

@@ -478,6 +478,56 @@ ctx_create(int device, uint64_t chunk_bytes, int threads, tulips_csum_ctx** ctx)
   return TULIPS_STATUS_OK;
 }
 
+// Toeplitz hashes (tulips_rss_toeplitz_batch) of host tuples on the
+// context's device, through slot 0's pinned staging, up to
+// MAX_SEGS_PER_CHUNK tuples per round trip. Blocks until `out` is written.
+int
+ctx_rss_hash(tulips_csum_ctx* ctx, const uint32_t* saddr, const uint32_t* daddr,
+             const uint16_t* sport, const uint16_t* dport, uint32_t n, const uint8_t* key,
+             size_t key_len, uint32_t init, uint32_t* out)
+{
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(ctx->device);
+  Slot& s = ctx->slots[0];
+  int rc = TULIPS_STATUS_OK;
+  for (uint32_t i = 0; i < n && e == hipSuccess && rc == TULIPS_STATUS_OK;
+       i += MAX_SEGS_PER_CHUNK) {
+    const uint32_t c = std::min<uint32_t>(MAX_SEGS_PER_CHUNK, n - i);
+    // the slot's previous work is retired: its pinned buffers are free
+    if ((e = hipStreamSynchronize(s.stream)) != hipSuccess) {
+      break;
+    }
+    memcpy(s.h_src, saddr + i, size_t(c) * 4);
+    memcpy(s.h_dst, daddr + i, size_t(c) * 4);
+    memcpy(s.h_seeds, sport + i, size_t(c) * 2);
+    memcpy(s.h_lens, dport + i, size_t(c) * 2);
+    if ((e = hipMemcpyAsync(s.d_src, s.h_src, size_t(c) * 4, hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_dst, s.h_dst, size_t(c) * 4, hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_seeds, s.h_seeds, size_t(c) * 2, hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_lens, s.h_lens, size_t(c) * 2, hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess) {
+      break;
+    }
+    rc = tulips_rss_toeplitz_batch(s.d_src, s.d_dst, s.d_seeds, s.d_lens, c, key, key_len,
+                                   init, s.d_fields, s.stream);
+    if (rc == TULIPS_STATUS_OK &&
+        ((e = hipMemcpyAsync(s.h_fields, s.d_fields, size_t(c) * 4, hipMemcpyDeviceToHost,
+                             s.stream)) != hipSuccess ||
+         (e = hipStreamSynchronize(s.stream)) != hipSuccess)) {
+      break;
+    }
+    if (rc == TULIPS_STATUS_OK) {
+      memcpy(out + i, s.h_fields, size_t(c) * 4);
+    }
+  }
+  (void)hipSetDevice(prev);
+  return e != hipSuccess ? status_of(e) : rc;
+}
+
 } // namespace tulips_amd
 
 extern "C" {

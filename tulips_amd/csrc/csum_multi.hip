@@ -42,6 +42,9 @@
 namespace tulips_amd {
 int pack_threads();
 int ctx_create(int device, uint64_t chunk_bytes, int threads, tulips_csum_ctx** ctx);
+int ctx_rss_hash(tulips_csum_ctx* ctx, const uint32_t* saddr, const uint32_t* daddr,
+                 const uint16_t* sport, const uint16_t* dport, uint32_t n, const uint8_t* key,
+                 size_t key_len, uint32_t init, uint32_t* out);
 }
 
 namespace {
@@ -358,6 +361,115 @@ tulips_csum_mctx_validate_frames_host(tulips_csum_mctx* m, const uint8_t* base,
     }
   }
   return rc;
+}
+
+int
+tulips_csum_mctx_validate_frames_rss_host(tulips_csum_mctx* m, const uint8_t* base,
+                                          const uint64_t* offsets, const uint16_t* lengths,
+                                          uint32_t n, const uint8_t* key, size_t key_len,
+                                          uint32_t init, const uint16_t* table,
+                                          uint32_t table_len, uint8_t* flags,
+                                          uint32_t* counters, uint16_t* device_of)
+{
+  if (!m || !key || key_len < 4 || !table || table_len == 0) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  const uint32_t nd = uint32_t(m->ctx.size());
+  for (uint32_t k = 0; k < table_len; ++k) {
+    if (table[k] >= nd) {
+      return TULIPS_STATUS_INVALID_ARGUMENT;
+    }
+  }
+  if (counters) {
+    memset(counters, 0, 4 * sizeof(uint32_t));
+  }
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths || !flags) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  // 1. the 4-tuple of every option-less IPv4/TCP frame, as the NIC's RSS
+  //    input: saddr | daddr | sport | dport (ports in host order); other
+  //    frames go where table[0] says (the reference keeps slot 0 for L2
+  //    flows, src/transport/ena/RedirectionTable.cpp:50-53)
+  std::vector<uint32_t> tup_i, sa, da, hash;
+  std::vector<uint16_t> sp, dp;
+  tup_i.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* f = base + offsets[i];
+    if (lengths[i] >= 38 && f[12] == 0x08 && f[13] == 0x00 && f[14] == 0x45 && f[23] == 6) {
+      uint32_t s4, d4;
+      memcpy(&s4, f + 26, 4);
+      memcpy(&d4, f + 30, 4);
+      tup_i.push_back(i);
+      sa.push_back(s4);
+      da.push_back(d4);
+      sp.push_back(uint16_t((f[34] << 8) | f[35]));
+      dp.push_back(uint16_t((f[36] << 8) | f[37]));
+    }
+  }
+  // 2. their Toeplitz hashes on the first device (src/stack/Utils.cpp:86-133)
+  hash.resize(tup_i.size());
+  if (!tup_i.empty()) {
+    const int rc = tulips_amd::ctx_rss_hash(m->ctx[0], sa.data(), da.data(), sp.data(),
+                                            dp.data(), uint32_t(tup_i.size()), key, key_len,
+                                            init, hash.data());
+    if (rc != TULIPS_STATUS_OK) {
+      return rc;
+    }
+  }
+  // 3. indirection table -> device (RedirectionTable.cpp:88-96: hash % size)
+  std::vector<uint16_t> dev(n, table[0]);
+  for (size_t t = 0; t < tup_i.size(); ++t) {
+    dev[tup_i[t]] = table[hash[t] % table_len];
+  }
+  // 4. each device validates its frames (arrival order kept within a
+  //    device, so a flow's frames stay in order on its device)
+  std::vector<std::vector<uint32_t>> idx(nd);
+  for (uint32_t i = 0; i < n; ++i) {
+    idx[dev[i]].push_back(i);
+  }
+  std::vector<std::vector<uint64_t>> offs(nd);
+  std::vector<std::vector<uint16_t>> lens(nd);
+  std::vector<std::vector<uint8_t>> fl(nd);
+  for (uint32_t k = 0; k < nd; ++k) {
+    offs[k].resize(idx[k].size());
+    lens[k].resize(idx[k].size());
+    fl[k].resize(idx[k].size());
+    for (size_t j = 0; j < idx[k].size(); ++j) {
+      offs[k][j] = offsets[idx[k][j]];
+      lens[k][j] = lengths[idx[k][j]];
+    }
+  }
+  std::vector<uint32_t> part(4 * nd, 0);
+  std::vector<int> st(nd, TULIPS_STATUS_OK);
+  m->workers->run([&](int k) {
+    if (!idx[k].empty()) {
+      st[k] = tulips_csum_validate_frames_host(m->ctx[k], base, offs[k].data(), lens[k].data(),
+                                               uint32_t(idx[k].size()), fl[k].data(),
+                                               counters ? part.data() + 4 * k : nullptr);
+    }
+  });
+  m->bounds[0] = 0;
+  for (uint32_t k = 0; k < nd; ++k) {
+    if (st[k] != TULIPS_STATUS_OK) {
+      return st[k];
+    }
+    m->bounds[k + 1] = m->bounds[k] + uint32_t(idx[k].size());
+    for (size_t j = 0; j < idx[k].size(); ++j) {
+      flags[idx[k][j]] = fl[k][j];
+    }
+    if (counters) {
+      for (int c = 0; c < 4; ++c) {
+        counters[c] += part[4 * k + c];
+      }
+    }
+  }
+  if (device_of) {
+    memcpy(device_of, dev.data(), size_t(n) * 2);
+  }
+  return TULIPS_STATUS_OK;
 }
 
 } // extern "C"

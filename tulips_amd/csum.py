@@ -151,6 +151,9 @@ _SIGNATURES = {
     "tulips_csum_mctx_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32,
                                                         _vp, _vp]),
     "tulips_csum_mctx_shard_bounds": (C.c_int, [_vp, _vp]),
+    "tulips_csum_mctx_validate_frames_rss_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32,
+                                                            _vp, C.c_size_t, C.c_uint32, _vp,
+                                                            C.c_uint32, _vp, _vp, _vp]),
     "tulips_csum_mctx_batch_fixed_device": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint32, _vp,
                                                       _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                       _vp]),
@@ -601,6 +604,29 @@ class MultiContext(HostContext):
             cnt.ctypes.data if with_counters else None),
             "tulips_csum_mctx_validate_frames_host")
         return (flags, cnt) if with_counters else flags
+
+    def validate_frames_rss(self, arena, offsets, lengths, key: bytes, table, *,
+                            init: int = 0, with_counters: bool = False):
+        """Flow-affine validation (tulips_csum_mctx_validate_frames_rss_host):
+        each TCP frame validated on device table[toeplitz(tuple) % len(table)].
+        Returns (flags, device_of[, counters])."""
+        import numpy as np
+        ar = arena if isinstance(arena, int) else _host(arena, np.uint8)
+        base = ar if isinstance(ar, int) else ar.ptr
+        off = _host(offsets, np.uint64)
+        ln = _host(lengths, np.uint16)
+        n = len(off.keep)
+        tb = np.ascontiguousarray(table, dtype=np.uint16)
+        kp, _keep = _buf(key)
+        flags = np.empty(n, dtype=np.uint8)
+        dev = np.empty(n, dtype=np.uint16)
+        cnt = np.zeros(4, dtype=np.uint32)
+        _check(lib.tulips_csum_mctx_validate_frames_rss_host(
+            self._h, base, off.ptr, ln.ptr, n, kp, len(key), init & 0xFFFFFFFF,
+            tb.ctypes.data, len(tb), flags.ctypes.data,
+            cnt.ctypes.data if with_counters else None, dev.ctypes.data),
+            "tulips_csum_mctx_validate_frames_rss_host")
+        return (flags, dev, cnt) if with_counters else (flags, dev)
 
     def batch_fixed_device(self, arena, stride: int, length: int, n: int, *, seeds=None,
                            src=None, dst=None, mode: int = RAW, out=None, stream=None,
