@@ -271,6 +271,22 @@ def main():
     value = total_bytes / t_max / GIB
     per_launch_s = t_local / steps_done
 
+    # the same graph replayed again, each replay timed alone (HIP events on
+    # the replay stream, max over ranks): the spread of `value` within one
+    # session (make the headline reproducible)
+    replays = []
+    if graph is not None:
+        for _ in range(7):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            ev0.record(stream)
+            graph.replay()
+            ev1.record(stream)
+            torch.cuda.synchronize()
+            tr = max_over_ranks(ev0.elapsed_time(ev1) / 1e3, dist, cdev)
+            replays.append(total_bytes / tr / GIB)
+
     # ---- parity of what was measured: shard digest vs the reference's -------
     gold = golden_digests().get("M8x1500", {})
     out_np = outs.cpu().numpy().view(np.uint16)
@@ -326,6 +342,13 @@ def main():
         "multi_gpu": multi,
         "wall_s_timed": round(t_wall, 4),
     }
+    if replays:
+        result["value_replays"] = {
+            "what": "the timed graph (all K steps) replayed 7 more times in this session, "
+                    "each replay timed on its own; GiB/s",
+            "median": round(float(np.median(replays)), 2),
+            "min": round(min(replays), 2), "max": round(max(replays), 2),
+            "all": [round(x, 1) for x in replays]}
 
     tun = csum.default_tuning(SEG)
     # Roofline of the kernel itself: bytes per launch / one launch's duration,
@@ -730,6 +753,14 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
         f9(i, sh)
     t = timer(f9, 40)
     tp = timer(f9, 40, branches=PIPE)
+    # the F9000 kernel's own read pattern without the arithmetic, over the
+    # same two rotated batches: the ceiling that kernel is held against
+    sink9 = torch.zeros(4, dtype=torch.int32, device=dev)
+
+    def f9r(i, st):
+        b = i % 2
+        lib.tulips_csum_stream_read_tiles(a9.data_ptr() + b * b9, L9, NSEG, sink9.data_ptr(), st)
+    t9r = timer(f9r, 40)
     gold = golden_digests()
     o = o9[:NSEG].cpu().numpy().view(np.uint16)
     tun = csum.default_tuning(L9)
@@ -739,6 +770,11 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                    "pipeline": pipe_entry(b9, tp),
                    "geometry": f"G={tun.group},U={tun.unroll}",
                    "traffic": read_traffic("F9000"),
+                   "read_same_bytes": {
+                       "what": "tulips_csum_stream_read_tiles: the kernel's loads (one wave per "
+                               "9000 B tile, 64 lanes x 12 clamped loads), no arithmetic",
+                       "avg_launch_us": round(t9r * 1e6, 2),
+                       "frac_of_peak": round(b9 / t9r / 1e9 / HBM_PEAK_GBS, 4)},
                    "parity": "ok" if fnv1a_u16(o) == gold.get("F9000", {}).get("fnv1a64")
                    else "MISMATCH"}
     del a9, o9
@@ -867,7 +903,7 @@ def mctx_leg(torch, csum, pinned, hoffs, hlens, batch_bytes, gold):
             else "MISMATCH"}
 
 
-BURSTS = (1, 64, 1024)
+BURSTS = (1, 8, 64, 256, 1024)
 
 
 def burst_frames(nf):
@@ -889,30 +925,44 @@ def burst_frames(nf):
 
 
 def burst_latency(torch, csum):
-    """What one receive poll burst costs on the GPU path the gpucsum decorator
-    takes (tulips_csum_validate_frames_host: pinned staging, H2D, one launch,
-    D2H of the flags), per burst size, median of repeated calls. The reference
-    verifies each frame on the CPU as it arrives (ipv4/Processor.cpp:94-103,
-    tcpv4/Processor.cpp:121-131); its cost for the same bursts is in
-    cpu_baseline.burst_latency."""
+    """What one receive poll burst costs on the two GPU paths the gpucsum
+    decorator takes, timed in C around each library call
+    (tulips_csum_time_validate: no interpreter in the loop), frames in a
+    page-locked 2 KiB-slot arena as the decorator stages them:
+      staged: tulips_csum_validate_frames_host (pinned DMA, launch, D2H);
+      zero_copy: tulips_csum_validate_frames_zc (the kernel reads the frames
+      in place over PCIe, descriptors in its arguments, flags written to a
+      page-locked mailbox the host spins on); gpu_service_us is the kernel's
+      own request-to-flags time from its realtime clock.
+    The reference verifies each frame on the CPU as it arrives
+    (ipv4/Processor.cpp:94-103, tcpv4/Processor.cpp:121-131); its C-timed
+    cost for the same bursts is cpu_baseline.burst_latency."""
+    import ctypes as C
     res = {}
+    out = (C.c_double * 5)()
     with csum.HostContext(torch.cuda.current_device(), chunk_bytes=4 << 20) as ctx:
         for nf in BURSTS:
             ar, offs, lens = burst_frames(nf)
             pinned = torch.from_numpy(ar).pin_memory()
             flags = np.empty(nf, np.uint8)
-            ts = []
-            for i in range(300 if nf < 1024 else 100):
-                t0 = time.perf_counter()
-                ctx.validate_frames(pinned.data_ptr(), offs, lens, flags=flags)
-                ts.append(time.perf_counter() - t0)
-            res[str(nf)] = {"us_per_burst": round(float(np.median(ts)) * 1e6, 2),
-                            "us_p99": round(float(np.percentile(ts, 99)) * 1e6, 2),
-                            "ns_per_frame": round(float(np.median(ts)) * 1e9 / nf, 1),
-                            "parity": "ok" if bool((flags == 0x0F).all()) else "MISMATCH"}
-    return {"workload": "TCP frames of 1514 B in 2 KiB pinned host slots, one "
-                        "tulips_csum_validate_frames_host call per burst (the gpucsum "
-                        "decorator's path)", "bursts": res}
+            ent = {}
+            for name, path in (("staged", 0), ("zero_copy", 1)):
+                reps = 2000 if nf <= 64 else 300
+                rc = csum.lib.tulips_csum_time_validate(
+                    ctx._h, path, pinned.data_ptr(), offs.ctypes.data, lens.ctypes.data, nf,
+                    reps, flags.ctypes.data, out)
+                if rc:
+                    ent[name] = {"error": rc}
+                    continue
+                ent[name] = {"us_median": round(out[0], 2), "us_p99": round(out[1], 2),
+                             "us_min": round(out[2], 2), "reps": reps,
+                             "parity": "ok" if bool((flags == 0x0F).all()) else "MISMATCH"}
+                if path == 1:
+                    ent[name]["gpu_service_us"] = round(out[4], 2)
+            res[str(nf)] = ent
+    return {"workload": "TCP frames of 1514 B in 2 KiB page-locked host slots, one "
+                        "validation call per burst, C-timed (tulips_csum_time_validate)",
+            "bursts": res}
 
 
 def rate_entry(alg_bytes, t, **kw):
@@ -1121,28 +1171,28 @@ def cpu_baseline(arena, batch_bytes, seconds):
     # the reference's per-frame receive verification over the same bursts as
     # extras.burst_latency_host: ipv4::checksum of each header and the tcpv4
     # checksum of each segment (its own build), one thread, as the stack's
-    # poll loop runs it
+    # poll loop runs it, timed in C (oracle/ref_harness.cpp
+    # ref_time_verify_burst)
     lat = {}
-    for nf in BURSTS:
-        far, foffs, flens = burst_frames(nf)
-        ip_offs, tcp_offs = foffs + np.uint64(14), foffs + np.uint64(34)
-        ip_lens = np.full(nf, 20, np.uint16)
-        tcp_lens = (flens - 34).astype(np.uint16)
-        src = far[(foffs + 26).astype(np.int64)[:, None] + np.arange(4)].copy().view("<u4")[:, 0]
-        dst = far[(foffs + 30).astype(np.int64)[:, None] + np.arange(4)].copy().view("<u4")[:, 0]
-        ts = []
-        for i in range(200 if nf < 1024 else 50):
-            t0 = time.perf_counter()
-            a = impl.batch(far, ip_offs, ip_lens, mode=1)
-            b = impl.batch(far, tcp_offs, tcp_lens, src=src, dst=dst, mode=2)
-            ts.append(time.perf_counter() - t0)
-        ok = bool((a == 0xFFFF).all() and (b == 0xFFFF).all())
-        lat[str(nf)] = {"us_per_burst": round(float(np.median(ts)) * 1e6, 2),
-                        "ns_per_frame": round(float(np.median(ts)) * 1e9 / nf, 1),
-                        "parity": "ok" if ok else "MISMATCH"}
+    if kind == "reference":
+        import ctypes as C
+        f = impl.lib.ref_time_verify_burst
+        f.restype = C.c_uint32
+        f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                      C.c_void_p]
+        out = (C.c_double * 4)()
+        for nf in BURSTS:
+            far, foffs, flens = burst_frames(nf)
+            reps = 20000 if nf <= 64 else 2000
+            good = f(far.ctypes.data, foffs.ctypes.data, flens.ctypes.data, nf, reps,
+                     C.addressof(out))
+            lat[str(nf)] = {"us_median": round(out[0], 3), "us_p99": round(out[1], 3),
+                            "ns_per_frame": round(out[0] * 1e3 / nf, 1), "reps": reps,
+                            "parity": "ok" if good == nf else "MISMATCH"}
     res["burst_latency"] = {"what": "reference ipv4 + tcpv4 checksum verification of each "
-                                    "frame of the burst, 1 thread (includes one ctypes "
-                                    "call per protocol per burst)", "bursts": lat}
+                                    "frame of the burst, 1 thread, C-timed "
+                                    "(oracle/ref_harness.cpp ref_time_verify_burst)",
+                            "bursts": lat}
     if kind == "reference" and Reference.available(REF_CLANG_SO):
         # the same reference sources built with clang, the compiler the
         # reference's CMake prefers (CMakeLists.txt:20-21)

@@ -90,6 +90,25 @@ int tulips_csum_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
 int tulips_csum_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
                             uint32_t max_blocks, void* stream);
 
+/* The F9000 checksum kernel's read pattern without its arithmetic: tile k =
+ * [p + k * tile_bytes, p + (k + 1) * tile_bytes) read by one wave, 64 lanes x
+ * 12 clamped 16-byte loads (tile_bytes <= 65535). The ceiling that kernel is
+ * compared against (bench.py extras.F9000.read_same_bytes). */
+int tulips_csum_stream_read_tiles(const uint8_t* p, uint64_t tile_bytes, uint32_t ntiles,
+                                  uint32_t* sink, void* stream);
+
+/* Latency of `reps` back-to-back receive validations of one burst of
+ * host-resident frames, timed in C with a steady clock around each call
+ * (no interpreter in the loop): path 0 = tulips_csum_validate_frames_host
+ * (staged), 1 = tulips_csum_validate_frames_zc. out[0..4] = median, p99,
+ * min, mean (us) and, for path 1, the median GPU service time (request
+ * picked up -> flags out, from the server's realtime clock; 0 otherwise).
+ * `flags` (n bytes) holds the last call's flags. */
+typedef struct tulips_csum_ctx tulips_csum_ctx;
+int tulips_csum_time_validate(tulips_csum_ctx* ctx, int path, const uint8_t* base,
+                              const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
+                              uint32_t reps, uint8_t* flags, double* out);
+
 #ifdef __cplusplus
 }
 #endif

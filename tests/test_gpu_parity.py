@@ -395,8 +395,8 @@ def test_host_context_span_straddling_two_pinned_blocks(oracle):
             lens = rng.integers(1, 3000, n).astype(np.uint16)
             at = rng.integers(0, size - 3000, n).astype(np.uint64)
             in_b = np.arange(n) >= n // 2
-            offs = np.where(in_b, (at + np.uint64((b - a) % 2**64)) % np.uint64(2**64), at)
-            offs = offs.astype(np.uint64)
+            offs = np.array([(int(at[i]) + (b - a if in_b[i] else 0)) % 2**64
+                             for i in range(n)], dtype=np.uint64)
             exp = np.array([oracle.checksum(0, (vb if in_b[i] else va)
                                             [int(at[i]):int(at[i]) + int(lens[i])].tobytes())
                             for i in range(n)], np.uint16)

@@ -1,35 +1,43 @@
-"""Probe of the low-latency validation path: one context, bursts of 1 and
-64 frames from pinned (or, with argv[1] == 'pageable', pageable) memory,
-timing and status of each call. Exits hard after the first failure (a
-server that never answered cannot be stopped)."""
+"""Probe of the receive-validation latency paths, C-timed
+(tulips_csum_time_validate): staged vs zero-copy, bursts of 1..1024 TCP
+frames of 1514 B in page-locked 2 KiB slots; TULIPS_ZC_MODE=resident picks
+the resident server. Also the reference CPU verify when oracle/_ref exists."""
+import ctypes as C
 import os
 import sys
-import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import torch  # noqa: E402
 from tulips_amd import csum  # noqa: E402
+import bench  # noqa: E402
 
-nf, slot, seg = 256, 2048, 1500
-t = torch.zeros(nf * slot, dtype=torch.uint8)
-pageable = len(sys.argv) > 1 and sys.argv[1] == "pageable"
-ar = t.numpy() if pageable else t.pin_memory().numpy()
-offs = np.arange(nf, dtype=np.uint64) * np.uint64(slot)
-lens = np.full(nf, seg + 14, np.uint16)
-ctx = csum.HostContext(0)
-res = {}
-for b in (1, 1, 64, 1, 64) + (1,) * 200 + (64,) * 200 + (256,) * 50:
-    t0 = time.perf_counter()
-    try:
-        fl = ctx.validate_frames(ar, offs[:b], lens[:b], low_latency=True)
-        res.setdefault(b, []).append(1e6 * (time.perf_counter() - t0))
-    except Exception as e:  # noqa: BLE001
-        print(f"burst {b}: {e!r} after {time.perf_counter() - t0:.2f} s", flush=True)
-        os._exit(3)
-ctx.close()
 mode = os.environ.get("TULIPS_ZC_MODE", "launch")
-for b, ts in res.items():
-    print(f"{mode} {'pageable' if pageable else 'pinned'} burst {b}: median "
-          f"{np.median(ts):.1f} us p99 {np.percentile(ts, 99):.1f} us (n={len(ts)})", flush=True)
+out = (C.c_double * 5)()
+with csum.HostContext(0, chunk_bytes=4 << 20) as ctx:
+    for nf in (1, 8, 64, 256, 1024):
+        ar, offs, lens = bench.burst_frames(nf)
+        pinned = torch.from_numpy(ar).pin_memory()
+        flags = np.empty(nf, np.uint8)
+        for name, path in (("staged", 0), ("zero_copy", 1)):
+            rc = csum.lib.tulips_csum_time_validate(ctx._h, path, pinned.data_ptr(),
+                                                    offs.ctypes.data, lens.ctypes.data, nf,
+                                                    1000, flags.ctypes.data, out)
+            print(f"{mode:8s} {name:9s} burst {nf:5d}: rc {rc} median {out[0]:7.2f} us p99 "
+                  f"{out[1]:7.2f} min {out[2]:7.2f} gpu {out[4]:6.2f} ok "
+                  f"{bool((flags == 0x0F).all())}", flush=True)
+try:
+    from oracle import Reference
+    ref = Reference()
+    f = ref.lib.ref_time_verify_burst
+    f.restype = C.c_uint32
+    f.argtypes = [C.c_void_p] * 3 + [C.c_uint32, C.c_uint32, C.c_void_p]
+    for nf in (1, 8, 64, 256, 1024):
+        ar, offs, lens = bench.burst_frames(nf)
+        g = f(ar.ctypes.data, offs.ctypes.data, lens.ctypes.data, nf, 5000, C.addressof(out))
+        print(f"cpu-ref   burst {nf:5d}: median {out[0]:7.3f} us p99 {out[1]:7.3f} good {g}")
+except Exception as e:  # noqa: BLE001
+    print("no reference:", e)

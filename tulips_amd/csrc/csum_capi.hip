@@ -550,6 +550,17 @@ tulips_csum_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
                                       static_cast<hipStream_t>(stream)));
 }
 
+int
+tulips_csum_stream_read_tiles(const uint8_t* p, uint64_t tile_bytes, uint32_t ntiles,
+                              uint32_t* sink, void* stream)
+{
+  if (ntiles && (!p || !sink || tile_bytes == 0 || tile_bytes > TULIPS_CSUM_MAX_SEGMENT)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return status_of(
+    launch_stream_tiles(p, tile_bytes, ntiles, sink, static_cast<hipStream_t>(stream)));
+}
+
 const char*
 tulips_csum_status_string(int status)
 {

@@ -893,30 +893,49 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
   } else {
     return ZC_NOT_APPLICABLE;
   }
+  // descriptors as 32-bit offsets from the hull's start
+  const uint64_t l0 = hi > lo ? lo : 0;
+  if ((hi > lo ? hi - lo : 0) >= (1ull << 32)) {
+    return ZC_NOT_APPLICABLE;
+  }
+  const uint64_t gbase = dbase + l0;
+  if ((z.seq + 1) % 65536 == 0) {
+    ++z.seq; // tags are 16-bit and never 0
+  }
   const uint64_t seq = ++z.seq;
+  const uint32_t tag = uint32_t(seq & 0xffffu);
   ZcArgs args{};
-  args.base = dbase;
-  args.seq = seq;
-  args.n = n;
-  // a launch per burst carries a small burst's descriptors in its arguments
-  const bool inl = !z.resident && n <= ZC_ARG_FRAMES && hi - (hi > lo ? lo : 0) < (1ull << 32);
-  if (inl) {
-    const uint64_t l0 = hi > lo ? lo : 0;
-    args.base = dbase + l0;
-    args.inline_n = n;
+  const bool inl = z.resident ? n <= ZC_REQ_FRAMES : n <= ZC_ARG_FRAMES;
+  auto off_of = [&](uint32_t k) { return (staged ? mb->offs[k] : offsets[k]) - l0; };
+  if (!inl) {
     for (uint32_t k = 0; k < n; ++k) {
-      args.off[k] = uint32_t((staged ? mb->offs[k] : offsets[k]) - l0);
-      args.len[k] = lengths[k];
-    }
-  } else {
-    if (!staged) {
-      memcpy(mb->offs, offsets, size_t(n) * 8);
+      mb->offs[k] = off_of(k);
     }
     memcpy(mb->lens, lengths, size_t(n) * 2);
-    mb->base = dbase;
-    mb->n = n;
   }
-  __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
+  if (z.resident) {
+    // tagged doorbell words, the first one last (zc_mailbox.h)
+    if (inl) {
+      for (uint32_t k = 0; k < n; ++k) {
+        __atomic_store_n(&mb->req[2 + k], zc_word(tag, (off_of(k) << 16) | lengths[k]),
+                         __ATOMIC_RELAXED);
+      }
+    }
+    __atomic_store_n(&mb->req[1], zc_word(tag, gbase), __ATOMIC_RELAXED);
+    __atomic_store_n(&mb->req[0], zc_word(tag, n), __ATOMIC_RELEASE);
+  } else {
+    args.base = gbase;
+    args.seq = tag;
+    args.n = n;
+    if (inl) {
+      args.inline_n = n;
+      for (uint32_t k = 0; k < n; ++k) {
+        args.off[k] = uint32_t(off_of(k));
+        args.len[k] = lengths[k];
+      }
+    }
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+  }
   // (re)start the server: first use, or it may have timed out since the
   // last burst (it idles out after 100 ms; checked from 50 ms on)
   const auto now = std::chrono::steady_clock::now();
@@ -950,7 +969,7 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
     }
   }
   for (uint64_t k = 1;; ++k) {
-    if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) {
+    if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == tag) {
       break;
     }
     __builtin_ia32_pause();
@@ -964,10 +983,10 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
                 "tulips_csum_validate_frames_zc: no answer in 2 s (seq %llu done %llu "
                 "seen %llu beat %llu stage %llu launched %d query %d base %llx mb %p/%llx "
                 "pin %llx-%llx dev %llx b0 %llx n %u)\n",
-                (unsigned long long)seq, (unsigned long long)mb->done,
+                (unsigned long long)tag, (unsigned long long)mb->done,
                 (unsigned long long)mb->seen, (unsigned long long)mb->beat,
                 (unsigned long long)0, int(z.launched),
-                int(hipStreamQuery(z.stream)), (unsigned long long)dbase, (void*)mb,
+                int(hipStreamQuery(z.stream)), (unsigned long long)gbase, (void*)mb,
                 (unsigned long long)z.mb_dev, (unsigned long long)z.pin.lo,
                 (unsigned long long)z.pin.hi, (unsigned long long)z.pin_dev,
                 (unsigned long long)b0, n);
@@ -1016,6 +1035,47 @@ tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,
     rc = tulips_csum_validate_frames_host(ctx, base, offsets, lengths, n, flags, counters);
   }
   return rc;
+}
+
+extern "C" int
+tulips_csum_time_validate(tulips_csum_ctx* ctx, int path, const uint8_t* base,
+                          const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
+                          uint32_t reps, uint8_t* flags, double* out)
+{
+  if (!ctx || !out || reps == 0 || (path != 0 && path != 1)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  std::vector<double> t(reps), g;
+  for (uint32_t r = 0; r < reps; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc =
+      path ? tulips_csum_validate_frames_zc(ctx, base, offsets, lengths, n, flags, nullptr)
+           : tulips_csum_validate_frames_host(ctx, base, offsets, lengths, n, flags, nullptr);
+    t[r] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
+             .count();
+    if (rc != TULIPS_STATUS_OK) {
+      return rc;
+    }
+    if (path && ctx->zc.mb) {
+      g.push_back(double(ctx->zc.mb->t_done - ctx->zc.mb->t_req) / 100.0); // 100 MHz
+    }
+  }
+  std::vector<double> s = t;
+  std::sort(s.begin(), s.end());
+  double mean = 0;
+  for (double x : t) {
+    mean += x / reps;
+  }
+  out[0] = s[reps / 2];
+  out[1] = s[std::min<size_t>(reps - 1, size_t(double(reps) * 0.99))];
+  out[2] = s[0];
+  out[3] = mean;
+  out[4] = 0;
+  if (!g.empty()) {
+    std::sort(g.begin(), g.end());
+    out[4] = g[g.size() / 2];
+  }
+  return TULIPS_STATUS_OK;
 }
 
 namespace {

@@ -775,7 +775,56 @@ stream_read_kernel(uintptr_t base, uint64_t nchunks,
   }
 }
 
+// The F9000 checksum kernel's exact read pattern without its arithmetic:
+// wave w reads the 16-byte chunks of tile [w * tile, (w + 1) * tile) at
+// absolute alignment, 64 lanes x 12 unconditional loads, slots past the
+// tile re-reading its last chunk (as csum_kernel<64, 12> does for one
+// segment per wave), in the same XCD-clustered block order. Bounds that
+// kernel from above.
+__global__ __launch_bounds__(256) void
+stream_tiles_kernel(uintptr_t base, uint64_t tile, uint32_t ntiles, uint32_t* __restrict__ sink)
+{
+  constexpr int U = 12;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6;
+  if (wave >= ntiles) {
+    return;
+  }
+  const uintptr_t sa = base + uint64_t(wave) * tile;
+  const uintptr_t a0 = sa & ~uintptr_t(15);
+  const int last = int((sa + tile - a0 + 15) >> 4) - 1;
+  const gchunk_ptr p = reinterpret_cast<gchunk_ptr>(a0);
+  uint32_t x = 0;
+  for (int c = int(lane); c <= last; c += U * 64) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = __builtin_nontemporal_load(p + min(c + u * 64, last));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+  }
+  if (x == 0x9e3779b9u) { // practically never; keeps the loads live
+    sink[0] = x;
+  }
+}
+
 } // namespace
+
+hipError_t
+launch_stream_tiles(const uint8_t* p, uint64_t tile, uint32_t ntiles, uint32_t* sink,
+                    hipStream_t stream)
+{
+  if (ntiles == 0 || tile == 0) {
+    return hipSuccess;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(stream_tiles_kernel, dim3((ntiles + 3) / 4), dim3(256), 0, stream,
+                     reinterpret_cast<uintptr_t>(p), tile, ntiles, sink);
+  return hipGetLastError();
+}
 
 hipError_t
 launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,

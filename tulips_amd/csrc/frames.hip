@@ -209,9 +209,8 @@ template<bool RESIDENT>
 __global__ __launch_bounds__(1024) void
 zc_server_kernel(ZcMailbox* mb, ZcArgs args)
 {
-  const uint64_t seq0 = args.seq;
   constexpr int FG = 16, FU = 6;
-  __shared__ uint64_t s_seq;
+  __shared__ uint64_t s_req[ZC_REQ_WORDS];
   __shared__ uint32_t s_exit;
   __shared__ uint32_t s_cnt[4];
   const int lane64 = threadIdx.x & 63;
@@ -219,28 +218,34 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
   const int sub0 = lane64 - lane;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t sub = threadIdx.x / FG, nsub = blockDim.x / FG;
-  uint64_t served = RESIDENT ? __hip_atomic_load(&mb->done, __ATOMIC_ACQUIRE,
-                                                 __HIP_MEMORY_SCOPE_SYSTEM)
-                             : 0;
+  // the last tag served (resident) / the request (one launch)
+  uint32_t served = RESIDENT ? uint32_t(__hip_atomic_load(&mb->done, __ATOMIC_ACQUIRE,
+                                                          __HIP_MEMORY_SCOPE_SYSTEM))
+                             : 0u;
   for (;;) {
     if (wave == 0) {
-      uint64_t seq = seq0;
       uint32_t ex = 0;
+      uint64_t w = 0;
       if (RESIDENT) {
-        // the whole wave polls the same word (one request per load)
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (uint32_t polls = 1;; ++polls) {
-          const uint64_t v =
-            __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-          seq = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(v >> 32))) << 32) |
-                __builtin_amdgcn_readfirstlane(uint32_t(v));
+          w = __hip_atomic_load(&mb->req[lane64], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          const uint32_t tag = uint32_t(w >> 48);
+          const uint32_t tag0 = __builtin_amdgcn_readfirstlane(tag);
           if ((polls & 1023u) == 0 && lane64 == 0) {
             __hip_atomic_store(&mb->beat, uint64_t(polls >> 10), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&mb->seen, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&mb->seen, uint64_t(tag0), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
           }
-          if (seq != served) {
-            break;
+          if (tag0 != (served & 0xffffu)) {
+            // a new request: every word it needs must carry its tag
+            const uint32_t n0 = __builtin_amdgcn_readfirstlane(uint32_t(w & 0xffffu));
+            const uint32_t need = 2u + (n0 <= ZC_REQ_FRAMES ? n0 : 0u);
+            if (__builtin_amdgcn_ballot_w64(uint32_t(lane64) < need && tag != tag0) == 0) {
+              break;
+            }
+            continue; // caught the host mid-write
           }
           const uint32_t stop = __builtin_amdgcn_readfirstlane(uint32_t(
             __hip_atomic_load(&mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
@@ -250,9 +255,18 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
           }
           __builtin_amdgcn_s_sleep(1);
         }
+      } else {
+        // the request as kernel arguments, in the same word format
+        const uint32_t tag = uint32_t(args.seq);
+        const uint32_t k = uint32_t(lane64) - 2u;
+        w = lane64 == 0   ? zc_word(tag, args.n)
+            : lane64 == 1 ? zc_word(tag, args.base)
+            : k < min(args.inline_n, ZC_ARG_FRAMES)
+              ? zc_word(tag, (uint64_t(args.off[k]) << 16) | args.len[k])
+              : 0ull;
       }
+      s_req[lane64] = w;
       if (lane64 == 0) {
-        s_seq = seq;
         s_exit = ex;
         s_cnt[0] = s_cnt[1] = s_cnt[2] = s_cnt[3] = 0;
       }
@@ -261,20 +275,25 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
     if (__builtin_amdgcn_readfirstlane(s_exit) != 0) {
       break;
     }
-    // every wave sees the request and the frames as the host left them
+    // every wave sees the frames (and any descriptor arrays) as the host left them
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    const uint64_t seq = s_seq;
-    const bool inl = !RESIDENT && args.inline_n != 0;
-    const uintptr_t base = inl ? uintptr_t(args.base)
-                               : uintptr_t(__hip_atomic_load(&mb->base, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_SYSTEM));
-    const uint32_t n =
-      inl ? min(args.inline_n, ZC_ARG_FRAMES)
-          : min(__hip_atomic_load(&mb->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                ZC_MAX_FRAMES);
+    const uint64_t t_req = __builtin_amdgcn_s_memrealtime();
+    const uint32_t tag = uint32_t(s_req[0] >> 48);
+    const uint32_t n = min(uint32_t(s_req[0] & 0xffffu), ZC_MAX_FRAMES);
+    const uintptr_t base = uintptr_t(s_req[1] & 0xffffffffffffull);
+    const bool inl = RESIDENT ? n <= ZC_REQ_FRAMES : args.inline_n != 0;
     for (uint32_t f = sub; f < n; f += nsub) {
-      const uintptr_t fa = base + (inl ? uint64_t(args.off[f]) : mb->offs[f]);
-      const uint32_t flen = inl ? uint32_t(args.len[f]) : uint32_t(mb->lens[f]);
+      uint64_t off;
+      uint32_t flen;
+      if (inl) {
+        const uint64_t d = s_req[2 + f];
+        off = (d >> 16) & 0xffffffffull;
+        flen = uint32_t(d & 0xffffu);
+      } else {
+        off = mb->offs[f];
+        flen = mb->lens[f];
+      }
+      const uintptr_t fa = base + off;
       FrameChunks<FG, FU> fc;
       load_frame<FG, FU, false>(fa, flen, lane, fc);
       const Header h = frame_header(fc, flen, sub0);
@@ -312,13 +331,17 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
         __hip_atomic_store(&mb->counters[k], s_cnt[k], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      __hip_atomic_store(&mb->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->t_req, t_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->t_done, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->done, uint64_t(tag), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (!RESIDENT) {
       break;
     }
-    served = seq;
-    __syncthreads(); // s_seq / s_cnt are rewritten by the next poll
+    served = tag;
+    __syncthreads(); // s_req / s_cnt are rewritten by the next poll
   }
 }
 

@@ -3,13 +3,13 @@
 // server kernel (frames.hip).
 //
 // A poll burst of a few frames costs the staged path (pinned staging copy,
-// H2D, launch, D2H of the flags, event wait) ~28 us, more than the
-// reference's CPU verify of one frame (~15 us). Here one workgroup stays
-// resident and polls a doorbell in page-locked, host-coherent memory: the
-// host copies the burst's offsets/lengths into the mailbox, bumps `seq`
-// (release), and spins on `done`; the kernel reads the frames straight from
-// the caller's page-locked arena over PCIe (no copies, no launch), writes
-// the flags into the mailbox and publishes `done` (release, system scope).
+// H2D, launch, D2H of the flags, event wait) ~28 us. Here the frames are read
+// straight from the caller's page-locked arena over PCIe (no copies) by one
+// workgroup, which writes the flags into this page-locked, host-coherent
+// mailbox and publishes `done` (release, system scope) while the host spins
+// on it. Either one launch per burst carries the request in its kernel
+// arguments (ZcArgs), or one workgroup stays resident and polls the tagged
+// doorbell words below (no launch at all).
 // The server exits when `stop` is set or after ZC_IDLE_TICKS of silence
 // (every wave reaches that exit: no kernel outlives an abandoned context);
 // the host relaunches it on the next burst.
@@ -31,22 +31,38 @@ constexpr uint32_t ZC_ARG_FRAMES = 64;
 struct ZcArgs
 {
   uint64_t base;                 // frames arena (GPU address)
-  uint64_t seq;                  // the request being served
+  uint64_t seq;                  // the request's 16-bit tag (published in `done`)
   uint32_t n;                    // frames
   uint32_t inline_n;             // n if <= ZC_ARG_FRAMES (descriptors below), else 0
+                                 // (then ZcMailbox offs / lens, from `base`)
   uint32_t off[ZC_ARG_FRAMES];   // frame offsets from base (inline form)
   uint16_t len[ZC_ARG_FRAMES];
 };
 
+// Resident server doorbell: 64 tagged words, read by one wave load (a word
+// per lane) on every poll. Each word carries the request's 16-bit tag in its
+// top bits and is stored atomically by the host, so a poll that finds every
+// word it needs carrying the new tag has a consistent request, and a poll
+// that catches the host mid-write simply polls again: the request is known
+// one PCIe round trip after the host posts it.
+//   req[0] = tag << 48 | n             (n frames)
+//   req[1] = tag << 48 | base          (GPU address of frame 0's arena, < 2^48)
+//   req[2 + k] = tag << 48 | off << 16 | len   for k < n <= ZC_REQ_FRAMES
+// Larger bursts put their descriptors in `offs` / `lens` (written before the
+// tagged words; offsets there are from `base`).
+constexpr uint32_t ZC_REQ_WORDS = 64, ZC_REQ_FRAMES = ZC_REQ_WORDS - 2;
+
+__host__ __device__ inline uint64_t
+zc_word(uint32_t tag, uint64_t payload)
+{
+  return (uint64_t(tag & 0xffffu) << 48) | (payload & 0xffffffffffffull);
+}
+
 struct alignas(64) ZcMailbox
 {
-  // request (host writes these, then `seq`)
-  uint64_t base;        // frames arena, host address the GPU may read
-  uint32_t n;           // frames
-  uint32_t pad0;
-  uint64_t pad1[6];
-  // doorbell and stop (host -> GPU)
-  alignas(64) uint64_t seq;
+  alignas(64) uint64_t req[ZC_REQ_WORDS];
+  // stop (host -> GPU)
+  alignas(64) uint64_t seq;   // (one-shot form: the posted request)
   uint64_t stop;
   uint64_t pad2[6];
   // completion (GPU -> host)
@@ -54,7 +70,9 @@ struct alignas(64) ZcMailbox
   uint32_t counters[4];  // IPv4, bad IP csum, TCP, bad L4 csum of request `done`
   uint64_t beat;         // server heartbeat: polls / 1024 (diagnostics)
   uint64_t seen;         // last doorbell value the server read (diagnostics)
-  uint64_t pad3[3];
+  uint64_t t_req;        // s_memrealtime when the request was picked up
+  uint64_t t_done;       // ... and when its flags were out (diagnostics)
+  uint64_t pad3;
   // per-frame arrays of the request
   alignas(64) uint64_t offs[ZC_MAX_FRAMES];
   uint16_t lens[ZC_MAX_FRAMES];

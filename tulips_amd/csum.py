@@ -126,6 +126,7 @@ _SIGNATURES = {
     "tulips_csum_fill_splitmix": (C.c_int, [_vp, C.c_uint64, C.c_uint64,
                                             C.c_uint64, _vp]),
     "tulips_csum_stream_read": (C.c_int, [_vp, C.c_uint64, _vp, C.c_uint32, _vp]),
+    "tulips_csum_stream_read_tiles": (C.c_int, [_vp, C.c_uint64, C.c_uint32, _vp, _vp]),
     "tulips_rss_toeplitz_host": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16,
                                            _u8p, C.c_size_t, C.c_uint32,
                                            C.POINTER(C.c_uint32)]),
@@ -162,6 +163,8 @@ _SIGNATURES = {
                                                       _vp]),
     "tulips_csum_generate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp]),
     "tulips_csum_validate_frames_zc": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp, _vp]),
+    "tulips_csum_time_validate": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_uint32,
+                                            C.c_uint32, _vp, _vp]),
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
 }
