@@ -930,9 +930,11 @@ def burst_latency(torch, csum):
     (tulips_csum_time_validate: no interpreter in the loop), frames in a
     page-locked 2 KiB-slot arena as the decorator stages them:
       staged: tulips_csum_validate_frames_host (pinned DMA, launch, D2H);
-      zero_copy: tulips_csum_validate_frames_zc (the kernel reads the frames
-      in place over PCIe, descriptors in its arguments, flags written to a
-      page-locked mailbox the host spins on); gpu_service_us is the kernel's
+      zero_copy: tulips_csum_validate_frames_zc, one launch per burst (the
+      kernel reads the frames in place over PCIe, descriptors in its
+      arguments, flags written to a page-locked mailbox the host spins on);
+      zero_copy_resident: the same with resident workgroups polling a
+      doorbell (tulips_csum_ctx_set_lowlat); gpu_service_us is the kernel's
       own request-to-flags time from its realtime clock.
     The reference verifies each frame on the CPU as it arrives
     (ipv4/Processor.cpp:94-103, tcpv4/Processor.cpp:121-131); its C-timed
@@ -946,7 +948,9 @@ def burst_latency(torch, csum):
             pinned = torch.from_numpy(ar).pin_memory()
             flags = np.empty(nf, np.uint8)
             ent = {}
-            for name, path in (("staged", 0), ("zero_copy", 1)):
+            for name, path, resident in (("staged", 0, False), ("zero_copy", 1, False),
+                                         ("zero_copy_resident", 1, True)):
+                ctx.set_lowlat(resident)
                 reps = 2000 if nf <= 64 else 300
                 rc = csum.lib.tulips_csum_time_validate(
                     ctx._h, path, pinned.data_ptr(), offs.ctypes.data, lens.ctypes.data, nf,

@@ -385,25 +385,31 @@ int tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
                                      uint8_t* flags, uint32_t* counters);
 
 /*
- * Low-latency form of tulips_csum_validate_frames_host for small poll
+ * Low-latency (zero-copy) form of tulips_csum_validate_frames_host for poll
  * bursts (the reference is a latency stack: docs/topics/Test-and-
  * Performance.md:12-15, its OFED poll drains whatever CQ batch is ready,
- * src/transport/ofed/Device.cpp:505-545). A workgroup stays resident on the
- * context's device and polls a doorbell in page-locked host memory; each
- * call copies the burst's offsets/lengths into that mailbox, rings it, and
- * spins until the flags are back. Frames in page-locked memory (one
+ * src/transport/ofed/Device.cpp:505-545). Frames in page-locked memory (one
  * hipHostMalloc / hipHostRegister allocation, e.g. a transport's staging
- * arena) are read in place over PCIe: no staging copy, no DMA, no launch.
- * Frames in pageable memory are first packed into the context's 2 MiB
- * page-locked staging. Bursts of more than TULIPS_CSUM_ZC_MAX_FRAMES frames,
- * or pageable bursts past 2 MiB, take tulips_csum_validate_frames_host. Same
- * flags and counters. The server leaves the GPU after 100 ms without a burst
- * (the next call restarts it) and when the context is destroyed.
+ * arena) are read in place over PCIe by the kernel: no staging copy and no
+ * DMA; the flags come back through a page-locked mailbox the calling thread
+ * spins on. By default each call is one launch whose arguments carry the
+ * burst's descriptors (up to 62 frames; larger bursts' descriptors go
+ * through the mailbox, one workgroup per 64 frames). With
+ * tulips_csum_ctx_set_lowlat(ctx, 1) eight workgroups stay resident on the
+ * context's device instead and poll tagged doorbell words in the mailbox
+ * (no launch per call; they leave the GPU after 100 ms without a burst, the
+ * next call restarting them, and when the context is destroyed or switched
+ * back). Frames in pageable memory are first packed into the context's
+ * 2 MiB page-locked staging. Bursts of more than TULIPS_CSUM_ZC_MAX_FRAMES
+ * frames, or pageable bursts past 2 MiB, take
+ * tulips_csum_validate_frames_host. Same flags and counters.
  */
 #define TULIPS_CSUM_ZC_MAX_FRAMES 1024u
 int tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,
                                    const uint64_t* offsets, const uint16_t* lengths,
                                    uint32_t n, uint8_t* flags, uint32_t* counters);
+/* 0 = one launch per burst (default), 1 = resident server. */
+int tulips_csum_ctx_set_lowlat(tulips_csum_ctx* ctx, int resident);
 
 /* In-place checksum generation for host-resident frames (what a transport's
  * send path would offload, src/transport/ofed/Device.cpp:756): the frames

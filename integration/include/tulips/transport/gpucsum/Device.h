@@ -73,9 +73,10 @@ public:
   };
 
   static constexpr uint32_t DEFAULT_BURST = 1024;
-  // bursts up to this size take the low-latency server (measured on MI355X:
-  // DESIGN.md §5 "Latency per poll burst")
-  static constexpr uint32_t DEFAULT_LOWLAT = 256;
+  // bursts up to this size take the zero-copy path (on MI355X it beats the
+  // staged one at every burst size up to its 1,024-frame limit: DESIGN.md §5
+  // "Latency per poll burst")
+  static constexpr uint32_t DEFAULT_LOWLAT = 1024;
 
   struct Config
   {
@@ -89,6 +90,8 @@ public:
     // low-latency server (tulips_csum_validate_frames_zc: frames read in
     // place from the pinned staging arena, no copies or launch); 0 = never
     uint32_t lowlat = DEFAULT_LOWLAT;
+    // ... served by workgroups resident on the GPU (no launch per burst)
+    bool lowlat_resident = false;
   };
 
   static Ref allocate(system::Logger& log, transport::Device::Ref device,

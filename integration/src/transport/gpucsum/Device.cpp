@@ -63,6 +63,9 @@ Device::Device(system::Logger& log, transport::Device::Ref device,
     throw std::runtime_error("gpucsum: cannot allocate the staging arena");
   }
   m_arena = static_cast<uint8_t*>(p);
+  if (config.lowlat_resident) {
+    tulips_csum_ctx_set_lowlat(m_ctx, 1);
+  }
   m_offsets.reserve(m_burst);
   m_lengths.reserve(m_burst);
   m_stamps.reserve(m_burst);

@@ -252,8 +252,9 @@ def test_gpu_host_context(oracle, pinned):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("resident", [False, True])
 @pytest.mark.parametrize("pinned", [True, False])
-def test_gpu_zero_copy_bursts(oracle, pinned):
+def test_gpu_zero_copy_bursts(oracle, pinned, resident):
     """tulips_csum_validate_frames_zc (the resident server, zc_mailbox.h):
     bursts of 1..1024 fixture frames (mutated) read in place from one
     page-locked arena, or packed from pageable memory, against the oracle;
@@ -272,11 +273,12 @@ def test_gpu_zero_copy_bursts(oracle, pinned):
     arena = buf.numpy()
     n = len(fx["offsets"])
     with csum.HostContext(0, chunk_bytes=1 << 17) as ctx:
+        ctx.set_lowlat(resident)
         for rnd in range(3):
             arena[:] = mutate(fx, rng, 1500)
             exp = oracle.validate_frames(arena, fx["offsets"], fx["lengths"])
             i = 0
-            for b in (1, 1, 7, 64, 200, 1024, 1, 1025, 3):
+            for b in (1, 1, 7, 61, 62, 63, 64, 65, 200, 1024, 1, 1025, 3):
                 if i + b > n:
                     i = 0
                 o, ln = fx["offsets"][i:i + b], fx["lengths"][i:i + b]
@@ -305,6 +307,7 @@ def test_gpu_zero_copy_two_contexts_and_destroy_while_serving(oracle):
     arena = torch.from_numpy(mutate(fx, np.random.default_rng(5), 900)).pin_memory().numpy()
     exp = oracle.validate_frames(arena, fx["offsets"], fx["lengths"])
     a = csum.HostContext(0)
+    a.set_lowlat(True)                          # one resident, one launch per burst
     with csum.HostContext(0) as b:
         for k in range(0, 2000, 50):
             sl = slice(k, k + 50)
@@ -325,6 +328,7 @@ def test_zero_copy_arguments_without_gpu():
     f = csum.lib.tulips_csum_validate_frames_zc
     assert f(None, 1, 1, 1, 4, 1, None) == 1                 # no context
     assert f(None, None, None, None, 0, None, None) == 1
+    assert csum.lib.tulips_csum_ctx_set_lowlat(None, 1) == 1
 
 
 # ------------------------------------------------- send-side generation -----

@@ -242,6 +242,7 @@ struct tulips_csum_ctx
   explicit tulips_csum_ctx(int threads) : pool(threads) {}
   int device = 0;
   ZcState zc;
+  bool zc_resident = false; // tulips_csum_ctx_set_lowlat
   uint64_t chunk = DEFAULT_CHUNK;
   Slot slots[NSLOTS];
   PackPool pool;
@@ -824,7 +825,7 @@ zc_setup(tulips_csum_ctx* ctx)
   }
   std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0xffffffffu);
   const char* mode = getenv("TULIPS_ZC_MODE");
-  z.resident = mode && strcmp(mode, "resident") == 0;
+  z.resident = ctx->zc_resident || (mode && strcmp(mode, "resident") == 0);
   const char* plain = getenv("TULIPS_ZC_PLAIN_STREAM");
   if ((e = (!z.resident || (plain && plain[0] == '1'))
              ? hipStreamCreateWithFlags(&z.stream, hipStreamNonBlocking)
@@ -904,6 +905,10 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
   }
   const uint64_t seq = ++z.seq;
   const uint32_t tag = uint32_t(seq & 0xffffu);
+  // the workgroups that answer this request (frames.hip launch_zc_server)
+  const uint32_t nwg = z.resident ? ZC_RES_WG
+                       : n <= ZC_ARG_FRAMES ? 1u
+                                            : std::min(ZC_MAX_WG, (n + 63) / 64);
   ZcArgs args{};
   const bool inl = z.resident ? n <= ZC_REQ_FRAMES : n <= ZC_ARG_FRAMES;
   auto off_of = [&](uint32_t k) { return (staged ? mb->offs[k] : offsets[k]) - l0; };
@@ -969,7 +974,11 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
     }
   }
   for (uint64_t k = 1;; ++k) {
-    if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == tag) {
+    uint32_t fin = 0;
+    for (uint32_t w = 0; w < nwg; ++w) {
+      fin += __atomic_load_n(&mb->done[w], __ATOMIC_ACQUIRE) == tag ? 1u : 0u;
+    }
+    if (fin == nwg) {
       break;
     }
     __builtin_ia32_pause();
@@ -983,7 +992,7 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
                 "tulips_csum_validate_frames_zc: no answer in 2 s (seq %llu done %llu "
                 "seen %llu beat %llu stage %llu launched %d query %d base %llx mb %p/%llx "
                 "pin %llx-%llx dev %llx b0 %llx n %u)\n",
-                (unsigned long long)tag, (unsigned long long)mb->done,
+                (unsigned long long)tag, (unsigned long long)mb->done[0],
                 (unsigned long long)mb->seen, (unsigned long long)mb->beat,
                 (unsigned long long)0, int(z.launched),
                 int(hipStreamQuery(z.stream)), (unsigned long long)gbase, (void*)mb,
@@ -998,13 +1007,33 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
   memcpy(flags, mb->flags, n);
   if (counters) {
     for (int k = 0; k < 4; ++k) {
-      counters[k] = mb->counters[k];
+      counters[k] = 0;
+      for (uint32_t w = 0; w < nwg; ++w) {
+        counters[k] += mb->counters[w][k];
+      }
     }
   }
   return TULIPS_STATUS_OK;
 }
 
 } // namespace
+
+extern "C" int
+tulips_csum_ctx_set_lowlat(tulips_csum_ctx* ctx, int resident)
+{
+  if (!ctx || (resident != 0 && resident != 1)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (ctx->zc.mb && ctx->zc.resident != (resident != 0)) {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(ctx->device);
+    zc_release(ctx->zc); // made again, in the new form, by the next call
+    (void)hipSetDevice(prev);
+  }
+  ctx->zc_resident = resident != 0;
+  return TULIPS_STATUS_OK;
+}
 
 extern "C" int
 tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,

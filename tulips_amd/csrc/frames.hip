@@ -217,9 +217,12 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
   const int lane = lane64 & (FG - 1);
   const int sub0 = lane64 - lane;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t sub = threadIdx.x / FG, nsub = blockDim.x / FG;
-  // the last tag served (resident) / the request (one launch)
-  uint32_t served = RESIDENT ? uint32_t(__hip_atomic_load(&mb->done, __ATOMIC_ACQUIRE,
+  // subgroup g of workgroup w takes frames (w * nsub + g) + k * gridDim.x * nsub
+  const uint32_t wg = blockIdx.x;
+  const uint32_t sub = wg * (blockDim.x / FG) + threadIdx.x / FG;
+  const uint32_t nsub = gridDim.x * (blockDim.x / FG);
+  // the last tag this workgroup served (resident) / the request (one launch)
+  uint32_t served = RESIDENT ? uint32_t(__hip_atomic_load(&mb->done[wg], __ATOMIC_ACQUIRE,
                                                           __HIP_MEMORY_SCOPE_SYSTEM))
                              : 0u;
   for (;;) {
@@ -232,7 +235,7 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
           w = __hip_atomic_load(&mb->req[lane64], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           const uint32_t tag = uint32_t(w >> 48);
           const uint32_t tag0 = __builtin_amdgcn_readfirstlane(tag);
-          if ((polls & 1023u) == 0 && lane64 == 0) {
+          if ((polls & 1023u) == 0 && lane64 == 0 && wg == 0) {
             __hip_atomic_store(&mb->beat, uint64_t(polls >> 10), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&mb->seen, uint64_t(tag0), __ATOMIC_RELAXED,
@@ -270,13 +273,15 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
         s_exit = ex;
         s_cnt[0] = s_cnt[1] = s_cnt[2] = s_cnt[3] = 0;
       }
+      // the frames (and any descriptor arrays) as the host left them: one
+      // invalidate of this CU's L1 and of L2 serves every wave of the
+      // workgroup (they load only after the barrier)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(s_exit) != 0) {
       break;
     }
-    // every wave sees the frames (and any descriptor arrays) as the host left them
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     const uint64_t t_req = __builtin_amdgcn_s_memrealtime();
     const uint32_t tag = uint32_t(s_req[0] >> 48);
     const uint32_t n = min(uint32_t(s_req[0] & 0xffffu), ZC_MAX_FRAMES);
@@ -323,18 +328,22 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
         }
       }
     }
-    // this wave's flag stores reach the host before `done` does
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    // this wave's flag stores (to the uncached, host-coherent mailbox) are
+    // complete before the barrier; thread 0's system-scope release then
+    // publishes them with `done`
+    __builtin_amdgcn_s_waitcnt(0x0f70); // vmcnt(0) expcnt(7) lgkmcnt(15)
     __syncthreads();
     if (threadIdx.x == 0) {
       for (int k = 0; k < 4; ++k) {
-        __hip_atomic_store(&mb->counters[k], s_cnt[k], __ATOMIC_RELAXED,
+        __hip_atomic_store(&mb->counters[wg][k], s_cnt[k], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      __hip_atomic_store(&mb->t_req, t_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&mb->t_done, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&mb->done, uint64_t(tag), __ATOMIC_RELEASE,
+      if (wg == 0) {
+        __hip_atomic_store(&mb->t_req, t_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->t_done, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __hip_atomic_store(&mb->done[wg], uint64_t(tag), __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (!RESIDENT) {
@@ -432,13 +441,17 @@ launch_zc_server(ZcMailbox* mb, const ZcArgs* oneshot, hipStream_t stream)
 {
   (void)hipGetLastError();
   if (oneshot) {
-    // a burst of up to 64 frames needs 4 waves, not 16
+    // a burst of up to 62 frames: one workgroup of a 16-lane subgroup per
+    // frame; more: one 1024-thread workgroup per 64 frames
+    const uint32_t n = oneshot->n;
     const uint32_t threads =
       oneshot->inline_n ? min(1024u, 64u * ((oneshot->inline_n + 3) / 4)) : 1024u;
-    hipLaunchKernelGGL(zc_server_kernel<false>, dim3(1), dim3(threads), 0, stream, mb,
+    const uint32_t wgs = oneshot->inline_n ? 1u : min(ZC_MAX_WG, (n + 63) / 64);
+    hipLaunchKernelGGL(zc_server_kernel<false>, dim3(wgs), dim3(threads), 0, stream, mb,
                        *oneshot);
   } else {
-    hipLaunchKernelGGL(zc_server_kernel<true>, dim3(1), dim3(1024), 0, stream, mb, ZcArgs{});
+    hipLaunchKernelGGL(zc_server_kernel<true>, dim3(ZC_RES_WG), dim3(1024), 0, stream, mb,
+                       ZcArgs{});
   }
   return hipGetLastError();
 }

@@ -26,7 +26,7 @@ constexpr uint64_t ZC_IDLE_TICKS = 100ull * 100000;   // 100 ms of s_memrealtime
 // One launch per burst: the request itself rides in the kernel arguments
 // (kernarg memory is device-resident), so a burst of up to ZC_ARG_FRAMES
 // frames costs the frame reads and the flag writes over PCIe, nothing else.
-constexpr uint32_t ZC_ARG_FRAMES = 64;
+constexpr uint32_t ZC_ARG_FRAMES = 62; // = ZC_REQ_FRAMES: the kernel builds the 64 doorbell words from them
 
 struct ZcArgs
 {
@@ -51,6 +51,7 @@ struct ZcArgs
 // Larger bursts put their descriptors in `offs` / `lens` (written before the
 // tagged words; offsets there are from `base`).
 constexpr uint32_t ZC_REQ_WORDS = 64, ZC_REQ_FRAMES = ZC_REQ_WORDS - 2;
+static_assert(ZC_ARG_FRAMES == ZC_REQ_FRAMES, "one wave turns the arguments into the words");
 
 __host__ __device__ inline uint64_t
 zc_word(uint32_t tag, uint64_t payload)
@@ -58,22 +59,29 @@ zc_word(uint32_t tag, uint64_t payload)
   return (uint64_t(tag & 0xffffu) << 48) | (payload & 0xffffffffffffull);
 }
 
+// Workgroups serving one request: a resident server keeps ZC_RES_WG of them
+// (each polls the doorbell, takes every ZC_RES_WG-th group of 64 frames and
+// publishes its own completion word); one launch per burst uses one per 64
+// frames, up to ZC_MAX_WG. More than one CU keeps more PCIe reads in flight
+// than one CU can (a 64-frame burst read by one CU: ~7.5 GB/s).
+constexpr uint32_t ZC_MAX_WG = 16, ZC_RES_WG = 8;
+
 struct alignas(64) ZcMailbox
 {
   alignas(64) uint64_t req[ZC_REQ_WORDS];
   // stop (host -> GPU)
-  alignas(64) uint64_t seq;   // (one-shot form: the posted request)
-  uint64_t stop;
-  uint64_t pad2[6];
-  // completion (GPU -> host)
-  alignas(64) uint64_t done;
-  uint32_t counters[4];  // IPv4, bad IP csum, TCP, bad L4 csum of request `done`
-  uint64_t beat;         // server heartbeat: polls / 1024 (diagnostics)
-  uint64_t seen;         // last doorbell value the server read (diagnostics)
+  alignas(64) uint64_t stop;
+  uint64_t pad2[7];
+  // completion (GPU -> host), per workgroup: the tag of the last request
+  // it finished and that request's counts {IPv4, bad IP csum, TCP, bad L4}
+  alignas(64) uint64_t done[ZC_MAX_WG];
+  uint32_t counters[ZC_MAX_WG][4];
+  // diagnostics (workgroup 0)
+  uint64_t beat;         // server heartbeat: polls / 1024
+  uint64_t seen;         // last doorbell tag the server read
   uint64_t t_req;        // s_memrealtime when the request was picked up
-  uint64_t t_done;       // ... and when its flags were out (diagnostics)
-  uint64_t pad3;
-  // per-frame arrays of the request
+  uint64_t t_done;       // ... and when its flags were out
+  // per-frame arrays of bursts past ZC_REQ_FRAMES
   alignas(64) uint64_t offs[ZC_MAX_FRAMES];
   uint16_t lens[ZC_MAX_FRAMES];
   uint8_t flags[ZC_MAX_FRAMES];

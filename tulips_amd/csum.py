@@ -163,6 +163,7 @@ _SIGNATURES = {
                                                       _vp]),
     "tulips_csum_generate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp]),
     "tulips_csum_validate_frames_zc": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp, _vp]),
+    "tulips_csum_ctx_set_lowlat": (C.c_int, [_vp, C.c_int]),
     "tulips_csum_time_validate": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_uint32,
                                             C.c_uint32, _vp, _vp]),
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
@@ -496,6 +497,12 @@ class HostContext:
         _check(rc, "tulips_csum_validate_frames_zc" if low_latency else
                "tulips_csum_validate_frames_host")
         return (flags, cnt) if with_counters else flags
+
+    def set_lowlat(self, resident: bool):
+        """Low-latency path form: one launch per burst (False) or a resident
+        server (True), tulips_csum_ctx_set_lowlat."""
+        _check(lib.tulips_csum_ctx_set_lowlat(self._h, 1 if resident else 0),
+               "tulips_csum_ctx_set_lowlat")
 
     def generate_frames(self, arena, offsets, lengths):
         """Write both checksum fields of host frames in `arena` (a writable
