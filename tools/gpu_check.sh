@@ -1,14 +1,15 @@
 #!/bin/bash
 # One GPU-box session (run under gpurun): parity tests, smoke, bench, then
-# rocprofv3 evidence for the bench workload — kernel-trace + stats (timing
-# agreement) and separate --pmc passes (FETCH_SIZE, WRITE_SIZE, EA read
-# requests) for HBM traffic. Summarise here afterwards with
+# rocprofv3 evidence for the bench workload - kernel-trace + stats (timing
+# agreement) and separate --pmc passes (FETCH_SIZE, WRITE_SIZE) for HBM
+# traffic - and the world-8 rehearsal (8 gloo ranks sharing GPU 0, every
+# N>1 leg at world 8). Summarise here afterwards with
 #   python tools/pmc_traffic.py gpurun_out/prof_$TAG profiles $TAG
 # Each GPU step has its own time limit; a crash / abort / timeout ends the
 # script (pytest's rc 1 = "tests failed" is reported and also ends it).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r01}
+TAG=${TAG:-r03}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -21,13 +22,14 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
 }
 rocminfo 2>/dev/null | grep -m1 -E "gfx9" || true
-step pytest_gpu 600 python -u -m pytest tests -q -m gpu -x -p no:cacheprovider --timeout 120 --timeout-method thread
+step pytest_gpu 600 python -u -m pytest tests -q -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 300 python bench.py
+step bench 400 python bench.py
 tail -1 $OUT/bench.log > $OUT/bench.json
-step stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python bench.py --no-cpu-baseline
+step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python bench.py --no-cpu-baseline
 python tools/trace_bursts.py $OUT/stats/run_kernel_trace.csv --all > $OUT/bursts_all.jsonl
-step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
-step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
-step pmc_rdreq 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d $OUT/pmc_rdreq -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
+step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
+step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
+step rehearsal_w8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 8 --dist-backend gloo --one-device --steps 64 --warmup 16 --no-cpu-baseline
+tail -1 $OUT/rehearsal_w8.log > $OUT/rehearsal_w8.json
 echo "== done"

@@ -26,22 +26,25 @@ from collections import defaultdict
 
 # (kernel name fragment, grid size or None, workload label): bench.py's
 # default geometries. The ZIPF kernels are also what the host path launches
-# per staging chunk, so ZIPF is told apart by its grid: the split-form span
-# kernel (prefix-only LDS) has one 256-thread workgroup per 24 KiB of the 43,772,673-byte arena
-# (1,782 ranges = 456,192 threads), the any-layout packed kernel 8 segments per wave
+# per staging chunk, so ZIPF is told apart by its grid: the arena span kernel
+# has one 256-thread workgroup per 24 KiB of the 43,772,673-byte arena (1,782
+# ranges = 456,192 threads), the any-layout packed kernel 8 segments per wave
 # (8,192 waves = 524,288 threads).
 WORKLOADS = [
     ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
     ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
-    ("csum_span4_kernel<6, true>", 456192, "ZIPF"),
-    ("csum_packed_kernel<8, 4, true, 1>", 524288, "ZIPF_any_layout"),  # PF = 1
+    ("csum_span_kernel<6>", 456192, "ZIPF"),
+    ("csum_packed_kernel<8, 4, true>", 524288, "ZIPF_any_layout"),
     # 65,536 frames, 16 per 256-thread block (the host path's small bursts
-    # launch the same kernels with smaller grids)
-    ("frame_kernel<false, 16, 6, true>", 1048576, "frames_validate_F1514"),
-    ("frame_kernel<true, 16, 6, true>", 1048576, "frames_generate_F1514"),
+    # launch the same kernels with smaller grids); frame_kernel<OP, ...>:
+    # 0 validate, 1 generate in place, 2 compact fields
+    ("frame_kernel<0, 16, 6, true>", 1048576, "frames_validate_F1514"),
+    ("frame_kernel<1, 16, 6, true>", 1048576, "frames_generate_F1514"),
+    ("frame_kernel<2, 16, 6, true>", 1048576, "frames_generate_fields_F1514"),
     ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
     ("seg_prologue_small_kernel", None, "segment_TSO_64K_mss1460_prologue"),
     ("rss_kernel", None, "rss_toeplitz_16M"),
+    ("stream_tiles_kernel", None, "F9000_read_same_bytes"),
 ]
 # algorithmic bytes per launch (bench.py): segment bytes; frame bytes; bytes
 # read + written by segmentation (super-frames in, segments out); RSS 12 B in
@@ -49,6 +52,8 @@ WORKLOADS = [
 ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673,
               "ZIPF_any_layout": 43772673,
               "frames_validate_F1514": 65536 * 1514, "frames_generate_F1514": 65536 * 1514,
+              "frames_generate_fields_F1514": 65536 * 1514 + 65536 * 4,
+              "F9000_read_same_bytes": 65536 * 9000,
               "segment_TSO_64K_mss1460": 1024 * 64294 + 45056 * 1514,
               "rss_toeplitz_16M": (1 << 24) * 16}
 
