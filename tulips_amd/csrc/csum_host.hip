@@ -1146,19 +1146,23 @@ segment_host(tulips_csum_ctx* ctx, const uint8_t* in_base, const uint64_t* in_of
   uint64_t produced = 0; // segments of the frames before this chunk
   uint32_t i = 0;
   while (i < n) {
-    // frames [i, j) that fit one staging chunk
-    uint64_t bytes = 0;
+    // frames [i, j) that fit one staging chunk, and the most segments they
+    // can make (a frame of L bytes carries at most L payload bytes: at most
+    // ceil(L / mss) segments, at least 1), which bounds the device output
+    uint64_t bytes = 0, most = 0;
     uint32_t j = i;
     while (j < n && j - i < MAX_SEGS_PER_CHUNK && bytes + in_lengths[j] <= ctx->chunk) {
       s.h_offs[j - i] = bytes;
       bytes += in_lengths[j];
+      most += std::max<uint64_t>(1, (uint64_t(in_lengths[j]) + mss - 1) / mss);
       ++j;
     }
     const uint32_t cnt = j - i;
     pack(ctx->pool, s, in_base, in_offsets, in_lengths, i, j);
     memcpy(s.h_lens, in_lengths + i, size_t(cnt) * 2);
-    const uint32_t room =
-      produced >= out_capacity ? 0u : uint32_t(out_capacity - produced);
+    const uint32_t room = produced >= out_capacity
+                            ? 0u
+                            : uint32_t(std::min<uint64_t>(out_capacity - produced, most));
     if (room) {
       uint64_t have_lens = ctx->seg_lens_n * 2;
       if ((e = grow(reinterpret_cast<void**>(&ctx->d_seg_out), &ctx->seg_out_bytes,
