@@ -33,7 +33,7 @@ from collections import defaultdict
 WORKLOADS = [
     ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
     ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
-    ("csum_span_kernel<6>", 456192, "ZIPF"),
+    ("csum_span_kernel<6,", 456192, "ZIPF"),
     ("csum_packed_kernel<8, 4, true>", 524288, "ZIPF_any_layout"),
     # 65,536 frames, 16 per 256-thread block (the host path's small bursts
     # launch the same kernels with smaller grids); frame_kernel<OP, ...>:
