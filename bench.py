@@ -832,9 +832,9 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                   "avg_launch_us": round(t * 1e6, 2),
                   "pipeline": pipe_entry(zb, tp),
                   "entry": "tulips_csum_batch_arena (segments in order in one arena)",
-                  "geometry": "span, split form: a workgroup per 24 KiB of arena bytes, "
+                  "geometry": "span, split form: a workgroup per 28 KiB of arena bytes, "
                               "no halo, chunk prefixes in LDS, boundary chunks loaded by "
-                              "the entry holders; a segment crossing ranges is summed in "
+                              "the entry holders ahead of the range's last rows; a segment crossing ranges is summed in "
                               "parts that meet in a per-range word (one returning atomic "
                               "per part)",
                   "traffic": read_traffic("ZIPF"),

@@ -25,8 +25,8 @@ from tulips_amd import csum  # noqa: E402
 
 DEV = "cuda:0"
 # (chunks per lane, form): the split form, 0 = default (= 7). The library
-# default is 6 chunks per lane (24 KiB ranges).
-GEOMS = ((4, 0), (5, 0), (6, 0), (7, 7), (8, 0))
+# default is 7 chunks per lane (28 KiB ranges).
+GEOMS = ((4, 0), (5, 0), (6, 0), (7, 7), (7, 0), (8, 0))
 
 
 @pytest.fixture(scope="module", autouse=True)

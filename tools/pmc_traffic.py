@@ -27,13 +27,13 @@ from collections import defaultdict
 # (kernel name fragment, grid size or None, workload label): bench.py's
 # default geometries. The ZIPF kernels are also what the host path launches
 # per staging chunk, so ZIPF is told apart by its grid: the arena span kernel
-# has one 256-thread workgroup per 24 KiB of the 43,772,673-byte arena (1,782
-# ranges = 456,192 threads), the any-layout packed kernel 8 segments per wave
+# has one 256-thread workgroup per 28 KiB of the 43,772,673-byte arena (1,527
+# ranges = 390,912 threads), the any-layout packed kernel 8 segments per wave
 # (8,192 waves = 524,288 threads).
 WORKLOADS = [
     ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
     ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
-    ("csum_span_kernel<6,", 456192, "ZIPF"),
+    ("csum_span_kernel<7,", 390912, "ZIPF"),
     ("csum_packed_kernel<8, 4, true>", 524288, "ZIPF_any_layout"),
     # 65,536 frames, 16 per 256-thread block (the host path's small bursts
     # launch the same kernels with smaller grids); frame_kernel<OP, ...>:

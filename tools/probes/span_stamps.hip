@@ -55,8 +55,8 @@ template<int STOP, int MH>
 void
 launch_diag(const SpanArgs& sp, uint32_t grid, uint32_t* sink, hipStream_t st)
 {
-  hipLaunchKernelGGL((csum_span_kernel<6, DiagProbe<STOP>, 8, 1024, MH>), dim3(grid), dim3(256),
-                     0, st, sp, DiagProbe<STOP>{sink});
+  hipLaunchKernelGGL((csum_span_kernel<6, DiagProbe<STOP>, 8, 1024, MH>), dim3(grid),
+                     dim3(256), 0, st, sp, DiagProbe<STOP>{sink});
 }
 
 template<uint32_t NWIN>
@@ -103,35 +103,35 @@ read_shape_kernel(SpanArgs p, uint32_t* sink)
   }
 }
 
-template<uint32_t XC, uint32_t NWIN, int MH = 6, uint32_t HT = 0>
+template<int U, uint32_t XC, uint32_t NWIN, int MH>
 void
 launch_v(const SpanArgs& sp, uint32_t grid, uint64_t* stamps, hipStream_t st)
 {
   if (stamps) {
-    hipLaunchKernelGGL((csum_span_kernel<6, StampProbe, XC, NWIN, MH, HT>), dim3(grid),
-                       dim3(256), 0, st, sp, StampProbe{stamps});
+    hipLaunchKernelGGL((csum_span_kernel<U, StampProbe, XC, NWIN, MH>), dim3(grid), dim3(256),
+                       0, st, sp, StampProbe{stamps});
   } else {
-    hipLaunchKernelGGL((csum_span_kernel<6, NoProbe, XC, NWIN, MH, HT>), dim3(grid), dim3(256),
-                       0, st, sp, NoProbe{});
+    hipLaunchKernelGGL((csum_span_kernel<U, NoProbe, XC, NWIN, MH>), dim3(grid), dim3(256), 0,
+                       st, sp, NoProbe{});
   }
 }
 
 } // namespace
 } // namespace tulips_amd
 
-// One launch of the product kernel at U = 6 with `xc` ranges per XCD run, an
-// `nwin`-entry window and `mh` range chunks issued before the window is
-// counted (8 / 1024 / 6 = the product), with per-wave stamps when
-// `stamps` is not NULL. `slots` must hold `ranges` zeroed words; `stamps`
-// ranges * 4 * 8 uint64.
+// One launch of the product kernel with `u` chunks per lane, `xc` ranges per
+// XCD run, an `nwin`-entry window and `mh` range chunks issued before the
+// window is counted (6 / 8 / 1024 / 3 = the product default), with per-wave
+// stamps when `stamps` is not NULL. `slots` must hold `ranges` zeroed words;
+// `stamps` ranges * 4 * 8 uint64.
 extern "C" int
 span_probe_launch(const uint8_t* base, uint64_t arena, const uint64_t* offs,
                   const uint16_t* lens, uint16_t* out, uint32_t n, uint64_t* slots,
-                  uint64_t nslots, uint32_t salt, uint64_t* stamps, uint32_t xc, uint32_t nwin,
-                  uint32_t mh, uint32_t ht, void* stream)
+                  uint64_t nslots, uint32_t salt, uint64_t* stamps, uint32_t u, uint32_t xc,
+                  uint32_t nwin, uint32_t mh, void* stream)
 {
   using namespace tulips_amd;
-  const uint64_t ranges = span_ranges(base, arena, 4096ull * 6);
+  const uint64_t ranges = span_ranges(base, arena, 4096ull * u);
   if (n == 0 || arena == 0 || ranges > nslots) {
     return 1;
   }
@@ -140,45 +140,18 @@ span_probe_launch(const uint8_t* base, uint64_t arena, const uint64_t* offs,
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const uint32_t g = uint32_t(ranges);
   (void)hipGetLastError();
-  if (ht != 0) {
-    if (xc != 8 || nwin != 1024) {
-      return 1;
-    }
-    const uint32_t key = mh * 100 + ht / 1024;
-    switch (key) {
-    case 304: launch_v<8, 1024, 3, 4096>(sp, g, stamps, st); break;
-    case 308: launch_v<8, 1024, 3, 8192>(sp, g, stamps, st); break;
-    case 604: launch_v<8, 1024, 6, 4096>(sp, g, stamps, st); break;
-    case 608: launch_v<8, 1024, 6, 8192>(sp, g, stamps, st); break;
-    case 312: launch_v<8, 1024, 3, 12288>(sp, g, stamps, st); break;
-    case 612: launch_v<8, 1024, 6, 12288>(sp, g, stamps, st); break;
-    default: return 1;
-    }
-  } else if (mh != 6) {
-    if (xc != 8 || nwin != 1024) {
-      return 1;
-    }
-    switch (mh) {
-    case 2: launch_v<8, 1024, 2>(sp, g, stamps, st); break;
-    case 3: launch_v<8, 1024, 3>(sp, g, stamps, st); break;
-    case 4: launch_v<8, 1024, 4>(sp, g, stamps, st); break;
-    case 5: launch_v<8, 1024, 5>(sp, g, stamps, st); break;
-    default: return 1;
-    }
-  } else if (nwin == 1024) {
-    switch (xc) {
-    case 8: launch_v<8, 1024>(sp, g, stamps, st); break;
-    case 16: launch_v<16, 1024>(sp, g, stamps, st); break;
-    case 32: launch_v<32, 1024>(sp, g, stamps, st); break;
-    case 64: launch_v<64, 1024>(sp, g, stamps, st); break;
-    default: return 1;
-    }
-  } else if (xc == 8 && nwin == 512) {
-    launch_v<8, 512>(sp, g, stamps, st);
-  } else if (xc == 8 && nwin == 2048) {
-    launch_v<8, 2048>(sp, g, stamps, st);
-  } else {
-    return 1;
+  const uint32_t key = u * 1000000 + xc * 10000 + (nwin / 256) * 100 + mh;
+  switch (key) {
+  case 6080406: launch_v<6, 8, 1024, 6>(sp, g, stamps, st); break;
+  case 6080403: launch_v<6, 8, 1024, 3>(sp, g, stamps, st); break;
+  case 6080402: launch_v<6, 8, 1024, 2>(sp, g, stamps, st); break;
+  case 7080402: launch_v<7, 8, 1024, 2>(sp, g, stamps, st); break;
+  case 7080403: launch_v<7, 8, 1024, 3>(sp, g, stamps, st); break;
+  case 7080404: launch_v<7, 8, 1024, 4>(sp, g, stamps, st); break;
+  case 8080403: launch_v<8, 8, 1024, 3>(sp, g, stamps, st); break;
+  case 8080404: launch_v<8, 8, 1024, 4>(sp, g, stamps, st); break;
+  case 7080303: launch_v<7, 8, 768, 3>(sp, g, stamps, st); break;
+  default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

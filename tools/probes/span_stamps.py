@@ -62,18 +62,18 @@ sink = torch.zeros(16, dtype=torch.int32, device=dev)
 sl.span_stamps_ranges.restype = C.c_uint64
 sl.span_stamps_ranges.argtypes = [C.c_void_p, C.c_uint64]
 ranges = max(int(sl.span_stamps_ranges(az.data_ptr() + b * zb, zb)) for b in range(nz))
-slots = torch.zeros(ranges, dtype=torch.int64, device=dev)
+slots = torch.zeros(2 * ranges, dtype=torch.int64, device=dev)  # room for U >= 3
 NL = 16
 stamps = torch.zeros(NL, ranges * 4 * 8, dtype=torch.int64, device=dev)
 
 
-def probe_fn(xc, stamped, nwin=1024, mh=6, ht=0):
+def probe_fn(u, stamped, mh, nwin=1024, xc=8):
     def f(i, st):
         b = i % nz
         sp = stamps[i % NL].data_ptr() if stamped else None
         assert sl.span_probe_launch(az.data_ptr() + b * zb, zb, doffs.data_ptr(),
                                     dlens.data_ptr(), oz.data_ptr() + b * NSEG * 2, NSEG,
-                                    slots.data_ptr(), ranges, 0x5eed, sp, xc, nwin, mh, ht, st) == 0
+                                    slots.data_ptr(), 2 * ranges, 0x5eed, sp, u, xc, nwin, mh, st) == 0
     return f
 
 
@@ -111,13 +111,14 @@ for name, lib in libs:
                                            dlens.data_ptr(), None, None, None,
                                            oz.data_ptr() + b * NSEG * 2, NSEG, 0, st) == 0
     cands.append((name, fz))
-cands.append(("probe_mh3", probe_fn(8, False, 1024, 3)))
-for mh, ht in ((3, 8192), (3, 12288), (6, 12288)):
-    cands.append((f"probe_mh{mh}_ht{ht}", probe_fn(8, False, 1024, mh, ht)))
-for nwin in (1024,):
-    cands.append((f"read_win{nwin}", read_fn(nwin)))
+for u, mh, nwin, xc in ((6, 6, 1024, 8), (6, 3, 1024, 8), (6, 2, 1024, 8), (7, 2, 1024, 8),
+                        (7, 3, 1024, 8), (7, 4, 1024, 8), (8, 3, 1024, 8), (8, 4, 1024, 8),
+                        (7, 3, 768, 8)):
+    cands.append((f"u{u}_mh{mh}_w{nwin}_xc{xc}", probe_fn(u, False, mh, nwin, xc)))
+cands.append(("read_win1024", read_fn(1024)))
 ab = {}
-for rnd in range(3):
+ROUNDS = int(os.environ.get("ROUNDS", "3"))
+for rnd in range(ROUNDS):
     for name, fz in cands:
         oz.zero_()
         for i in range(nz):
@@ -130,13 +131,13 @@ for rnd in range(3):
         print(f"round {rnd} {name:12s}: serial {ts * 1e6:6.2f} us  4-branch {tp * 1e6:6.2f} us "
               f"parity {'ok' if ok else 'MISMATCH'}", flush=True)
 out["ab"] = ab
-out["ab_median"] = {k: {"serial": sorted(x[0] for x in v)[1], "branch4": sorted(x[1] for x in v)[1],
+out["ab_median"] = {k: {"serial": float(np.median([x[0] for x in v])),
+                        "branch4": float(np.median([x[1] for x in v])),
                         "parity": all(x[2] for x in v)} for k, v in ab.items()}
 
 # 2. stamps (the product body, and with MH = 3)
-STAMP_MH = int(os.environ.get("STAMP_MH", "6"))
-STAMP_HT = int(os.environ.get("STAMP_HT", "0"))
-fs = probe_fn(8, True, 1024, STAMP_MH, STAMP_HT)
+STAMP_MH = int(os.environ.get("STAMP_MH", "3"))
+fs = probe_fn(6, True, STAMP_MH)
 oz.zero_()
 stamps.zero_()
 
@@ -174,7 +175,9 @@ out["stamped"] = {"us_per_launch_serial_graph": round(t_stamped * 1e6, 3), "pari
 for L in launches[nz:nz + 3]:
     print(json.dumps(L), flush=True)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-with open(os.path.join(ROOT, "gpurun_out", f"span_stamps_mh{STAMP_MH}_ht{STAMP_HT}.json"), "w") as f:
+with open(os.path.join(ROOT, "gpurun_out", f"span_stamps_mh{STAMP_MH}.json"), "w") as f:
     json.dump(out, f, indent=1)
+for k, v in out["ab_median"].items():
+    print(f"median {k:22s} serial {v['serial']:6.2f}  4-branch {v['branch4']:6.2f}")
 print(json.dumps({"ab": ab, "stamped_us": out["stamped"]["us_per_launch_serial_graph"],
                   "parity": ok}))

@@ -138,11 +138,6 @@ tulips_csum_tcp_host(uint32_t src, uint32_t dst, uint16_t len,
 // ---------------------------------------------------------------------------
 namespace {
 
-// KIND_SPAN chunks per lane: 24 KiB per workgroup range, split form with
-// the chunk prefixes in LDS (tools/probe_gen.py, profiles/probe_split_r02.txt:
-// ZIPF 11.2-11.3 us serial and 7.9-8.0 us per launch with 4 launches in
-// flight, against 11.4-11.5 / 8.3-8.7 for the staged split form)
-constexpr int SPAN_DEFAULT_UNROLL = 6;
 
 thread_local char last_error[160] = "";
 

@@ -47,9 +47,6 @@ namespace {
 constexpr uint64_t DEFAULT_CHUNK = 16ull << 20;
 constexpr uint32_t MAX_SEGS_PER_CHUNK = 1u << 20;
 constexpr int NSLOTS = 3;
-// KIND_SPAN chunks per lane for in-order staged chunks (csum_capi.hip; the
-// default split form)
-constexpr int SPAN_UNROLL = 6;
 // Staging-copy threads: the CPUs this process may run on, at most 16 (a GPU's
 // share of a host; 16 threads took pageable F1500 from 37 to 44 GiB/s over 8
 // on the MI355X box, alternating builds).
@@ -672,7 +669,7 @@ run(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
       if (arena_ok) {
         // segments in order in the staged bytes: work cut by bytes
         a.kind = TULIPS_CSUM_KIND_SPAN;
-        a.unroll = SPAN_UNROLL;
+        a.unroll = tulips_amd::SPAN_DEFAULT_UNROLL;
         a.group = 0;
         TCS_Q(launch_span(dbase, hbytes, s.d_offs, s.d_lens, a, st));
       } else {

@@ -47,6 +47,11 @@ hipError_t launch_var(const uint8_t* base, const uint64_t* offs,
 // Whether launch_span has a kernel for (unroll, group) (checked on the CPU
 // before any HIP call).
 bool span_geometry_ok(int unroll, int group);
+// Chunks per lane of the default arena geometry: 28 KiB per workgroup range
+// (tools/probes/span_stamps.py, profiles/probe_span_geometry_r03.txt: ZIPF
+// 11.3 us serial and 7.8 us per launch on 4 branches, against 11.5 / 8.0 at
+// 6 and 11.6 / 8.0 at 8).
+constexpr int SPAN_DEFAULT_UNROLL = 7;
 // In-order arena (KIND_SPAN): segments lie in order in [base, base + arena);
 // a.unroll = chunks per lane (4 KiB of arena per workgroup each), a.group the
 // form (include/tulips_csum_util.h).

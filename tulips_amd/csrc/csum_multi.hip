@@ -654,7 +654,7 @@ run_piece(const Job& J, const Piece& pc, const uint8_t* local, const uint64_t* o
   a.n = cnt;
   a.mode = J.mode;
   a.kind = 5; // TULIPS_CSUM_KIND_SPAN
-  a.unroll = 6;
+  a.unroll = tulips_amd::SPAN_DEFAULT_UNROLL;
   a.group = 0;
   a.nontemporal = true;
   a.offs_bias = pc.lo;

@@ -30,11 +30,13 @@ namespace {
 //     counts over the window give the segments starting in the range
 //     [lo, hi) (a 256-ary search by wave 0 when the window misses);
 //   * only the row-wise wave scans of the chunks' 16-bit-half sums (v_dot2)
-//     live in LDS (4 B per chunk), so seven workgroups share a CU (registers
-//     bounded to 7 waves per SIMD) and a ZIPF launch (1,782 ranges) is one
-//     generation. A segment's two boundary chunks are loaded by the thread
-//     holding its window entry as soon as the window is in, while the range's
-//     own loads (temporal: the lines are in L2 or in flight) are outstanding;
+//     live in LDS (4 B per chunk), so at least seven workgroups share a CU
+//     (registers bounded to 7 waves per SIMD) and a ZIPF launch (1,527
+//     ranges of 28 KiB) is one generation. A segment's two boundary chunks
+//     are loaded by the thread holding its window entry as soon as the
+//     window is in, between the range's first U / 3 rows and the rest
+//     (temporal: the lines are in L2 or in flight), so they arrive before
+//     the range's last rows and cost no round trip after the data;
 //   * a segment crossing range boundaries is summed in parts: every range it
 //     touches adds its part (folded with end-around carry, so zero iff its
 //     bytes are) and an arrival to ONE 64-bit word, its first range's, by a
@@ -69,13 +71,10 @@ struct NoProbe
 
 // XC: consecutive ranges kept on one XCD (xcd_block_c); NWIN: entries of the
 // speculative offsets window; MH: range chunks per lane issued before the
-// window is counted (the rest after the boundary chunks); HT (a multiple of
-// 4 KiB): a segment that starts in the range and ends at most HT bytes past
-// it is finished by the range, whose threads load its bytes past the range
-// (HT / 4 KiB chunks each), instead of meeting its next part in a word (0 =
-// never). The product uses NoProbe, 8, 1024, U and 0.
-template<int U, class Probe = NoProbe, uint32_t XC = 8, uint32_t NWIN = 1024, int MH = U,
-         uint32_t HT = 0>
+// window is counted (the rest after the boundary chunks, which then arrive
+// before the range's last rows). The product uses NoProbe, 8, 1024 and U / 3
+// (tools/probes/span_stamps.py, profiles/probe_span_geometry_r03.txt).
+template<int U, class Probe = NoProbe, uint32_t XC = 8, uint32_t NWIN = 1024, int MH = U / 3>
 __global__ __launch_bounds__(256, 7) void
 csum_span_kernel(SpanArgs p, Probe pr)
 {
@@ -87,19 +86,12 @@ csum_span_kernel(SpanArgs p, Probe pr)
   __shared__ uint32_t s_woff[4][4 * U];
   __shared__ uint32_t s_cnt[8];
   __shared__ uint32_t s_meta[2];
-  __shared__ uint32_t s_tl;      // HT: bytes past the range of the segment finished here
-  __shared__ uint32_t s_tail[4]; // HT: their per-wave sums
 
   const uint32_t t = threadIdx.x, lane = t & 63u;
   const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t k = xcd_block_c<XC>(blockIdx.x, gridDim.x);
   pr.mark(k, w, lane, 0);
-  constexpr int TQ = int(HT / 4096u);
-  if constexpr (TQ > 0) {
-    if (t == 0) {
-      s_tl = 0; // (published by the first barrier)
-    }
-  }
+
   const uintptr_t b = reinterpret_cast<uintptr_t>(p.base);
   const uint64_t d = b & 15u;
   const uintptr_t A = b & ~uintptr_t(15);
@@ -178,9 +170,6 @@ csum_span_kernel(SpanArgs p, Probe pr)
       if (lo > 0 && i == lo - 1) {
         const uintptr_t ie = min(b + wo[r] + wl[r], aend);
         a = ie > x0;
-        if constexpr (HT > 0) { // finished by the previous range
-          a = a && !(b + wo[r] >= x0 - W && ie <= x0 + HT);
-        }
       }
       if (a) {
         act = true;
@@ -204,45 +193,13 @@ csum_span_kernel(SpanArgs p, Probe pr)
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  // HT: the segment crossing the range end, when it ends within HT bytes
-  // past it, is finished here: its holder publishes how far, and every
-  // thread loads TQ chunks of those bytes (zeros past them)
-  const bool town = TQ > 0 && act && sa >= x0 && se > x1 && se <= x1 + HT;
-  uint32_t tl = 0;
-  u32x4 tv[TQ > 0 ? TQ : 1];
-  if constexpr (TQ > 0) {
-    if (town) {
-      s_tl = uint32_t(se - x1);
-    }
-    lds_barrier();
-    tl = s_tl;
-#pragma unroll
-    for (int q = 0; q < TQ; ++q) {
-      const uint32_t o = 16u * (t + 256u * uint32_t(q));
-      tv[q] = load_chunk<false>(reinterpret_cast<gchunk_ptr>(o < tl ? x1 + o : zero));
-    }
-  }
   // MH < U: the boundary chunks arrive before the range's last rows, so
   // their masked sums are taken now and the chunks do not stay live through
-  // the scans; likewise the tail's sum
+  // the scans
   uint32_t bsum = 0;
   if constexpr (MH < U) {
     const int ha = int(u0 & 15u), tb = int(((u1 - 1) & 15u) + 1u);
     bsum = ca == ce ? masked_value(bh, ha, tb) : masked_value(bh, ha, 16) + masked_value(bt, 0, tb);
-  }
-  if constexpr (TQ > 0) { // this thread's share of the tail, summed per wave
-    uint32_t x = 0;
-#pragma unroll
-    for (int q = 0; q < TQ; ++q) {
-      const uint32_t o = 16u * (t + 256u * uint32_t(q));
-      if (o < tl) {
-        x += o + 16u > tl ? masked_value(tv[q], 0, int(tl - o)) : chunk_value(tv[q]);
-      }
-    }
-    x = wave_incl_scan(x);
-    if (lane == 63) {
-      s_tail[w] = x; // (published by the scans' barrier)
-    }
   }
   if constexpr (Probe::stop == 1) { // loads and window only
     uint32_t x = bh.x ^ bt.y;
@@ -273,10 +230,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
   }
   pr.mark(k, w, lane, 3);
   auto P = [&](uint32_t c) { return s_woff[w][c >> 6] + s_sc[c]; };
-  uint32_t tsum = 0;
-  if constexpr (TQ > 0) {
-    tsum = town ? s_tail[0] + s_tail[1] + s_tail[2] + s_tail[3] : 0u;
-  }
+
   if constexpr (Probe::stop == 2) { // + scans
     pr.keep(P(t) ^ bh.x ^ bt.y);
     return;
@@ -306,9 +260,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
     // a part goes to a word only for a segment starting inside the arena
     // whose first range has one (always, under the arena contract)
     const uint64_t ra = (sa - A) / W;
-    const bool whole = HT > 0 && sa >= x0 && se > x1 && se <= x1 + HT; // tail added by caller
-    const bool split =
-      act && !whole && (sa < x0 || se > x1) && sa >= A && sa < se && ra < p.nslots;
+    const bool split = act && (sa < x0 || se > x1) && sa >= A && sa < se && ra < p.nslots;
     bool done = act && !split;
     uint32_t r = finish(sum, (sa & 1u) != 0, p.mode, side.seed, side.src, side.dst, sl);
     if constexpr (Probe::stop == 3) { // + every part stored as a result, no atomics
@@ -373,9 +325,9 @@ csum_span_kernel(SpanArgs p, Probe pr)
   if (fast) {
     if (__builtin_amdgcn_ballot_w64(act) != 0) {
       if constexpr (MH < U) {
-        emit(s, act, sa, se, sl, has ? bsum + (ca == ce ? 0u : P(ce - 1) - P(ca)) + tsum : 0u);
+        emit(s, act, sa, se, sl, has ? bsum + (ca == ce ? 0u : P(ce - 1) - P(ca)) : 0u);
       } else {
-        emit(s, act, sa, se, sl, has ? part_of(u0, u1, ca, ce, bh, bt) + tsum : 0u);
+        emit(s, act, sa, se, sl, has ? part_of(u0, u1, ca, ce, bh, bt) : 0u);
       }
     }
     pr.mark(k, w, lane, 5);
@@ -422,37 +374,6 @@ csum_span_kernel(SpanArgs p, Probe pr)
     L = s_meta[0];
     H = s_meta[1];
   }
-  uint32_t stail = 0; // HT: the sum past the range of the segment H - 1 finishes here
-  if constexpr (TQ > 0) {
-    if (t == 0) {
-      uint32_t v = 0;
-      if (H > L) {
-        const uintptr_t ia = b + (p.offs[H - 1] - p.bias);
-        const uintptr_t ie = min(ia + p.lens[H - 1], aend);
-        if (ia >= x0 && ie > x1 && ie <= x1 + HT) {
-          v = uint32_t(ie - x1);
-        }
-      }
-      s_tl = v;
-    }
-    lds_barrier();
-    const uint32_t stl = s_tl;
-    uint32_t x = 0;
-#pragma unroll
-    for (int q = 0; q < TQ; ++q) {
-      const uint32_t o = 16u * (t + 256u * uint32_t(q));
-      const u32x4 c = load_chunk<false>(reinterpret_cast<gchunk_ptr>(o < stl ? x1 + o : zero));
-      if (o < stl) {
-        x += o + 16u > stl ? masked_value(c, 0, int(stl - o)) : chunk_value(c);
-      }
-    }
-    x = wave_incl_scan(x);
-    if (lane == 63) {
-      s_tail[w] = x;
-    }
-    lds_barrier();
-    stail = s_tail[0] + s_tail[1] + s_tail[2] + s_tail[3];
-  }
   for (uint32_t s0 = L > 0 ? L - 1 : 0; s0 < H; s0 += 256u) {
     const uint32_t i = s0 + t;
     bool a = i < H;
@@ -461,9 +382,6 @@ csum_span_kernel(SpanArgs p, Probe pr)
     const uintptr_t ia = b + o, ie = min(b + o + l, aend);
     if (i < L) {
       a = a && ie > x0;
-      if constexpr (HT > 0) { // finished by the previous range
-        a = a && !(ia >= x0 - W && ie <= x0 + HT);
-      }
     }
     const uintptr_t v0 = max(ia, x0), v1 = min(ie, x1);
     const bool h = a && v1 > v0;
@@ -471,9 +389,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
     const uint32_t qe = h ? uint32_t((v1 - 1 - x0) >> 4) : 0u;
     const u32x4 ch = load_chunk<false>(chunk_at(x0 + 16u * qa));
     const u32x4 ct = load_chunk<false>(chunk_at(x0 + 16u * qe));
-    const uint32_t tail = a && ia >= x0 && ie > x1 && ie <= x1 + HT ? stail : 0u;
-    emit(i, a, a ? ia : b, a ? ie : b, a ? l : 0u,
-         h ? part_of(v0, v1, qa, qe, ch, ct) + tail : 0u);
+    emit(i, a, a ? ia : b, a ? ie : b, a ? l : 0u, h ? part_of(v0, v1, qa, qe, ch, ct) : 0u);
   }
   pr.mark(k, w, lane, 5);
 }
