@@ -19,6 +19,7 @@ namespace {
 struct StampProbe
 {
   static constexpr int stop = 0;
+  static constexpr bool data_mark = false;
   uint64_t* buf;
   __device__ __forceinline__ void keep(uint32_t) const {}
   __device__ __forceinline__ void mark(uint32_t k, uint32_t w, uint32_t lane, int point) const
@@ -41,6 +42,7 @@ template<int STOP>
 struct DiagProbe
 {
   static constexpr int stop = STOP;
+  static constexpr bool data_mark = false;
   uint32_t* sink;
   __device__ __forceinline__ void mark(uint32_t, uint32_t, uint32_t, int) const {}
   __device__ __forceinline__ void keep(uint32_t x) const

@@ -40,13 +40,17 @@ namespace {
 //   * a segment crossing range boundaries is summed in parts: every range it
 //     touches adds its part (folded with end-around carry, so zero iff its
 //     bytes are) and an arrival to ONE 64-bit word, its first range's, by a
-//     returning agent-scope compare-and-swap (executed at the memory side, so
-//     no cross-XCD fence); the arrival that completes the count finishes the
-//     segment and zeroes the word. No workgroup ever waits for another.
+//     returning agent-scope atomic (executed at the memory side, so no
+//     cross-XCD fence); the arrival that completes the count finishes the
+//     segment. A two-part segment (every segment shorter than a range) uses
+//     one exchange per part and leaves its word as it is; longer ones
+//     compare-and-swap and zero the word at the end. No workgroup ever waits
+//     for another.
 // Words (stream_state.h span_slots) are tagged with the launch's AQL dispatch
-// id (per-queue packet index: distinct for every launch and every graph
-// replay on a queue), so a word left behind by a batch breaking the arena
-// contract is taken over, never added to. A split part is only sent to a word
+// id (per-queue packet index, 40 bits kept: distinct for every launch and
+// every graph replay on a queue until 2^40 dispatches), so a word left by an
+// earlier launch is never taken for a part of this one: it is overwritten,
+// never added to. A split part is only sent to a word
 // when the segment starts inside the arena and its range has a word;
 // otherwise (contract broken) it is finished locally with an undefined
 // result. Contract (include/tulips_csum.h): offsets[i] + lengths[i] <=
@@ -55,9 +59,11 @@ namespace {
 // ---------------------------------------------------------------------------
 extern "C" __device__ uint64_t llvm_amdgcn_dispatch_id() __asm("llvm.amdgcn.dispatch.id");
 
-// Split word: tag (32) | arrivals before the last (4) | sum of parts (28).
-constexpr uint32_t WORD_ARR_SHIFT = 28;
+// Split word: tag (40) | arrivals before the last (4) | sum of parts (20;
+// at most 15 parts of at most 0xffff each before the last).
+constexpr uint32_t WORD_ARR_SHIFT = 20, WORD_TAG_SHIFT = 24;
 constexpr uint64_t WORD_SUM_MASK = (1ull << WORD_ARR_SHIFT) - 1;
+constexpr uint64_t WORD_TAG_MASK = (1ull << 40) - 1;
 
 // The product's probe: no marks. tools/probes/span_stamps.hip instantiates
 // the same kernel with a probe that records per-wave realtime stamps at
@@ -65,6 +71,7 @@ constexpr uint64_t WORD_SUM_MASK = (1ull << WORD_ARR_SHIFT) - 1;
 struct NoProbe
 {
   static constexpr int stop = 0; // diagnostic builds stop after phase 1/2/3
+  static constexpr bool data_mark = false; // stamp when the wave's loads are in
   __device__ __forceinline__ void mark(uint32_t, uint32_t, uint32_t, int) const {}
   __device__ __forceinline__ void keep(uint32_t) const {}
 };
@@ -74,7 +81,12 @@ struct NoProbe
 // window is counted (the rest after the boundary chunks, which then arrive
 // before the range's last rows). The product uses NoProbe, 8, 1024 and U / 3
 // (tools/probes/span_stamps.py, profiles/probe_span_geometry_r03.txt).
-template<int U, class Probe = NoProbe, uint32_t XC = 8, uint32_t NWIN = 1024, int MH = U / 3>
+// XCHG: a segment in two parts (always, when its length is below the range
+// size) meets its other part by one exchange per part, and the word is not
+// re-zeroed: the next launch's tag differs (profiles/probe_span_early_r03.txt:
+// 0.2-0.4 us per ZIPF launch against compare-and-swap + re-zero).
+template<int U, class Probe = NoProbe, uint32_t XC = 8, uint32_t NWIN = 1024, int MH = U / 3,
+         bool XCHG = true>
 __global__ __launch_bounds__(256, 7) void
 csum_span_kernel(SpanArgs p, Probe pr)
 {
@@ -211,6 +223,10 @@ csum_span_kernel(SpanArgs p, Probe pr)
     return;
   }
 
+  if constexpr (Probe::data_mark) { // stamps only: when all of the wave's loads are in
+    __builtin_amdgcn_s_waitcnt(0x0f70); // vmcnt(0)
+    pr.mark(k, w, lane, 6);
+  }
   // 3. row-wise wave scans of the range's chunk values
 #pragma unroll
   for (uint32_t j = 0; j < U; ++j) {
@@ -242,7 +258,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
   //    the compare-and-swap makes its round trip)
   const uint32_t want = (p.mode & FLAG_COMPLEMENT) ? 0u : 0xffffu;
   const bool side_in = (p.mode & MODE_MASK) == MODE_TCP || p.seeds != nullptr;
-  const uint32_t tag = uint32_t(llvm_amdgcn_dispatch_id()) ^ p.salt;
+  const uint64_t tag = (llvm_amdgcn_dispatch_id() ^ p.salt) & WORD_TAG_MASK;
   auto store = [&](uint32_t s, uint32_t r) {
     if (p.out) {
       if (p.nt_store) {
@@ -277,14 +293,26 @@ csum_span_kernel(SpanArgs p, Probe pr)
       if (split) {
         const uint32_t need = uint32_t((se - 1 - A) / W - ra); // arrivals before the last
         const uint32_t part = fold32(sum);
-        const uint64_t mine = (uint64_t(tag) << 32) | (1ull << WORD_ARR_SHIFT) | part;
+        const uint64_t mine = (tag << WORD_TAG_SHIFT) | (1ull << WORD_ARR_SHIFT) | part;
         unsigned long long* wp = reinterpret_cast<unsigned long long*>(p.slots + ra);
-        unsigned long long seen = atomicCAS(wp, 0ull, mine);
+        unsigned long long seen = 0;
+        if (XCHG && need == 1) {
+          // two parts: the one that finds the other's part (this launch's
+          // tag, an arrival counted) is last; the word keeps residue
+          seen = atomicExch(wp, mine);
+          if ((seen >> WORD_TAG_SHIFT) == tag && ((seen >> WORD_ARR_SHIFT) & 0xfu) != 0) {
+            done = true;
+            sum = uint32_t(seen & WORD_SUM_MASK) + part;
+          }
+          seen = 0;
+        } else {
+          seen = atomicCAS(wp, 0ull, mine);
+        }
         // every failed exchange means another arrival changed the word: the
         // loop ends after at most as many rounds as the segment has parts
         for (int round = 0; seen != 0 && round < 64; ++round) {
           unsigned long long next;
-          if (uint32_t(seen >> 32) != tag) {
+          if ((seen >> WORD_TAG_SHIFT) != tag) {
             next = mine; // residue of an earlier launch: taken over
           } else if (uint32_t((seen >> WORD_ARR_SHIFT) & 0xfu) == need) {
             done = true;

@@ -50,16 +50,17 @@ struct StreamState
   void* seg_desc = nullptr; // 16 B per input frame
   uint64_t seg_ndesc = 0;
 
-  // SPAN split-form words (csum_kernels.hip csum_span_kernel): one 64-bit
-  // word per arena range, zero again after every launch of a batch that
-  // keeps the arena contract, and tagged with the launch's dispatch id so
-  // that residue of one that does not is never added to. The calls one
+  // SPAN split-form words (span_kernel.h csum_span_kernel): one 64-bit word
+  // per arena range, tagged with the launch's dispatch id, so a word left by
+  // an earlier launch (two-part segments leave theirs as they are) is never
+  // added to. The calls one
   // capture records on this stream run in order in the graph, so they share
   // one array (a spare, or made in relaxed capture mode), owned by the graph
   // from then on and salted apart from other arrays
   uint32_t span_salt = 0;
   uint64_t* span_slots = nullptr;
   uint64_t span_nslots = 0;
+  uint64_t span_calls = 0; // direct arena calls (the words are re-zeroed every 2^20)
   std::vector<uint64_t*> span_spare;
   std::vector<uint64_t*> span_owned;
   struct Capture

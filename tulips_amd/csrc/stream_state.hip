@@ -209,6 +209,15 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64
       s.span_nslots = want;
       s.span_spare.assign(made.begin() + 1, made.end());
     }
+    // words keep the tags of earlier launches (span_kernel.h): zeroed every
+    // 2^20 direct calls, so no word outlives that many calls of this stream
+    // (a tag only repeats after 2^40 dispatches on the stream's queue)
+    if ((++s.span_calls & ((1u << 20) - 1)) == 0) {
+      const hipError_t e = hipMemsetAsync(s.span_slots, 0, s.span_nslots * 8, s.stream);
+      if (e != hipSuccess) {
+        return e;
+      }
+    }
     *out = s.span_slots;
     *nslots = s.span_nslots;
     *salt = 0;
