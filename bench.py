@@ -467,42 +467,47 @@ def mctx_device_leg(torch, dist, csum, cdev, rank, world, args):
     devs = [0] * world if args.one_device else list(range(world))
     res = {}
     if rank == 0:
-        n = world * SHARD_SEGMENTS
-        d0 = torch.device("cuda", 0)
-        with torch.cuda.device(d0):
-            arena = torch.empty(n * SEG + 64, dtype=torch.uint8, device=d0)
-            csum.fill_splitmix(arena, n * SEG, seed=DATA_SEED)
-            out = torch.empty(n, dtype=torch.uint16, device=d0)
-            st = torch.cuda.current_stream(d0)
-            with csum.MultiContext(devs, chunk_bytes=1 << 20) as m:
-                m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)   # buffers made
-                st.synchronize()
-                best = None
-                for _ in range(3):
+        # rank 0 alone works here: an error must still reach the barrier below,
+        # or the other ranks would meet rank 0's next collective there
+        try:
+            n = world * SHARD_SEGMENTS
+            d0 = torch.device("cuda", 0)
+            with torch.cuda.device(d0):
+                arena = torch.empty(n * SEG + 64, dtype=torch.uint8, device=d0)
+                csum.fill_splitmix(arena, n * SEG, seed=DATA_SEED)
+                out = torch.empty(n, dtype=torch.uint16, device=d0)
+                st = torch.cuda.current_stream(d0)
+                with csum.MultiContext(devs, chunk_bytes=1 << 20) as m:
+                    m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)   # buffers made
                     st.synchronize()
-                    t0 = time.perf_counter()
-                    m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)
-                    st.synchronize()
-                    t = time.perf_counter() - t0
-                    best = t if best is None else min(best, t)
-                bounds = m.bounds().tolist()
-            o = out.cpu().numpy().view(np.uint16)
-        gold = golden_digests().get("M8x1500", {})
-        shards = gold.get("shards", [])
-        ok = all(fnv1a_u16(o[k * SHARD_SEGMENTS:(k + 1) * SHARD_SEGMENTS]) ==
-                 shards[k]["fnv1a64"] for k in range(min(world, len(shards))))
-        if world == 8:
-            ok = ok and fnv1a_u16(o) == gold.get("fnv1a64")
-        nbytes = float(n) * SEG
-        res = {"entry": "tulips_csum_mctx_batch_fixed_device (one process, devices "
-                        f"{devs})",
-               "workload": f"{n:,} x 1500 B resident on GPU 0 ({nbytes / 1e9:.2f} GB)",
-               "bytes_pulled_by_peers": int(nbytes * (world - 1) / world),
-               "ms": round(best * 1e3, 3),
-               "value_exchange_inclusive_GiBps": round(nbytes / best / GIB, 2),
-               "shard_bounds": bounds,
-               "parity": "ok" if ok else "MISMATCH"}
-        del arena, out
+                    best = None
+                    for _ in range(3):
+                        st.synchronize()
+                        t0 = time.perf_counter()
+                        m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)
+                        st.synchronize()
+                        t = time.perf_counter() - t0
+                        best = t if best is None else min(best, t)
+                    bounds = m.bounds().tolist()
+                o = out.cpu().numpy().view(np.uint16)
+            gold = golden_digests().get("M8x1500", {})
+            shards = gold.get("shards", [])
+            ok = all(fnv1a_u16(o[k * SHARD_SEGMENTS:(k + 1) * SHARD_SEGMENTS]) ==
+                     shards[k]["fnv1a64"] for k in range(min(world, len(shards))))
+            if world == 8:
+                ok = ok and fnv1a_u16(o) == gold.get("fnv1a64")
+            nbytes = float(n) * SEG
+            res = {"entry": "tulips_csum_mctx_batch_fixed_device (one process, devices "
+                            f"{devs})",
+                   "workload": f"{n:,} x 1500 B resident on GPU 0 ({nbytes / 1e9:.2f} GB)",
+                   "bytes_pulled_by_peers": int(nbytes * (world - 1) / world),
+                   "ms": round(best * 1e3, 3),
+                   "value_exchange_inclusive_GiBps": round(nbytes / best / GIB, 2),
+                   "shard_bounds": bounds,
+                   "parity": "ok" if ok else "MISMATCH"}
+            del arena, out
+        except Exception as e:  # noqa: BLE001 - reported, never hidden
+            res = {"error": f"{type(e).__name__}: {e}"}
     dist.barrier()
     import json as _json
     return _json.loads(gather_strings(_json.dumps(res), dist)[0])
