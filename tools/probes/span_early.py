@@ -24,7 +24,7 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
 stream = torch.cuda.current_stream()
 timer = bench.Timer(torch, stream)
-sl = C.CDLL(os.path.join(HERE, "libspan_early.so"))
+sl = C.CDLL(os.path.join(HERE, os.environ.get("SPAN_LIB", "libspan_early.so")))
 sl.span_early_launch.restype = C.c_int
 sl.span_early_launch.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
