@@ -123,6 +123,34 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
 {
   return xcd_block_c<8>(b, nb);
 }
+
+// Sum of x over each aligned G-lane subgroup of the wave (G = 16, 32 or 64),
+// returned to every lane of it, without the LDS crossbar. Four DPP row
+// rotations (row_ror 8, 4, 2, 1) fold each 16-lane row in VALU; wider
+// subgroups add the row totals read with readlane. A __shfl_xor butterfly
+// compiles to ds_bpermute_b32, one dependent LDS round trip per step (five
+// at G = 32), and that chain sits between a subgroup's last load and its
+// result store. Every lane of a subgroup must be active (or none).
+template<int G>
+__device__ __forceinline__ uint32_t subgroup_total(uint32_t x)
+{
+  static_assert(G == 16 || G == 32 || G == 64, "rows of 16 lanes");
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x128, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x124, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x122, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x121, 0xf, 0xf, false));
+  if constexpr (G == 16) {
+    return x;
+  } else {
+    const uint32_t r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
+    if constexpr (G == 32) {
+      return (threadIdx.x & 32u) ? r2 + r3 : r0 + r1;
+    } else {
+      return (r0 + r1) + (r2 + r3);
+    }
+  }
+}
 #endif
 
 }

@@ -116,11 +116,15 @@ template<int G>
 __device__ __forceinline__ uint32_t
 subgroup_sum(uint32_t x)
 {
+  if constexpr (G >= 16) {
+    return subgroup_total<G>(x);
+  } else {
 #pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) {
-    x += __shfl_xor(x, m, 64);
+    for (int m = G / 2; m >= 1; m >>= 1) {
+      x += __shfl_xor(x, m, 64);
+    }
+    return x;
   }
-  return x;
 }
 
 struct FixedSegs
