@@ -332,25 +332,45 @@ frame_header(const FrameChunks<G, U>& fc, uint32_t flen, int sub0)
 }
 
 // This lane's LE dword sum of the bytes at chunk-relative offsets [lo, hi)
-// (offsets from a0; the range must lie inside the frame). Bytes beyond the
-// G*U chunks held in registers are loaded by a trailing lane_sum (jumbo).
-template<int G, int U, bool NT>
+// (offsets from a0; the range must lie inside the frame). Only the first UM
+// rows of registers are looked at: a range known to end inside them (the
+// IPv4 header, UM = 1) skips the others at compile time. With UM == U,
+// bytes beyond the G*U chunks held in registers are loaded by a trailing
+// lane_sum (jumbo). Branch-free: the range's chunks are added whole by a
+// select, then the lanes holding its first and last chunk subtract the
+// bytes of those chunks that lie outside it (a per-chunk mask under a
+// branch per chunk cost ~2x the instructions, most of them exec-mask
+// bookkeeping, between a frame's last load and its flags).
+template<int G, int U, bool NT, int UM = U>
 __device__ __forceinline__ uint64_t
 range_sum(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
 {
+  static_assert(UM >= 1 && UM <= U, "rows");
+  const int clo = lo >> 4, chi = (hi - 1) >> 4;
   uint64_t acc = 0;
+  u32x4 vlo = fc.v[0], vhi = fc.v[0];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int b = 16 * (lane + u * G);
-    const int l = max(lo - b, 0), h = min(hi - b, 16);
-    if (l < h) {
-      acc += (l == 0 && h == 16) ? hsum(fc.v[u]) : masked_hsum(fc.v[u], l, h);
+  for (int u = 0; u < UM; ++u) {
+    const int c = lane + u * G;
+    acc += (c >= clo && c <= chi) ? hsum(fc.v[u]) : 0ull;
+    if (u > 0) {
+      vlo = clo / G == u ? fc.v[u] : vlo;
+      vhi = chi / G == u ? fc.v[u] : vhi;
     }
   }
-  constexpr int held = 16 * G * U;
-  if (hi > held) {
-    const int from = max(lo, held);
-    acc += lane_sum<G, U, NT>(fc.a0 + uintptr_t(from), uint32_t(hi - from), lane);
+  const int l = lo & 15, h = hi & 15;
+  if (l != 0 && lane == (clo & (G - 1)) && clo < G * UM) {
+    acc -= masked_hsum(vlo, 0, l);
+  }
+  if (h != 0 && lane == (chi & (G - 1)) && chi < G * UM) {
+    acc -= masked_hsum(vhi, h, 16);
+  }
+  if constexpr (UM == U) {
+    constexpr int held = 16 * G * U;
+    if (hi > held) {
+      const int from = max(lo, held);
+      acc += lane_sum<G, U, NT>(fc.a0 + uintptr_t(from), uint32_t(hi - from), lane);
+    }
   }
   return acc;
 }

@@ -113,7 +113,7 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
     const int h0 = fc.h0;
     const bool do_l4 = h.tcp && !h.trunc && (!GENERATE || h.tcplen >= 18u);
     const uint32_t ip_part = sub_sum<FG>(
-      fold64(h.ipv4 ? range_sum<FG, FU, NT>(fc, lane, h0 + 14, h0 + 34) : 0));
+      fold64(h.ipv4 ? range_sum<FG, FU, NT, 1>(fc, lane, h0 + 14, h0 + 34) : 0));
     const uint32_t l4_part = sub_sum<FG>(fold64(
       do_l4 ? range_sum<FG, FU, NT>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen))
             : 0));
@@ -305,7 +305,7 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
       const int h0 = fc.h0;
       const bool do_l4 = h.tcp && !h.trunc;
       const uint32_t ip_part = sub_sum<FG>(
-        fold64(h.ipv4 ? range_sum<FG, FU, false>(fc, lane, h0 + 14, h0 + 34) : 0));
+        fold64(h.ipv4 ? range_sum<FG, FU, false, 1>(fc, lane, h0 + 14, h0 + 34) : 0));
       const uint32_t l4_part = sub_sum<FG>(fold64(
         do_l4 ? range_sum<FG, FU, false>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen)) : 0));
       if (lane == 0) {
