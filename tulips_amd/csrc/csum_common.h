@@ -124,6 +124,25 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
   return xcd_block_c<8>(b, nb);
 }
 
+// Inclusive u32 add-scan over the 64 lanes of a wave: DPP row shifts inside
+// each row of 16 lanes, then the row totals from lanes 15/31/47 (readlane).
+// No LDS crossbar (a __shfl_up scan is six dependent ds_bpermute_b32).
+__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t x)
+{
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xf, 0xf, false));
+  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xf, 0xf, false));
+  const int lane = threadIdx.x & 63;
+  const uint32_t r0 = __builtin_amdgcn_readlane(x, 15);
+  const uint32_t r1 = __builtin_amdgcn_readlane(x, 31);
+  const uint32_t r2 = __builtin_amdgcn_readlane(x, 47);
+  x += lane >= 16 ? r0 : 0u;
+  x += lane >= 32 ? r1 : 0u;
+  x += lane >= 48 ? r2 : 0u;
+  return x;
+}
+
 // Sum of x over each aligned G-lane subgroup of the wave (G = 16, 32 or 64),
 // returned to every lane of it, without the LDS crossbar. Four DPP row
 // rotations (row_ror 8, 4, 2, 1) fold each 16-lane row in VALU; wider

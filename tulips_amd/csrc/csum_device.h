@@ -244,23 +244,11 @@ masked_value(u32x4 v, int lo, int hi)
   return chunk_value(m);
 }
 
-// Inclusive u32 add-scan over the 64 lanes of a wave: DPP row shifts inside
-// each row of 16 lanes, then the row totals from lanes 15/31/47.
+// Inclusive u32 add-scan over the 64 lanes of a wave (csum_common.h).
 __device__ __forceinline__ uint32_t
 wave_incl_scan(uint32_t x)
 {
-  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xf, 0xf, false));
-  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xf, 0xf, false));
-  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xf, 0xf, false));
-  x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xf, 0xf, false));
-  const int lane = threadIdx.x & 63;
-  const uint32_t r0 = __builtin_amdgcn_readlane(x, 15);
-  const uint32_t r1 = __builtin_amdgcn_readlane(x, 31);
-  const uint32_t r2 = __builtin_amdgcn_readlane(x, 47);
-  x += lane >= 16 ? r0 : 0u;
-  x += lane >= 32 ? r1 : 0u;
-  x += lane >= 48 ? r2 : 0u;
-  return x;
+  return wave_inclusive_sum(x);
 }
 
 __device__ __forceinline__ uint64_t

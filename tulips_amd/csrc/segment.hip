@@ -93,13 +93,7 @@ __device__ __forceinline__ uint32_t
 block_inclusive_scan(uint32_t x, uint32_t* lds, uint32_t& total)
 {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(x, d, 64);
-    if (lane >= d) {
-      x += t;
-    }
-  }
+  x = wave_inclusive_sum(x);
   if (lane == 63) {
     lds[w] = x;
   }
