@@ -295,16 +295,38 @@ load_frame(uintptr_t fa, uint32_t flen, int lane, FrameChunks<G, U>& fc)
 // Frame-aligned header dwords F[j] = frame bytes 4j .. 4j+3 for j = 3..12
 // (bytes 12..51), assembled from chunks 0..4 held by lanes 0..4 of the
 // subgroup. Bytes past the frame end are unspecified (callers bound them).
+// G = 16 (a subgroup is one DPP row): row_newbcast moves lane c's dwords to
+// the whole row in VALU; G = 64: readlane; otherwise ds_bpermute.
+template<int G>
+__device__ __forceinline__ uint32_t
+from_lane(uint32_t x, int c, int sub0)
+{
+  if constexpr (G == 16) {
+    switch (c) { // (the DPP control must be an immediate)
+    case 0: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x150, 0xf, 0xf, false));
+    case 1: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x151, 0xf, 0xf, false));
+    case 2: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x152, 0xf, 0xf, false));
+    case 3: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x153, 0xf, 0xf, false));
+    default: return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x154, 0xf, 0xf, false));
+    }
+  } else if constexpr (G == 64) {
+    return __builtin_amdgcn_readlane(x, c);
+  } else {
+    return __shfl(x, sub0 + c, 64);
+  }
+}
+
+template<int G>
 __device__ __forceinline__ void
 header_words(const u32x4& v0, int h0, int sub0, uint32_t (&F)[13])
 {
   uint32_t w[20];
 #pragma unroll
   for (int c = 0; c < 5; ++c) {
-    w[4 * c + 0] = __shfl(v0.x, sub0 + c, 64);
-    w[4 * c + 1] = __shfl(v0.y, sub0 + c, 64);
-    w[4 * c + 2] = __shfl(v0.z, sub0 + c, 64);
-    w[4 * c + 3] = __shfl(v0.w, sub0 + c, 64);
+    w[4 * c + 0] = from_lane<G>(v0.x, c, sub0);
+    w[4 * c + 1] = from_lane<G>(v0.y, c, sub0);
+    w[4 * c + 2] = from_lane<G>(v0.z, c, sub0);
+    w[4 * c + 3] = from_lane<G>(v0.w, c, sub0);
   }
   const int s = h0 >> 2;
   const uint32_t r = uint32_t(h0 & 3);
@@ -323,7 +345,7 @@ __device__ __forceinline__ Header
 frame_header(const FrameChunks<G, U>& fc, uint32_t flen, int sub0)
 {
   uint32_t F[13];
-  header_words(fc.v[0], fc.h0, sub0, F);
+  header_words<G>(fc.v[0], fc.h0, sub0, F);
   return parse_header<true>(
     [&](int k) -> uint32_t {
       return uint32_t(k) < flen ? (F[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
