@@ -218,6 +218,37 @@ load_header(uintptr_t fa, uint32_t flen)
   return parse_header_chunks(load_header_chunks(fa, flen), fa, flen);
 }
 
+// The header fields a segment count needs (Ethernet type, IPv4 version/IHL,
+// total length, fragment bits, protocol: frame bytes 12..23; TCP data
+// offset: byte 46) from THREE chunk loads instead of five: the chunk holding
+// byte 12, the next one (bytes 12..23 span at most two chunks), and the one
+// holding byte 46 (never one of those two). The other fields of the returned
+// Header are unspecified. One thread per frame in the segmentation prologue:
+// a single workgroup issues these scattered loads for up to 1,024 frames, and
+// its memory pipeline, one 64-byte line per lane, is what the prologue waits
+// on.
+__device__ __forceinline__ Header
+load_seg_header(uintptr_t fa, uint32_t flen)
+{
+  const uintptr_t lo = fa & ~uintptr_t(15);
+  const uintptr_t hi = flen ? (fa + flen - 1) & ~uintptr_t(15) : lo;
+  const int h0 = int(fa - lo);
+  const int ca = (h0 + 12) >> 4, cb = (h0 + 46) >> 4;
+  auto ld = [&](int c) {
+    uintptr_t q = lo + 16 * uintptr_t(c);
+    q = q > hi ? hi : q;
+    return *reinterpret_cast<gchunk_ptr>(
+      flen ? q : reinterpret_cast<uintptr_t>(&k_hdr_zero_chunk));
+  };
+  const u32x4 x = ld(ca), y = ld(ca + 1), z = ld(cb);
+  HeaderChunks hc;
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    hc.c[c] = c == ca ? x : (c == ca + 1 ? y : z);
+  }
+  return parse_header_chunks(hc, fa, flen);
+}
+
 __device__ __forceinline__ uint32_t
 frame_flags(const Header& h, bool ip_ok, bool l4_ok)
 {

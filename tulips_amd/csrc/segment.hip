@@ -122,7 +122,7 @@ seg_count_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
   if (i < n) {
     const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + offs[i];
     const uint32_t flen = lens[i];
-    const SegInfo si = seg_info(load_header(fa, flen), mss);
+    const SegInfo si = seg_info(load_seg_header(fa, flen), mss);
     c = si.nseg;
     if (desc) {
       desc[i] = make_desc(fa, flen, si);
@@ -542,7 +542,7 @@ seg_prologue_small_kernel(const uint8_t* base, const uint64_t* __restrict__ offs
     if (i < n) {
       const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + offs[i];
       const uint32_t flen = lens[i];
-      const SegInfo si = seg_info(load_header(fa, flen), mss);
+      const SegInfo si = seg_info(load_seg_header(fa, flen), mss);
       c = si.nseg;
       if (desc) {
         desc[i] = make_desc(fa, flen, si);
