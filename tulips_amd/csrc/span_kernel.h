@@ -86,17 +86,19 @@ struct NoProbe
 // re-zeroed: the next launch's tag differs (profiles/probe_span_early_r03.txt:
 // 0.2-0.4 us per ZIPF launch against compare-and-swap + re-zero).
 template<int U, class Probe = NoProbe, uint32_t XC = 8, uint32_t NWIN = 1024, int MH = U / 3,
-         bool XCHG = true>
-__global__ __launch_bounds__(256, 7) void
+         bool XCHG = true, uint32_t TB = 256>
+__global__ __launch_bounds__(TB, 7) void
 csum_span_kernel(SpanArgs p, Probe pr)
 {
-  constexpr uint32_t NC = 256u * U;
+  constexpr uint32_t NWV = TB / 64; // waves per workgroup
+  static_assert(TB % 64 == 0 && NWV * U <= 64, "row totals fit one wave scan");
+  constexpr uint32_t NC = TB * U;
   constexpr uint64_t W = 16ull * NC;
-  constexpr int RW = NWIN / 256;
+  constexpr int RW = NWIN / TB;
   __shared__ uint32_t s_sc[NC];
-  __shared__ uint32_t s_tot[4 * U];
-  __shared__ uint32_t s_woff[4][4 * U];
-  __shared__ uint32_t s_cnt[8];
+  __shared__ uint32_t s_tot[NWV * U];
+  __shared__ uint32_t s_woff[NWV][NWV * U];
+  __shared__ uint32_t s_cnt[2 * NWV];
   __shared__ uint32_t s_meta[2];
 
   const uint32_t t = threadIdx.x, lane = t & 63u;
@@ -132,14 +134,14 @@ csum_span_kernel(SpanArgs p, Probe pr)
   uint32_t wl[RW];
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
-    const uint32_t i = min(G + t + 256u * r, n - 1);
+    const uint32_t i = min(G + t + TB * r, n - 1);
     wo[r] = offs[i] - p.bias;
     wl[r] = lens[i];
   }
   u32x4 v[U];
 #pragma unroll
   for (uint32_t j = 0; j < uint32_t(MH); ++j) {
-    v[j] = load_chunk<false>(chunk_at(x0 + 16u * (j * 256u + t)));
+    v[j] = load_chunk<false>(chunk_at(x0 + 16u * (j * TB + t)));
   }
   __builtin_amdgcn_sched_barrier(0);
   pr.mark(k, w, lane, 1);
@@ -147,28 +149,32 @@ csum_span_kernel(SpanArgs p, Probe pr)
     uint32_t c0 = 0, c1 = 0;
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
-      const bool in = G + t + 256u * r < n;
+      const bool in = G + t + TB * r < n;
       c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg0));
       c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(in && wo[r] < tg1));
     }
     if (lane == 0) {
       s_cnt[w] = c0;
-      s_cnt[4 + w] = c1;
+      s_cnt[NWV + w] = c1;
     }
   }
   lds_barrier(); // (the range's loads stay in flight)
   pr.mark(k, w, lane, 2);
-  const uint32_t c0 = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-  const uint32_t c1 = s_cnt[4] + s_cnt[5] + s_cnt[6] + s_cnt[7];
+  uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < NWV; ++q) {
+    c0 += s_cnt[q];
+    c1 += s_cnt[NWV + q];
+  }
   const uint32_t nw = min(NWIN, n - G);
   const bool tail_ok = G + NWIN >= n;
   const bool ok = (c0 > 0 || G == 0) && (c0 < nw || tail_ok) && (c1 > 0 || G == 0) &&
                   (c1 < nw || tail_ok);
   const uint32_t lo = G + c0, hi = G + c1;
   const uint32_t first = lo > 0 ? lo - 1 : 0;
-  // fast path: at most 256 entries to finish, so each thread holds at most
+  // fast path: at most TB entries to finish, so each thread holds at most
   // one of them
-  const bool fast = ok && hi - first <= 256u;
+  const bool fast = ok && hi - first <= TB;
 
   // 2. this thread's entry and its two boundary chunks, issued now
   bool act = false;
@@ -177,7 +183,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
   if (fast) {
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
-      const uint32_t i = G + t + 256u * r;
+      const uint32_t i = G + t + TB * r;
       bool a = i >= lo && i < hi;
       if (lo > 0 && i == lo - 1) {
         const uintptr_t ie = min(b + wo[r] + wl[r], aend);
@@ -201,7 +207,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
   if constexpr (MH < U) {
 #pragma unroll
     for (uint32_t j = MH; j < uint32_t(U); ++j) {
-      v[j] = load_chunk<false>(chunk_at(x0 + 16u * (j * 256u + t)));
+      v[j] = load_chunk<false>(chunk_at(x0 + 16u * (j * TB + t)));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -231,16 +237,16 @@ csum_span_kernel(SpanArgs p, Probe pr)
 #pragma unroll
   for (uint32_t j = 0; j < U; ++j) {
     const uint32_t sc = wave_incl_scan(chunk_value(v[j]));
-    s_sc[j * 256u + t] = sc;
+    s_sc[j * TB + t] = sc;
     if (lane == 63) {
-      s_tot[4 * j + w] = sc;
+      s_tot[NWV * j + w] = sc;
     }
   }
   lds_barrier();
   {
-    const uint32_t x = lane < 4 * U ? s_tot[lane] : 0u;
+    const uint32_t x = lane < NWV * U ? s_tot[lane] : 0u;
     const uint32_t inc = wave_incl_scan(x);
-    if (lane < 4 * U) {
+    if (lane < NWV * U) {
       s_woff[w][lane] = inc - x;
     }
   }
@@ -362,7 +368,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
     return;
   }
   // rare: [lo, hi) from a search when the window missed; metadata and
-  // boundary chunks from memory, 256 entries per round
+  // boundary chunks from memory, TB entries per round
   pr.mark(k, w, lane, 7);
   uint32_t L = lo, H = hi;
   if (!ok) {
@@ -402,7 +408,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
     L = s_meta[0];
     H = s_meta[1];
   }
-  for (uint32_t s0 = L > 0 ? L - 1 : 0; s0 < H; s0 += 256u) {
+  for (uint32_t s0 = L > 0 ? L - 1 : 0; s0 < H; s0 += TB) {
     const uint32_t i = s0 + t;
     bool a = i < H;
     const uint64_t o = a ? p.offs[i] - p.bias : 0;
