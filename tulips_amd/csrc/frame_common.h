@@ -389,34 +389,23 @@ frame_header(const FrameChunks<G, U>& fc, uint32_t flen, int sub0)
 // rows of registers are looked at: a range known to end inside them (the
 // IPv4 header, UM = 1) skips the others at compile time. With UM == U,
 // bytes beyond the G*U chunks held in registers are loaded by a trailing
-// lane_sum (jumbo). Branch-free: the range's chunks are added whole by a
-// select, then the lanes holding its first and last chunk subtract the
-// bytes of those chunks that lie outside it (a per-chunk mask under a
-// branch per chunk cost ~2x the instructions, most of them exec-mask
-// bookkeeping, between a frame's last load and its flags).
+// lane_sum (jumbo). (A branch-free form - whole chunks by select, the
+// boundary chunks picked by a runtime-indexed select - took 10 % fewer
+// instructions at 16 x 6 but spilled at 16 x 8 and 8 x 8/16, where
+// generation then ran 4x slower: profiles/probe_frames_r03.txt.)
 template<int G, int U, bool NT, int UM = U>
 __device__ __forceinline__ uint64_t
 range_sum(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
 {
   static_assert(UM >= 1 && UM <= U, "rows");
-  const int clo = lo >> 4, chi = (hi - 1) >> 4;
   uint64_t acc = 0;
-  u32x4 vlo = fc.v[0], vhi = fc.v[0];
 #pragma unroll
   for (int u = 0; u < UM; ++u) {
-    const int c = lane + u * G;
-    acc += (c >= clo && c <= chi) ? hsum(fc.v[u]) : 0ull;
-    if (u > 0) {
-      vlo = clo / G == u ? fc.v[u] : vlo;
-      vhi = chi / G == u ? fc.v[u] : vhi;
+    const int b = 16 * (lane + u * G);
+    const int l = max(lo - b, 0), h = min(hi - b, 16);
+    if (l < h) {
+      acc += (l == 0 && h == 16) ? hsum(fc.v[u]) : masked_hsum(fc.v[u], l, h);
     }
-  }
-  const int l = lo & 15, h = hi & 15;
-  if (l != 0 && lane == (clo & (G - 1)) && clo < G * UM) {
-    acc -= masked_hsum(vlo, 0, l);
-  }
-  if (h != 0 && lane == (chi & (G - 1)) && chi < G * UM) {
-    acc -= masked_hsum(vhi, h, 16);
   }
   if constexpr (UM == U) {
     constexpr int held = 16 * G * U;

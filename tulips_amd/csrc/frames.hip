@@ -62,7 +62,9 @@ using namespace frame;
 // (0 = no bound). Generation: 94 -> 80 VGPRs, 5 -> 6 waves/SIMD, no spill;
 // 3 alternations on one box (profiles/ab_r01.txt): 21.2-22.0 -> 20.8-21.4 us
 // serial, 19.4-19.7 -> 18.7-19.0 us on 4 branches. Validation at 7 waves
-// spills 12 B and is slower.
+// spills 12 B and is slower. The generation bound applies to the default
+// geometry and smaller (U <= 6): at 16 x 8 and 8 x 8/16 it spilled 12-364 B
+// per lane, so those keep their natural register counts.
 constexpr int FRAME_VAL_WAVES = 0, FRAME_GEN_WAVES = 6;
 
 // OP: 0 = validate (flags, counters), 1 = generate in place (the two
@@ -71,7 +73,7 @@ constexpr int FRAME_VAL_WAVES = 0, FRAME_GEN_WAVES = 6;
 enum { OP_VALIDATE = 0, OP_GENERATE = 1, OP_FIELDS = 2 };
 
 template<int OP, int FG, int FU, bool NT>
-__global__ __launch_bounds__(1024, OP != OP_VALIDATE ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
+__global__ __launch_bounds__(1024, OP != OP_VALIDATE && FU <= 6 ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
 frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ shards,
