@@ -231,3 +231,49 @@ def test_missing_library_fails_loudly(tmp_path):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "no CPU fallback" in r.stderr
+
+
+READELF = "/opt/rocm/llvm/bin/llvm-readelf"
+
+
+@pytest.mark.skipif(not os.path.exists(READELF), reason="llvm-readelf not installed")
+def test_no_kernel_spills_to_scratch(tmp_path):
+    """Every gfx950 kernel in the library keeps its registers on chip: a
+    scratch spill turns a bandwidth-bound kernel into a scratch-bound one
+    (a frame geometry spilling 200 B per lane ran 4x slower,
+    profiles/probe_frames_r03.txt). Reads the AMDGPU metadata of the code
+    objects embedded in libtulips_csum.so (clang offload bundles); no GPU."""
+    import struct
+    import subprocess
+    data = open(csum.LIB_PATH, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    objs, pos = [], 0
+    while True:
+        i = data.find(magic, pos)
+        if i < 0:
+            break
+        n = struct.unpack_from("<Q", data, i + 24)[0]
+        off = i + 32
+        for _ in range(n):
+            eo, es, ts = struct.unpack_from("<QQQ", data, off)
+            off += 24
+            triple = data[off:off + ts].decode()
+            off += ts
+            if "gfx950" in triple and es:
+                objs.append(data[i + eo:i + eo + es])
+        pos = i + len(magic)
+    assert objs, "no gfx950 code object in the library"
+    kernels, spilling = 0, []
+    for k, co in enumerate(objs):
+        p = tmp_path / f"co{k}.o"
+        p.write_bytes(co)
+        out = subprocess.run([READELF, "--notes", str(p)], capture_output=True, text=True,
+                             check=True).stdout
+        for block in out.split(".private_segment_fixed_size:")[1:]:
+            kernels += 1
+            size = int(block.split()[0])
+            if size:
+                name = re.search(r"\.name:\s+(\S+)", block)
+                spilling.append((name.group(1) if name else "?", size))
+    assert kernels >= 100, kernels
+    assert not spilling, spilling
