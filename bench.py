@@ -57,9 +57,11 @@ def parse():
                    help="torch.distributed backend for N>1 (nccl = RCCL)")
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal only: every rank uses cuda:0 (use with gloo)")
-    p.add_argument("--streams", type=int, default=4,
+    p.add_argument("--streams", type=int, default=8,
                    help="independent graph branches the timed steps round-robin over "
-                        "(batches are independent; 4 = GPU_MAX_HW_QUEUES on the box)")
+                        "(batches are independent; 8 = two per hardware queue, "
+                        "GPU_MAX_HW_QUEUES being 4 on the box: the next launch is "
+                        "already queued when one ends; profiles/probe_branches_r03.txt)")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from Python instead of replaying a "
                         "captured HIP graph of one shard rotation (16 launches); "
@@ -692,14 +694,24 @@ def zipf_sharded_leg(torch, dist, csum, dev, cdev, stream, rank, world):
             "parity": "ok" if ok else "MISMATCH"}
 
 
-PIPE = 4   # graph branches for the "pipeline" figures (bench --streams default)
+PIPE = 4    # graph branches for the "pipeline" figures: one per hardware queue
+PIPE_WIDE = 8   # two per hardware queue (the bench --streams default)
 
 
-def pipe_entry(nbytes, t):
-    """Rate of `PIPE` overlapped graph branches (seconds per launch t)."""
-    return {"branches": PIPE, "us_per_launch": round(t * 1e6, 2),
-            "GiBps": round(nbytes / t / GIB, 1),
-            "frac_of_peak": round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4)}
+def pipe_times(timer, fn, reps):
+    """Seconds per launch of `fn` over PIPE and over PIPE_WIDE graph branches."""
+    return timer(fn, reps, branches=PIPE), timer(fn, reps, branches=PIPE_WIDE)
+
+
+def pipe_entry(nbytes, tt):
+    """Rates of overlapped graph branches: (t at PIPE, t at PIPE_WIDE) in seconds."""
+    def one(b, t):
+        return {"branches": b, "us_per_launch": round(t * 1e6, 2),
+                "GiBps": round(nbytes / t / GIB, 1),
+                "frac_of_peak": round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4)}
+    e = one(PIPE, tt[0])
+    e["wide"] = one(PIPE_WIDE, tt[1])
+    return e
 
 
 def read_traffic(workload):
@@ -734,7 +746,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     for i in range(NBATCH):
         one(i, sh)
     t1 = timer(one, 64)
-    tp1 = timer(one, 64, branches=PIPE)
+    tp1 = pipe_times(timer, one, 64)
     ex["stream_read_F1500_batch"] = {
         "what": "plain 16-byte streaming read of one F1500 batch per launch (98.3 MB), "
                 "batches rotated: the single-launch ceiling roofline.frac compares with",
@@ -757,7 +769,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     for i in range(4):
         f9(i, sh)
     t = timer(f9, 40)
-    tp = timer(f9, 40, branches=PIPE)
+    tp = pipe_times(timer, f9, 40)
     # the F9000 kernel's own read pattern without the arithmetic, over the
     # same two rotated batches: the ceiling that kernel is held against
     sink9 = torch.zeros(4, dtype=torch.int32, device=dev)
@@ -814,12 +826,12 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     for i in range(nz):
         fz_any(i, sh)
     ta = timer(fz_any, 80)
-    tpa = timer(fz_any, 80, branches=PIPE)
+    tpa = pipe_times(timer, fz_any, 80)
     oa = oz[:NSEG].cpu().numpy().view(np.uint16)
     for i in range(nz):
         fz(i, sh)
     t = timer(fz, 80)
-    tp = timer(fz, 80, branches=PIPE)
+    tp = pipe_times(timer, fz, 80)
     o = oz[:NSEG].cpu().numpy().view(np.uint16)
     zgold = gold.get("ZIPF", {}).get("fnv1a64")
     # the single-launch read ceiling for these bytes: a plain streaming read
@@ -831,7 +843,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
         b = i % nz
         lib.tulips_csum_stream_read(az.data_ptr() + b * zr, zr, zsink.data_ptr(), 0, st)
     tr = timer(fzr, 80)
-    trp = timer(fzr, 80, branches=PIPE)
+    trp = pipe_times(timer, fzr, 80)
     ex["ZIPF"] = {"GiBps": round(zb / t / GIB, 1), "Mseg_per_s": round(NSEG / t / 1e6, 1),
                   "frac_of_peak": round(zb / t / 1e9 / HBM_PEAK_GBS, 4),
                   "avg_launch_us": round(t * 1e6, 2),
@@ -1016,7 +1028,7 @@ def frame_extras(torch, csum, dev, timer):
     for i in range(nb):
         fgen(i, torch.cuda.current_stream().cuda_stream)
     t = timer(fgen, 64)
-    tp = timer(fgen, 64, branches=PIPE)
+    tp = pipe_times(timer, fgen, 64)
     ex["frames_generate_F1514"] = rate_entry(
         alg, t, kernel="frame_kernel<GENERATE, 16 lanes x 6 chunks per frame>",
         workload="65,536 x 1514 B TCP frames per launch, 2 KiB slots, 8 bursts rotated",
@@ -1035,7 +1047,7 @@ def frame_extras(torch, csum, dev, timer):
     for i in range(nb):
         ffld(i, torch.cuda.current_stream().cuda_stream)
     t = timer(ffld, 64)
-    tp = timer(ffld, 64, branches=PIPE)
+    tp = pipe_times(timer, ffld, 64)
     fv = v.view(nb * nf, slot)
     want = (fv[:, 24].int() | (fv[:, 25].int() << 8) | (fv[:, 50].int() << 16) |
             (fv[:, 51].int() << 24))
@@ -1047,7 +1059,7 @@ def frame_extras(torch, csum, dev, timer):
         traffic=read_traffic("frames_generate_fields_F1514"))
     del fields, fv, want
     t = timer(fval, 64)
-    tp = timer(fval, 64, branches=PIPE)
+    tp = pipe_times(timer, fval, 64)
     ok = bool((flags == 0x0F).all().item())
     ex["frames_validate_F1514"] = rate_entry(
         alg, t, kernel="frame_kernel<VALIDATE, 16 lanes x 6 chunks per frame>",
@@ -1087,7 +1099,7 @@ def frame_extras(torch, csum, dev, timer):
     for i in range(sb):
         fseg(i, torch.cuda.current_stream().cuda_stream)
     t = timer(fseg, 32)
-    tp = timer(fseg, 32, branches=PIPE)
+    tp = pipe_times(timer, fseg, 32)
     moved = nsf * sflen + nseg * (54 + mss)       # read super-frames + write segments
     so = torch.arange(nseg, dtype=torch.int64, device=dev) * ostride
     sfl = csum.validate_frames(sout[:nseg * ostride], so, solen[:nseg])
@@ -1118,7 +1130,7 @@ def frame_extras(torch, csum, dev, timer):
             0, rout.data_ptr(), st)
     frss(0, torch.cuda.current_stream().cuda_stream)
     t = timer(frss, 32)
-    tp = timer(frss, 32, branches=PIPE)
+    tp = pipe_times(timer, frss, 32)
     # parity: 2,048 tuples spread over the batch against the host symbol
     js = torch.arange(0, nt, nt // 2048)
     cols = [x.cpu().numpy() for x in (sa_[js], da_[js], sp_[js], dp_[js], rout[js])]
