@@ -341,6 +341,48 @@ def test_captured_contract_breaking_replay_does_not_spoil_the_next(oracle):
 
 
 @pytest.mark.gpu
+def test_captured_arena_call_replayed_on_alternating_streams(oracle):
+    """One captured arena call replayed on two streams in turn (two hardware
+    queues, whose dispatch ids may run in step), the bytes changed between
+    replays: the word array is the graph's, so consecutive launches on it come
+    from different queues. The split words' tag offsets the dispatch id by a
+    hash of the queue (span_kernel.h launch_tag), so a launch never takes the
+    other queue's residue for its partner's part: every replay is exact."""
+    import torch
+    from tulips_amd import csum
+    rng = np.random.default_rng(5151)
+    n = 24000
+    lens = rng.integers(40, 4000, n).astype(np.uint16)
+    offs = np.zeros(n, np.uint64)
+    np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+    total = int(lens.astype(np.int64).sum())
+    bufs = [rng.integers(0, 256, total + 16, dtype=np.uint8) for _ in range(2)]
+    exps = [oracle.batch(b, offs, lens, mode=MODE_INET, nthreads=8) for b in bufs]
+    a, o, l = _dev(bufs[0], offs.astype(np.int64), lens.view(np.int16))
+    srcs = [torch.from_numpy(b).to("cuda:0") for b in bufs]
+    out = torch.empty(n, dtype=torch.int16, device="cuda:0")
+    cap = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        assert csum.lib.tulips_csum_batch_arena(a.data_ptr(), total, o.data_ptr(),
+                                                l.data_ptr(), None, None, None,
+                                                out.data_ptr(), n, MODE_INET,
+                                                cap.cuda_stream) == 0
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for i in range(32):
+        d = (i // 2) % 2
+        with torch.cuda.stream(streams[i % 2]):
+            a.copy_(srcs[d])
+            out.fill_(0)
+            g.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), exps[d],
+                                      err_msg=f"replay {i}")
+    del g
+    csum.release_stream(cap.cuda_stream)
+
+
+@pytest.mark.gpu
 def test_zero_frames_zero_the_counters():
     import torch
     from tulips_amd import csum

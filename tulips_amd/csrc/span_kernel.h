@@ -48,7 +48,8 @@ namespace {
 //     for another.
 // Words (stream_state.h span_slots) are tagged with the launch's AQL dispatch
 // id (per-queue packet index, 40 bits kept: distinct for every launch and
-// every graph replay on a queue until 2^40 dispatches), so a word left by an
+// every graph replay on a queue until 2^40 dispatches) offset by a hash of the
+// queue (launch_tag: ids of different queues overlap), so a word left by an
 // earlier launch is never taken for a part of this one: it is overwritten,
 // never added to. A split part is only sent to a word
 // when the segment starts inside the arena and its range has a word;
@@ -64,6 +65,23 @@ extern "C" __device__ uint64_t llvm_amdgcn_dispatch_id() __asm("llvm.amdgcn.disp
 constexpr uint32_t WORD_ARR_SHIFT = 20, WORD_TAG_SHIFT = 24;
 constexpr uint64_t WORD_SUM_MASK = (1ull << WORD_ARR_SHIFT) - 1;
 constexpr uint64_t WORD_TAG_MASK = (1ull << 40) - 1;
+
+// This launch's tag: its dispatch id (the packet's index on its queue) offset
+// by a hash of the queue's address, xor the word array's salt. Every hardware
+// queue counts from 0, and one word array can see launches from several
+// queues (a graph replayed on another stream, a stream handle reused after
+// hipStreamDestroy), so two queues in step would give two launches the same
+// bare dispatch id and the later one would take the earlier one's residue for
+// its own part. With the offset two queues' tags meet only when their
+// counters differ by the difference of their offsets, a pseudo-random 40-bit
+// number.
+__device__ __forceinline__ uint64_t
+launch_tag(uint32_t salt)
+{
+  const uint64_t q = uint64_t(reinterpret_cast<uintptr_t>(__builtin_amdgcn_queue_ptr()));
+  const uint64_t h = (q * 0x9E3779B97F4A7C15ull) >> 24;
+  return ((llvm_amdgcn_dispatch_id() + h) ^ salt) & WORD_TAG_MASK;
+}
 
 // The product's probe: no marks. tools/probes/span_stamps.hip instantiates
 // the same kernel with a probe that records per-wave realtime stamps at
@@ -264,7 +282,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
   //    the compare-and-swap makes its round trip)
   const uint32_t want = (p.mode & FLAG_COMPLEMENT) ? 0u : 0xffffu;
   const bool side_in = (p.mode & MODE_MASK) == MODE_TCP || p.seeds != nullptr;
-  const uint64_t tag = (llvm_amdgcn_dispatch_id() ^ p.salt) & WORD_TAG_MASK;
+  const uint64_t tag = launch_tag(p.salt);
   auto store = [&](uint32_t s, uint32_t r) {
     if (p.out) {
       if (p.nt_store) {
