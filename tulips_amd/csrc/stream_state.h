@@ -51,7 +51,7 @@ struct StreamState
   uint64_t seg_ndesc = 0;
 
   // SPAN split-form words (span_kernel.h csum_span_kernel): one 64-bit word
-  // per arena range, tagged with the launch's dispatch id, so a word left by
+  // per arena range, tagged with the launch's dispatch id and queue, so a word left by
   // an earlier launch (two-part segments leave theirs as they are) is never
   // added to. The calls one
   // capture records on this stream run in order in the graph, so they share

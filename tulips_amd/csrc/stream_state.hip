@@ -257,8 +257,9 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64
   }
   s.span_owned.push_back(p);
   // a graph may be replayed on other streams (other hardware queues, whose
-  // dispatch ids overlap this one's): a salt per captured array keeps such
-  // replays' tags apart
+  // dispatch ids overlap this one's): the kernel's tag adds a hash of the
+  // queue (span_kernel.h launch_tag), and a salt per captured array sets
+  // its tags apart from every other array's as well
   s.span_salt = s.span_salt * 0x9E3779B1u + 0x7F4A7C15u;
   s.span_capture[id] = StreamState::Capture{ p, size, s.span_salt };
   *out = p;
