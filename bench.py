@@ -121,9 +121,11 @@ class Timer:
     def __init__(self, torch, stream, graph=True):
         self.torch, self.stream, self.graph = torch, stream, graph
 
-    def __call__(self, fn, reps, branches=1):
+    def __call__(self, fn, reps, branches=1, replays=1):
         """branches > 1: launch i goes to graph branch i % branches (independent
-        launches overlap); the result is then time per launch of the pipeline."""
+        launches overlap); the result is then time per launch of the pipeline.
+        replays > 1 (graph only): the captured graph is replayed that many
+        times, each timed on its own, and the median is returned."""
         t = self.torch
         a, b = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
         g = None
@@ -147,6 +149,15 @@ class Timer:
                     main.wait_stream(sd)
             g.replay()                      # warm replay
         t.cuda.synchronize()
+        if g is not None and replays > 1:
+            times = []
+            for _ in range(replays):
+                a.record(self.stream)
+                g.replay()
+                b.record(self.stream)
+                b.synchronize()
+                times.append(a.elapsed_time(b) / 1e3 / reps)
+            return float(np.median(times))
         a.record(self.stream)
         if g is not None:
             g.replay()
@@ -698,9 +709,17 @@ PIPE = 4    # graph branches for the "pipeline" figures: one per hardware queue
 PIPE_WIDE = 8   # two per hardware queue (the bench --streams default)
 
 
+PIPE_LAUNCHES = 4   # a pipeline graph holds this many times the serial launches
+
+
 def pipe_times(timer, fn, reps):
-    """Seconds per launch of `fn` over PIPE and over PIPE_WIDE graph branches."""
-    return timer(fn, reps, branches=PIPE), timer(fn, reps, branches=PIPE_WIDE)
+    """Seconds per launch of `fn` over PIPE and over PIPE_WIDE graph branches:
+    PIPE_LAUNCHES x reps launches per graph, so its fork and join are spread
+    thin (profiles/probe_branches_r03.txt: ZIPF over 160 launches on 4
+    branches 7.5-8.8 us, over 640 7.5-7.9), median of 3 replays."""
+    n = PIPE_LAUNCHES * reps
+    return (timer(fn, n, branches=PIPE, replays=3),
+            timer(fn, n, branches=PIPE_WIDE, replays=3))
 
 
 def pipe_entry(nbytes, tt):

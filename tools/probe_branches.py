@@ -58,16 +58,24 @@ def main():
                                         fl.data_ptr(), nf, flags.data_ptr() + b * nf, None, st)
     work = {"F1500": (f1500, bb, 256), "ZIPF": (zipf, zb, 160), "frames_validate": (fval,
                                                                                    nf * flen, 128)}
+    # PROBE_REPS_SCALE="1,2,4": also time each pipeline over 2x / 4x the
+    # launches (the graph's fork and join are then spread over more launches)
+    scales = [int(x) for x in os.environ.get("PROBE_REPS_SCALE", "1").split(",")]
+    only = os.environ.get("PROBE_ONLY")
     res = {}
     for rnd in range(3):
-        for name, (fn, nbytes, reps) in work.items():
-            for br in (4, 8):
-                t = timer(fn, reps, branches=br)
-                res.setdefault((name, br), []).append(t * 1e6)
-                print(f"round {rnd} {name:16s} {br} branches: {t * 1e6:6.2f} us per launch "
-                      f"({nbytes / t / 8e12:.3f})", flush=True)
-    for (name, br), v in res.items():
-        print(f"{name:16s} {br} branches: median {np.median(v):6.2f} us "
+        for name, (fn, nbytes, reps0) in work.items():
+            if only and name != only:
+                continue
+            for sc in scales:
+                reps = reps0 * sc
+                for br in (4, 8):
+                    t = timer(fn, reps, branches=br)
+                    res.setdefault((name, br, reps), []).append(t * 1e6)
+                    print(f"round {rnd} {name:16s} {reps:4d} launches {br} branches: "
+                          f"{t * 1e6:6.2f} us per launch ({nbytes / t / 8e12:.3f})", flush=True)
+    for (name, br, reps), v in res.items():
+        print(f"{name:16s} {reps:4d} launches {br} branches: median {np.median(v):6.2f} us "
               f"({work[name][1] / np.median(v) / 8e6:.3f})")
 
 
