@@ -1085,6 +1085,23 @@ def frame_extras(torch, csum, dev, timer):
         workload="same frames: generated checksums verified (flags == 0x0F)",
         pipeline=pipe_entry(alg, tp), parity="ok" if ok else "MISMATCH",
         traffic=read_traffic("frames_validate_F1514"))
+    # the frame kernels' read pattern without the arithmetic, over the same
+    # rotated bursts: the ceiling those kernels are held against
+    fsink = torch.zeros(4, dtype=torch.int32, device=dev)
+
+    def frd(i, st):
+        b = i % nb
+        lib.tulips_csum_stream_read_slots(ar.data_ptr() + b * burst, slot, flen, nf,
+                                          fsink.data_ptr(), st)
+    t = timer(frd, 64)
+    tp = pipe_times(timer, frd, 64)
+    ex["frames_validate_F1514"]["read_same_bytes"] = {
+        "what": "tulips_csum_stream_read_slots: the frame kernels' loads (one 16-lane "
+                "subgroup per 1514 B frame in its 2 KiB slot, 6 clamped loads per lane), "
+                "no arithmetic",
+        "avg_launch_us": round(t * 1e6, 2),
+        "frac_of_peak": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+        "pipeline": pipe_entry(alg, tp)}
     del ar, v, flags
 
     # Segmentation offload: 4 batches x 1024 super-frames of 64,294 B (44 x

@@ -97,6 +97,14 @@ int tulips_csum_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
 int tulips_csum_stream_read_tiles(const uint8_t* p, uint64_t tile_bytes, uint32_t ntiles,
                                   uint32_t* sink, void* stream);
 
+/* The frame kernels' read pattern without their arithmetic: slot k's first
+ * read_bytes bytes, [p + k * slot_bytes, + read_bytes), read by one 16-lane
+ * subgroup, 6 clamped 16-byte loads per lane per pass (read_bytes <= 65535,
+ * slot_bytes >= read_bytes). The ceiling the frame kernels are compared
+ * against (bench.py extras.frames_validate_F1514.read_same_bytes). */
+int tulips_csum_stream_read_slots(const uint8_t* p, uint64_t slot_bytes, uint32_t read_bytes,
+                                  uint32_t nslots, uint32_t* sink, void* stream);
+
 /* Latency of `reps` back-to-back receive validations of one burst of
  * host-resident frames, timed in C with a steady clock around each call
  * (no interpreter in the loop): path 0 = tulips_csum_validate_frames_host

@@ -182,6 +182,11 @@ def test_batch_validation_without_gpu():
     assert lib.tulips_csum_ctx_destroy(None) == 1
     assert lib.tulips_csum_batch_host(None, FAKE, FAKE, FAKE, None, None, None, FAKE, 4, 0) == 1
     assert lib.tulips_csum_stream_read(FAKE + 1, 16, FAKE, 0, None) == 1
+    assert lib.tulips_csum_stream_read_tiles(FAKE, 0, 4, FAKE, None) == 1
+    assert lib.tulips_csum_stream_read_slots(FAKE, 2048, 0, 4, FAKE, None) == 1
+    assert lib.tulips_csum_stream_read_slots(FAKE, 1000, 1514, 4, FAKE, None) == 1
+    assert lib.tulips_csum_stream_read_slots(FAKE, 70000, 65536, 4, FAKE, None) == 1
+    assert lib.tulips_csum_stream_read_slots(None, 2048, 1514, 0, None, None) == 0
 
 
 def test_python_binding_raises_typed_errors():

@@ -556,6 +556,18 @@ tulips_csum_stream_read_tiles(const uint8_t* p, uint64_t tile_bytes, uint32_t nt
     launch_stream_tiles(p, tile_bytes, ntiles, sink, static_cast<hipStream_t>(stream)));
 }
 
+int
+tulips_csum_stream_read_slots(const uint8_t* p, uint64_t slot_bytes, uint32_t read_bytes,
+                              uint32_t nslots, uint32_t* sink, void* stream)
+{
+  if (nslots && (!p || !sink || read_bytes == 0 || read_bytes > TULIPS_CSUM_MAX_SEGMENT ||
+                 slot_bytes < read_bytes)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return status_of(launch_stream_slots(p, slot_bytes, read_bytes, nslots, sink,
+                                       static_cast<hipStream_t>(stream)));
+}
+
 const char*
 tulips_csum_status_string(int status)
 {
