@@ -57,10 +57,10 @@ def parse():
                    help="torch.distributed backend for N>1 (nccl = RCCL)")
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal only: every rank uses cuda:0 (use with gloo)")
-    p.add_argument("--streams", type=int, default=8,
+    p.add_argument("--streams", type=int, default=16,
                    help="independent graph branches the timed steps round-robin over "
-                        "(batches are independent; 8 = two per hardware queue, "
-                        "GPU_MAX_HW_QUEUES being 4 on the box: the next launch is "
+                        "(batches are independent; 16 = four per hardware queue, "
+                        "GPU_MAX_HW_QUEUES being 4 on the box: the next launches are "
                         "already queued when one ends; profiles/probe_branches_r03.txt)")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from Python instead of replaying a "
