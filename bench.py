@@ -19,7 +19,14 @@ the plain streaming-read ceiling on the same buffer, the end-to-end host path
 box's cores (cpu_baseline).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N>1 under `python -m torch.distributed.run --nproc-per-node N ...`)
+       N>1 runs one rank per GPU: under `python -m torch.distributed.run
+       --nproc-per-node N ...`, or, with no launcher (WORLD_SIZE unset), this
+       script starts that launcher itself as a child process (before any GPU
+       call), relays its output and exits with its status.
+
+Parity of the measured work: the result buffers are poisoned (0xA5 bytes)
+before every timed replay and the digests of what the replay wrote are
+compared with the reference's afterwards (per batch, tests/golden).
 """
 from __future__ import annotations
 
@@ -62,6 +69,10 @@ def parse():
                         "(batches are independent; 16 = four per hardware queue, "
                         "GPU_MAX_HW_QUEUES being 4 on the box: the next launches are "
                         "already queued when one ends; profiles/probe_branches_r03.txt)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher and process-group check only (no GPU work): ranks form "
+                        "the group, assert its size and rank 0 prints the JSON line "
+                        "without measurements")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from Python instead of replaying a "
                         "captured HIP graph of one shard rotation (16 launches); "
@@ -99,6 +110,17 @@ def fnv1a_u16(v: np.ndarray) -> str:
     return f"{h:016x}"
 
 
+def golden_rotations():
+    """Reference digests of the distinct batches the side measurements
+    rotate over (tests/golden/make_golden.py rotation_digests)."""
+    path = os.path.join(ROOT, "tests", "golden", "digests.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("rotations", {})
+    except OSError:
+        return {}
+
+
 def golden_digests():
     path = os.path.join(ROOT, "tests", "golden", "digests.json")
     try:
@@ -121,11 +143,14 @@ class Timer:
     def __init__(self, torch, stream, graph=True):
         self.torch, self.stream, self.graph = torch, stream, graph
 
-    def __call__(self, fn, reps, branches=1, replays=1):
+    def __call__(self, fn, reps, branches=1, replays=1, poison=None):
         """branches > 1: launch i goes to graph branch i % branches (independent
         launches overlap); the result is then time per launch of the pipeline.
         replays > 1 (graph only): the captured graph is replayed that many
-        times, each timed on its own, and the median is returned."""
+        times, each timed on its own, and the median is returned.
+        poison(): overwrites the launches' outputs after every untimed launch
+        (capture warm-up, warm replay) and before the timed replay(s), so what
+        the caller checks afterwards was written inside the timed region."""
         t = self.torch
         a, b = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
         g = None
@@ -149,6 +174,9 @@ class Timer:
                     main.wait_stream(sd)
             g.replay()                      # warm replay
         t.cuda.synchronize()
+        if poison is not None:
+            poison()
+            t.cuda.synchronize()
         if g is not None and replays > 1:
             times = []
             for _ in range(replays):
@@ -169,21 +197,42 @@ class Timer:
         return a.elapsed_time(b) / 1e3 / reps  # seconds per launch
 
 
+def self_launch(args):
+    """--gpus N > 1 without a launcher: run this script under
+    torch.distributed.run with N ranks as a CHILD process (no exec: nothing
+    here has touched the GPU, and the child owns its own HIP state), stream
+    its output through and return its exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     import torch
     import torch.distributed as dist
-    from tulips_amd import csum
-    from tulips_amd.shard import (all_ranks_ok, gather_results, gather_strings,
-                                  max_over_ranks, shard_for)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if args.one_device:
         local = 0
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    from tulips_amd import csum
+    from tulips_amd.shard import (all_ranks_ok, gather_results, gather_strings,
+                                  max_over_ranks, shard_for)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # control-plane reductions live on the GPU under RCCL, on the CPU under gloo
@@ -193,6 +242,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        check_world(dist, args)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     lib = csum.lib
@@ -259,6 +309,10 @@ def main():
     # ---- timed region ------------------------------------------------------
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    # every result word overwritten first: what is checked after the timed
+    # replay was written by it (outside the timed region)
+    outs.view(torch.uint8).fill_(0xA5)
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -284,6 +338,25 @@ def main():
     value = total_bytes / t_max / GIB
     per_launch_s = t_local / steps_done
 
+    # ---- parity of what the timed replay wrote: per-batch digests vs the
+    # reference's (shard <rank> of M8x1500, batch b = steps i with i % 16 == b)
+    gold = golden_digests().get("M8x1500", {})
+    written = sorted({i % NBATCH for i in range(steps_done)})
+    got_b = row_digests(outs, NBATCH, NSEG)
+    ok = False
+    if rank < 8 and gold.get("shards") and "batches" in gold["shards"][rank]:
+        want_b = gold["shards"][rank]["batches"]
+        ok = all(got_b[b] == want_b[b] for b in written)
+    parity = "ok" if all_ranks_ok(ok, dist, cdev) else "MISMATCH"
+    parity_checked = (f"result words poisoned (0xA5A5) before the timed replay; the "
+                      f"{len(written)} batches it wrote per rank checked against the "
+                      "reference's per-batch digests of M8x1500 shard <rank>")
+    if len(written) < NBATCH:
+        # the later legs use the whole shard's results
+        for b in range(NBATCH):
+            step(b)
+        torch.cuda.synchronize()
+
     # the same graph replayed again, each replay timed alone (HIP events on
     # the replay stream, max over ranks): the spread of `value` within one
     # session (make the headline reproducible)
@@ -300,14 +373,7 @@ def main():
             tr = max_over_ranks(ev0.elapsed_time(ev1) / 1e3, dist, cdev)
             replays.append(total_bytes / tr / GIB)
 
-    # ---- parity of what was measured: shard digest vs the reference's -------
-    gold = golden_digests().get("M8x1500", {})
-    out_np = outs.cpu().numpy().view(np.uint16)
-    digest = fnv1a_u16(out_np)
-    ok = True
-    if rank < 8 and gold.get("shards"):
-        ok = digest == gold["shards"][rank]["fnv1a64"]
-    parity = "ok" if all_ranks_ok(ok, dist, cdev) else "MISMATCH"
+    digest = fnv1a_u16(outs.cpu().numpy().view(np.uint16))
     shard_digests = gather_strings(digest, dist)
 
     # exchange-inclusive figures (N>1, reported beside `value`, never as it):
@@ -329,7 +395,7 @@ def main():
                       "`config.streams` independent branches (bursts overlap); one launch "
                       "at a time is roofline.avg_launch_us / roofline.frac",
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": dist.get_world_size() if dist.is_initialized() else 1,
         "steps": steps_done,
         "warmup": args.warmup,
         "ms_per_step": round(t_max / steps_done * 1e3, 5),
@@ -349,6 +415,7 @@ def main():
             "streams": args.streams if graph is not None else 1,
         },
         "parity": parity,
+        "parity_checked": parity_checked,
         "dist": dist_info(torch, dist, world, local, args),
         "shard_digests": shard_digests,
         "exchange": exchange,
@@ -400,6 +467,38 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def check_world(dist, args):
+    """Every rank: the process group holds exactly --gpus ranks."""
+    if dist.get_world_size() != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has "
+                         f"{dist.get_world_size()} ranks")
+
+
+def dry_run(args, world, rank):
+    """The launcher/process-group half of a run, with no GPU call: ranks
+    form the group over gloo, check its size against --gpus, gather their
+    ranks and rank 0 prints one JSON line (tests/test_bench_launch.py)."""
+    import torch.distributed as dist
+    from tulips_amd.shard import gather_strings
+    ranks = [0]
+    if world > 1:
+        dist.init_process_group("gloo")
+        check_world(dist, args)
+        ranks = [int(x) for x in gather_strings(str(rank), dist)]
+        dist.barrier()
+        n = dist.get_world_size()
+        dist.destroy_process_group()
+    else:
+        n = 1
+        if args.gpus != 1:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has 1 rank")
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": n,
+                          "dry_run": True, "parity": "not run (dry run)",
+                          "dist": {"world_size": n, "backend": "gloo" if n > 1 else None,
+                                   "ranks": ranks}}), flush=True)
 
 
 def dist_info(torch, dist, world, local, args):
@@ -519,11 +618,75 @@ def mctx_device_leg(torch, dist, csum, cdev, rank, world, args):
                    "shard_bounds": bounds,
                    "parity": "ok" if ok else "MISMATCH"}
             del arena, out
+            res["kernel_only"] = single_process_kernel_only(torch, csum, devs)
         except Exception as e:  # noqa: BLE001 - reported, never hidden
             res = {"error": f"{type(e).__name__}: {e}"}
     dist.barrier()
     import json as _json
     return _json.loads(gather_strings(_json.dumps(res), dist)[0])
+
+
+def single_process_kernel_only(torch, csum, devs, rotations=4):
+    """The kernel-only half of the one-process form: device k of `devs`
+    holds M8x1500 shard k resident in its own HBM; one process replays, on
+    every device, a captured graph of `rotations` passes over the shard's 16
+    batches (graph replays, so the host's launch rate is not what is timed),
+    and the wall time from the first replay to the last device's completion
+    gives the aggregate. Parity: every device's results poisoned before the
+    timed replays, then its shard digest vs the reference's."""
+    from tulips_amd.shard import SHARD_SEGMENTS
+    gold = golden_digests().get("M8x1500", {}).get("shards", [])
+    fixed = csum.lib.tulips_csum_batch_fixed
+    per = []
+    for k, d in enumerate(devs):
+        dv = torch.device("cuda", d)
+        with torch.cuda.device(dv):
+            a = torch.empty(SHARD_SEGMENTS * SEG + 256, dtype=torch.uint8, device=dv)
+            csum.fill_splitmix(a, SHARD_SEGMENTS * SEG, seed=DATA_SEED,
+                               byte_off=k * SHARD_SEGMENTS * SEG)
+            o = torch.empty(SHARD_SEGMENTS, dtype=torch.uint16, device=dv)
+            st = torch.cuda.Stream(device=dv)
+
+            def one(stream_h, a=a, o=o):
+                for _ in range(rotations):
+                    for b in range(NBATCH):
+                        rc = fixed(a.data_ptr() + b * NSEG * SEG, SEG, SEG, None, None, None,
+                                   o.data_ptr() + b * NSEG * 2, NSEG, 0, stream_h)
+                        if rc:
+                            raise csum.CsumError(rc, "tulips_csum_batch_fixed")
+            one(st.cuda_stream)
+            torch.cuda.synchronize(dv)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                one(st.cuda_stream)
+        per.append((dv, a, o, st, g))
+
+    def sync_all():
+        for dv, *_ in per:
+            torch.cuda.synchronize(dv)
+    best = None
+    for _ in range(3):
+        for dv, a, o, st, g in per:
+            with torch.cuda.device(dv):
+                o.view(torch.uint8).fill_(0xA5)
+        sync_all()
+        t0 = time.perf_counter()
+        for dv, a, o, st, g in per:
+            with torch.cuda.device(dv):
+                g.replay()
+        sync_all()
+        t = time.perf_counter() - t0
+        best = t if best is None else min(best, t)
+    ok = all(k < len(gold) and fnv1a_u16(o.cpu().numpy().view(np.uint16)) ==
+             gold[k]["fnv1a64"] for k, (dv, a, o, st, g) in enumerate(per))
+    nbytes = float(len(devs)) * rotations * SHARD_SEGMENTS * SEG
+    del per
+    return {"what": "one process, every device checksumming its own resident shard: "
+                    f"a captured graph of {rotations} x 16 F1500 launches replayed per "
+                    "device, wall time first replay -> last device done (best of 3)",
+            "devices": list(devs), "ms": round(best * 1e3, 3),
+            "value_GiBps": round(nbytes / best / GIB, 2),
+            "parity": "ok" if ok else "MISMATCH"}
 
 
 def exchange_overlapped(torch, dist, csum, cdev, stream, arena, rank, world, args,
@@ -712,14 +875,34 @@ PIPE_WIDE = 8   # two per hardware queue (the bench --streams default)
 PIPE_LAUNCHES = 4   # a pipeline graph holds this many times the serial launches
 
 
-def pipe_times(timer, fn, reps):
+def pipe_times(timer, fn, reps, poison=None):
     """Seconds per launch of `fn` over PIPE and over PIPE_WIDE graph branches:
     PIPE_LAUNCHES x reps launches per graph, so its fork and join are spread
     thin (profiles/probe_branches_r03.txt: ZIPF over 160 launches on 4
     branches 7.5-8.8 us, over 640 7.5-7.9), median of 3 replays."""
     n = PIPE_LAUNCHES * reps
-    return (timer(fn, n, branches=PIPE, replays=3),
-            timer(fn, n, branches=PIPE_WIDE, replays=3))
+    return (timer(fn, n, branches=PIPE, replays=3, poison=poison),
+            timer(fn, n, branches=PIPE_WIDE, replays=3, poison=poison))
+
+
+POISON = 0xA5   # byte the outputs are overwritten with before a timed replay
+
+
+def poisoner(*tensors):
+    """A poison() for Timer: every byte of the tensors set to POISON (0xA5A5
+    as a u16 result, 0xA5 as a frame flag byte, which no valid flag set is)."""
+    import torch
+
+    def run():
+        for x in tensors:
+            x.view(torch.uint8).fill_(POISON)
+    return run
+
+
+def row_digests(t, rows, per):
+    """FNV-1a-64 of rows [0, rows) of a flat u16 device tensor, `per` each."""
+    o = t[:rows * per].cpu().numpy().view(np.uint16)
+    return [fnv1a_u16(o[r * per:(r + 1) * per]) for r in range(rows)]
 
 
 def pipe_entry(nbytes, tt):
@@ -773,36 +956,59 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
         "frac_of_peak": round(batch_bytes / t1 / 1e9 / HBM_PEAK_GBS, 4),
         "pipeline": pipe_entry(batch_bytes, tp1)}
 
-    # F9000 (configs[2]): 2 distinct 590 MB batches, rotated (> Infinity Cache)
-    L9 = 9000
-    b9 = NSEG * L9
-    a9 = torch.empty(2 * b9 + 256, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(a9, 2 * b9)
-    o9 = torch.empty(2 * NSEG, dtype=torch.uint16, device=dev)
-    fixed = lib.tulips_csum_batch_fixed
+    gold = golden_digests()
+    rot = golden_rotations()
 
-    def f9(i, st):
-        b = i % 2
-        fixed(a9.data_ptr() + b * b9, L9, L9, None, None, None,
-              o9.data_ptr() + b * NSEG * 2, NSEG, 0, st)
-    for i in range(4):
+    # F9000 (configs[2]): 4 distinct 590 MB batches (2.36 GB, 9x the 256 MB
+    # Infinity Cache) rotated, so every launch streams from HBM; the 2-batch
+    # rotation (1.18 GB) of earlier rounds beside it as `mall_assisted`.
+    # Outputs are poisoned before the timed replay and every batch's digest
+    # is checked against the reference's after it.
+    L9, NB9 = 9000, 4
+    b9 = NSEG * L9
+    a9 = torch.empty(NB9 * b9 + 256, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(a9, NB9 * b9)
+    o9 = torch.empty(NB9 * NSEG, dtype=torch.uint16, device=dev)
+    fixed = lib.tulips_csum_batch_fixed
+    p9 = poisoner(o9)
+
+    def f9_over(nb):
+        def f9(i, st):
+            b = i % nb
+            fixed(a9.data_ptr() + b * b9, L9, L9, None, None, None,
+                  o9.data_ptr() + b * NSEG * 2, NSEG, 0, st)
+        return f9
+
+    def f9_ok(nb):
+        want = rot.get("F9000", [])[:nb]
+        return len(want) == nb and row_digests(o9, nb, NSEG) == want
+    f9 = f9_over(NB9)
+    for i in range(NB9):
         f9(i, sh)
-    t = timer(f9, 40)
-    tp = pipe_times(timer, f9, 40)
+    t = timer(f9, 40, poison=p9)
+    ok9 = f9_ok(NB9)
+    tp = pipe_times(timer, f9, 40, poison=p9)
+    ok9 = ok9 and f9_ok(NB9)
+    t2 = timer(f9_over(2), 40, poison=p9)
+    ok9_2 = f9_ok(2)
     # the F9000 kernel's own read pattern without the arithmetic, over the
-    # same two rotated batches: the ceiling that kernel is held against
+    # same rotated batches: the ceiling that kernel is held against
     sink9 = torch.zeros(4, dtype=torch.int32, device=dev)
 
-    def f9r(i, st):
-        b = i % 2
-        lib.tulips_csum_stream_read_tiles(a9.data_ptr() + b * b9, L9, NSEG, sink9.data_ptr(), st)
-    t9r = timer(f9r, 40)
-    gold = golden_digests()
-    o = o9[:NSEG].cpu().numpy().view(np.uint16)
+    def f9r_over(nb):
+        def f9r(i, st):
+            b = i % nb
+            lib.tulips_csum_stream_read_tiles(a9.data_ptr() + b * b9, L9, NSEG,
+                                              sink9.data_ptr(), st)
+        return f9r
+    t9r = timer(f9r_over(NB9), 40)
+    t9r2 = timer(f9r_over(2), 40)
     tun = csum.default_tuning(L9)
     ex["F9000"] = {"GiBps": round(b9 / t / GIB, 1), "GBps": round(b9 / t / 1e9, 1),
                    "frac_of_peak": round(b9 / t / 1e9 / HBM_PEAK_GBS, 4),
                    "avg_launch_us": round(t * 1e6, 2),
+                   "rotation": f"{NB9} distinct batches of 65,536 x 9000 B "
+                               f"({NB9 * b9 / 1e9:.2f} GB), HBM-resident working set",
                    "pipeline": pipe_entry(b9, tp),
                    "geometry": f"G={tun.group},U={tun.unroll}",
                    "traffic": read_traffic("F9000"),
@@ -811,73 +1017,123 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                                "9000 B tile, 64 lanes x 12 clamped loads), no arithmetic",
                        "avg_launch_us": round(t9r * 1e6, 2),
                        "frac_of_peak": round(b9 / t9r / 1e9 / HBM_PEAK_GBS, 4)},
-                   "parity": "ok" if fnv1a_u16(o) == gold.get("F9000", {}).get("fnv1a64")
-                   else "MISMATCH"}
+                   "mall_assisted": {
+                       "rotation": f"2 batches ({2 * b9 / 1e9:.2f} GB)",
+                       "avg_launch_us": round(t2 * 1e6, 2),
+                       "frac_of_peak": round(b9 / t2 / 1e9 / HBM_PEAK_GBS, 4),
+                       "read_same_bytes_frac": round(b9 / t9r2 / 1e9 / HBM_PEAK_GBS, 4),
+                       "parity": "ok" if ok9_2 else "MISMATCH"},
+                   "parity": "ok" if ok9 else "MISMATCH",
+                   "parity_checked": "outputs poisoned before the timed replays; the "
+                                     f"{NB9} batch digests after them vs the reference's"}
     del a9, o9
 
-    # ZIPF (configs[3]): 8 batches with the same lengths, different bytes
+    # ZIPF (configs[3]): 24 copies with the same lengths, different bytes
+    # (1.05 GB rotated: HBM-resident), the 8-copy rotation (350 MB) beside it
+    # as `mall_assisted`. Copy c = stream bytes [c * zb, (c + 1) * zb); copy 0
+    # is the golden ZIPF arena.
     lens = zipf_lengths(NSEG)
     offs = np.zeros(NSEG, dtype=np.uint64)
     np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
     zb = int(lens.astype(np.int64).sum())
-    nz = 8
+    nz = 24
     az = torch.empty(nz * zb + 256, dtype=torch.uint8, device=dev)
     csum.fill_splitmix(az, nz * zb)
-    # batch 0 = the golden ZIPF arena (stream bytes [0, zb))
     doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
     dlens = torch.from_numpy(lens).to(dev)
     oz = torch.empty(nz * NSEG, dtype=torch.uint16, device=dev)
     batch = lib.tulips_csum_batch
     arena_batch = lib.tulips_csum_batch_arena
+    batch_tuned = lib.tulips_csum_batch_tuned
+    pz = poisoner(oz)
+
+    def z_ok(ncopies):
+        want = rot.get("ZIPF", [])[:ncopies]
+        return len(want) == ncopies and row_digests(oz, ncopies, NSEG) == want
 
     # the batch is one in-order arena (segments back to back): the arena
     # entry point cuts the work by bytes (KIND_SPAN)
-    def fz(i, st):
-        b = i % nz
-        assert arena_batch(az.data_ptr() + b * zb, zb, doffs.data_ptr(), dlens.data_ptr(),
-                           None, None, None, oz.data_ptr() + b * NSEG * 2, NSEG, 0, st) == 0
+    def fz_over(nc):
+        def fz(i, st):
+            b = i % nc
+            assert arena_batch(az.data_ptr() + b * zb, zb, doffs.data_ptr(), dlens.data_ptr(),
+                               None, None, None, oz.data_ptr() + b * NSEG * 2, NSEG, 0, st) == 0
+        return fz
 
     # the same batch through the any-layout entry point (offsets alone)
     def fz_any(i, st):
         b = i % nz
         assert batch(az.data_ptr() + b * zb, doffs.data_ptr(), dlens.data_ptr(), None, None,
                      None, oz.data_ptr() + b * NSEG * 2, NSEG, 0, st) == 0
+
+    # configs[3] as written: one wave (64 lanes) per segment
+    wave_t = csum.Tuning(kind=csum.KIND_SUBGROUP, group=64, unroll=4, sps=1)
+
+    def fz_wave(i, st):
+        b = i % nz
+        assert batch_tuned(az.data_ptr() + b * zb, doffs.data_ptr(), dlens.data_ptr(), None,
+                           None, None, oz.data_ptr() + b * NSEG * 2, NSEG, 0,
+                           __import__("ctypes").byref(wave_t), st) == 0
     for i in range(nz):
         fz_any(i, sh)
-    ta = timer(fz_any, 80)
-    tpa = pipe_times(timer, fz_any, 80)
-    oa = oz[:NSEG].cpu().numpy().view(np.uint16)
-    for i in range(nz):
-        fz(i, sh)
-    t = timer(fz, 80)
-    tp = pipe_times(timer, fz, 80)
-    o = oz[:NSEG].cpu().numpy().view(np.uint16)
-    zgold = gold.get("ZIPF", {}).get("fnv1a64")
+    ta = timer(fz_any, 80, poison=pz)
+    ok_any = z_ok(nz)
+    tpa = pipe_times(timer, fz_any, 80, poison=pz)
+    ok_any = ok_any and z_ok(nz)
+    tw = timer(fz_wave, 80, poison=pz)
+    ok_wave = z_ok(nz)
+    fz = fz_over(nz)
+    t = timer(fz, 80, poison=pz)
+    okz = z_ok(nz)
+    tp = pipe_times(timer, fz, 80, poison=pz)
+    okz = okz and z_ok(nz)
+    t8 = timer(fz_over(8), 80, poison=pz)
+    okz8 = z_ok(8)
     # the single-launch read ceiling for these bytes: a plain streaming read
-    # of one ZIPF arena per launch, the 8 copies rotated
+    # of one ZIPF arena per launch, the copies rotated
     zsink = torch.zeros(4, dtype=torch.int32, device=dev)
     zr = zb & ~15
 
-    def fzr(i, st):
-        b = i % nz
-        lib.tulips_csum_stream_read(az.data_ptr() + b * zr, zr, zsink.data_ptr(), 0, st)
-    tr = timer(fzr, 80)
-    trp = pipe_times(timer, fzr, 80)
+    def fzr_over(nc):
+        def fzr(i, st):
+            b = i % nc
+            lib.tulips_csum_stream_read(az.data_ptr() + b * zr, zr, zsink.data_ptr(), 0, st)
+        return fzr
+    tr = timer(fzr_over(nz), 80)
+    trp = pipe_times(timer, fzr_over(nz), 80)
+    tr8 = timer(fzr_over(8), 80)
     ex["ZIPF"] = {"GiBps": round(zb / t / GIB, 1), "Mseg_per_s": round(NSEG / t / 1e6, 1),
                   "frac_of_peak": round(zb / t / 1e9 / HBM_PEAK_GBS, 4),
                   "avg_launch_us": round(t * 1e6, 2),
+                  "rotation": f"{nz} copies of the golden Zipf batch ({nz * zb / 1e9:.2f} GB), "
+                              "HBM-resident working set",
                   "pipeline": pipe_entry(zb, tp),
                   "entry": "tulips_csum_batch_arena (segments in order in one arena)",
                   "geometry": "span, split form: a workgroup per 28 KiB of arena bytes, "
                               "no halo, chunk prefixes in LDS, boundary chunks loaded by "
-                              "the entry holders ahead of the range's last rows; a segment crossing ranges is summed in "
-                              "parts that meet in a per-range word (one returning atomic "
-                              "per part)",
+                              "the entry holders ahead of the range's last rows; a segment "
+                              "crossing ranges is summed in parts that meet in a per-range "
+                              "word (one returning atomic per part)",
                   "traffic": read_traffic("ZIPF"),
-                  "parity": "ok" if fnv1a_u16(o) == zgold else "MISMATCH",
+                  "parity": "ok" if okz else "MISMATCH",
+                  "parity_checked": "outputs poisoned before the timed replays; the "
+                                    f"{nz} copy digests after them vs the reference's",
                   "read_same_bytes": {"avg_launch_us": round(tr * 1e6, 2),
                                       "frac_of_peak": round(zr / tr / 1e9 / HBM_PEAK_GBS, 4),
                                       "pipeline": pipe_entry(zr, trp)},
+                  "mall_assisted": {"rotation": f"8 copies ({8 * zb / 1e6:.0f} MB)",
+                                    "avg_launch_us": round(t8 * 1e6, 2),
+                                    "frac_of_peak": round(zb / t8 / 1e9 / HBM_PEAK_GBS, 4),
+                                    "read_same_bytes_frac": round(
+                                        zr / tr8 / 1e9 / HBM_PEAK_GBS, 4),
+                                    "parity": "ok" if okz8 else "MISMATCH"},
+                  "one_wave_per_segment": {
+                      "what": "BASELINE configs[3] as written: tulips_csum_batch with one "
+                              "64-lane wave per segment (KIND_SUBGROUP, group 64, unroll 4)",
+                      "GBps": round(zb / tw / 1e9, 1),
+                      "frac_of_peak": round(zb / tw / 1e9 / HBM_PEAK_GBS, 4),
+                      "avg_launch_us": round(tw * 1e6, 2),
+                      "parity": "ok" if ok_wave else "MISMATCH"},
                   "any_layout": {
                       "entry": "tulips_csum_batch (offsets only)",
                       "geometry": "packed: one wave per 8 segments, chunks packed end to "
@@ -886,7 +1142,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                       "frac_of_peak": round(zb / ta / 1e9 / HBM_PEAK_GBS, 4),
                       "avg_launch_us": round(ta * 1e6, 2),
                       "pipeline": pipe_entry(zb, tpa),
-                      "parity": "ok" if fnv1a_u16(oa) == zgold else "MISMATCH"}}
+                      "parity": "ok" if ok_any else "MISMATCH"}}
     del az, oz
 
     # end-to-end host path: F1500 batch from host memory, results back to host
@@ -913,6 +1169,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     except Exception as e:  # noqa: BLE001
         ex["mctx_host_F1500"] = {"error": repr(e)}
     ex["burst_latency_host"] = burst_latency(torch, csum)
+    ex["F1500_beside_resident_server"] = beside_server(torch, csum, timer, arena, batch_bytes)
     ex.update(frame_extras(torch, csum, dev, timer))
     return ex
 
@@ -985,7 +1242,8 @@ def burst_latency(torch, csum):
             flags = np.empty(nf, np.uint8)
             ent = {}
             for name, path, resident in (("staged", 0, False), ("zero_copy", 1, False),
-                                         ("zero_copy_resident", 1, True)):
+                                         ("zero_copy_resident", 1, True),
+                                         ("cpu_product", 2, False)):
                 ctx.set_lowlat(resident)
                 reps = 2000 if nf <= 64 else 300
                 rc = csum.lib.tulips_csum_time_validate(
@@ -1000,9 +1258,51 @@ def burst_latency(torch, csum):
                 if path == 1:
                     ent[name]["gpu_service_us"] = round(out[4], 2)
             res[str(nf)] = ent
+    # the burst size from which the zero-copy launch beats the host code
+    cross = None
+    for nf in BURSTS:
+        e = res[str(nf)]
+        if "us_median" in e.get("zero_copy", {}) and "us_median" in e.get("cpu_product", {}) \
+                and e["zero_copy"]["us_median"] < e["cpu_product"]["us_median"]:
+            cross = nf
+            break
     return {"workload": "TCP frames of 1514 B in 2 KiB page-locked host slots, one "
-                        "validation call per burst, C-timed (tulips_csum_time_validate)",
+                        "validation call per burst, C-timed (tulips_csum_time_validate); "
+                        "cpu_product = tulips_csum_validate_frames_cpu, the library's host "
+                        "code the gpucsum decorator uses below its crossover",
+            "gpu_beats_cpu_from_burst": cross,
             "bursts": res}
+
+
+def beside_server(torch, csum, timer, arena, batch_bytes):
+    """What the resident low-latency server (8 workgroups of 1,024 threads
+    polling the mailbox, tulips_csum_ctx_set_lowlat) costs a bulk kernel
+    sharing the GPU: the F1500 serial launch rate with the server idle-
+    polling beside it, against the same launches without it."""
+    fixed = csum.lib.tulips_csum_batch_fixed
+    outs = torch.empty(NBATCH * NSEG, dtype=torch.uint16, device=arena.device)
+
+    def f(i, st):
+        b = i % NBATCH
+        fixed(arena.data_ptr() + b * batch_bytes, SEG, SEG, None, None, None,
+              outs.data_ptr() + b * NSEG * 2, NSEG, 0, st)
+    t_alone = timer(f, 64)
+    ar, offs, lens = burst_frames(8)
+    pinned = torch.from_numpy(ar).pin_memory()
+    with csum.HostContext(torch.cuda.current_device()) as ctx:
+        ctx.set_lowlat(True)
+        fl = ctx.validate_frames(pinned.numpy(), offs, lens, low_latency=True)
+        # the server idles out 100 ms after its last burst: the capture,
+        # warm replay and timed replay of 64 launches take a few ms
+        t_srv = timer(f, 64)
+        fl2 = ctx.validate_frames(pinned.numpy(), offs, lens, low_latency=True)
+    ok = bool((fl == 0x0F).all()) and bool((fl2 == 0x0F).all())
+    return {"what": "F1500 serial launches with the resident zero-copy server idle-polling "
+                    "on the same GPU (8 x 1,024-thread workgroups) vs without",
+            "avg_launch_us_alone": round(t_alone * 1e6, 2),
+            "avg_launch_us_with_server": round(t_srv * 1e6, 2),
+            "slowdown": round(t_srv / t_alone, 4),
+            "parity": "ok" if ok else "MISMATCH"}
 
 
 def rate_entry(alg_bytes, t, **kw):
@@ -1044,10 +1344,15 @@ def frame_extras(torch, csum, dev, timer):
         b = i % nb
         val(ar.data_ptr() + b * burst, offs.data_ptr(), lens.data_ptr(), nf,
             flags.data_ptr() + b * nf, None, st)
+    def gen_poison():
+        # both checksum fields of every frame: what the timed replay must write
+        # (checked below by the fields comparison and by validation == 0x0F)
+        v[:, 24:26].fill_(POISON)
+        v[:, 50:52].fill_(POISON)
     for i in range(nb):
         fgen(i, torch.cuda.current_stream().cuda_stream)
-    t = timer(fgen, 64)
-    tp = pipe_times(timer, fgen, 64)
+    t = timer(fgen, 64, poison=gen_poison)
+    tp = pipe_times(timer, fgen, 64, poison=gen_poison)
     ex["frames_generate_F1514"] = rate_entry(
         alg, t, kernel="frame_kernel<GENERATE, 16 lanes x 6 chunks per frame>",
         workload="65,536 x 1514 B TCP frames per launch, 2 KiB slots, 8 bursts rotated",
@@ -1065,8 +1370,8 @@ def frame_extras(torch, csum, dev, timer):
             fields.data_ptr() + b * nf * 4, None, st)
     for i in range(nb):
         ffld(i, torch.cuda.current_stream().cuda_stream)
-    t = timer(ffld, 64)
-    tp = pipe_times(timer, ffld, 64)
+    t = timer(ffld, 64, poison=poisoner(fields))
+    tp = pipe_times(timer, ffld, 64, poison=poisoner(fields))
     fv = v.view(nb * nf, slot)
     want = (fv[:, 24].int() | (fv[:, 25].int() << 8) | (fv[:, 50].int() << 16) |
             (fv[:, 51].int() << 24))
@@ -1077,9 +1382,10 @@ def frame_extras(torch, csum, dev, timer):
         pipeline=pipe_entry(alg + 4 * nf, tp), parity="ok" if ok else "MISMATCH",
         traffic=read_traffic("frames_generate_fields_F1514"))
     del fields, fv, want
-    t = timer(fval, 64)
-    tp = pipe_times(timer, fval, 64)
+    t = timer(fval, 64, poison=poisoner(flags))
     ok = bool((flags == 0x0F).all().item())
+    tp = pipe_times(timer, fval, 64, poison=poisoner(flags))
+    ok = ok and bool((flags == 0x0F).all().item())
     ex["frames_validate_F1514"] = rate_entry(
         alg, t, kernel="frame_kernel<VALIDATE, 16 lanes x 6 chunks per frame>",
         workload="same frames: generated checksums verified (flags == 0x0F)",
@@ -1134,12 +1440,16 @@ def frame_extras(torch, csum, dev, timer):
             solen.data_ptr() + b * nseg * 2, sfirst.data_ptr() + b * (nsf + 1) * 4, st)
     for i in range(sb):
         fseg(i, torch.cuda.current_stream().cuda_stream)
-    t = timer(fseg, 32)
-    tp = pipe_times(timer, fseg, 32)
+    t = timer(fseg, 32, poison=poisoner(sout, solen, sfirst))
+    tp = pipe_times(timer, fseg, 32, poison=poisoner(sout, solen, sfirst))
     moved = nsf * sflen + nseg * (54 + mss)       # read super-frames + write segments
     so = torch.arange(nseg, dtype=torch.int64, device=dev) * ostride
-    sfl = csum.validate_frames(sout[:nseg * ostride], so, solen[:nseg])
-    ok = bool((sfl == 0x0F).all().item()) and int(sfirst[nsf].item()) == nseg
+    ok = True
+    for b in range(sb):     # every rotated call's segments, written in the timed replays
+        sfl = csum.validate_frames(sout[b * nseg * ostride:(b + 1) * nseg * ostride], so,
+                                   solen[b * nseg:(b + 1) * nseg])
+        ok = ok and bool((sfl == 0x0F).all().item()) and \
+            int(sfirst[b * (nsf + 1) + nsf].item()) == nseg
     ex["segment_TSO_64K_mss1460"] = rate_entry(
         moved, t, kernel="seg_prologue_small_kernel + segment_kernel<16,6> "
                          "(16-lane subgroup per output segment)",
@@ -1165,8 +1475,8 @@ def frame_extras(torch, csum, dev, timer):
         rss(sa_.data_ptr(), da_.data_ptr(), sp_.data_ptr(), dp_.data_ptr(), nt, kp, len(key),
             0, rout.data_ptr(), st)
     frss(0, torch.cuda.current_stream().cuda_stream)
-    t = timer(frss, 32)
-    tp = pipe_times(timer, frss, 32)
+    t = timer(frss, 32, poison=poisoner(rout))
+    tp = pipe_times(timer, frss, 32, poison=poisoner(rout))
     # parity: 2,048 tuples spread over the batch against the host symbol
     js = torch.arange(0, nt, nt // 2048)
     cols = [x.cpu().numpy() for x in (sa_[js], da_[js], sp_[js], dp_[js], rout[js])]

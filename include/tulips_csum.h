@@ -229,12 +229,13 @@ int tulips_csum_mctx_batch_arena_device(tulips_csum_mctx* ctx, const uint8_t* ba
 /*
  * Flow-affine receive validation ("enables flow-affine GPU
  * sharding"), the GPU analogue of NIC RSS queues with an indirection table
- * (src/transport/ena/RedirectionTable.cpp:74-98): every option-less
- * IPv4/TCP frame's 4-tuple (saddr | daddr | sport | dport, as
+ * (src/transport/ena/RedirectionTable.cpp:74-98): every option-less,
+ * unfragmented IPv4/TCP frame's 4-tuple (saddr | daddr | sport | dport, as
  * tulips_rss_toeplitz_batch takes it) is hashed with the `key_len`-byte
  * Toeplitz key from `init` on the context's first device, and the frame is
  * validated on device table[hash % table_len] (entries index the context's
- * devices); frames without such a tuple go to table[0]. All frames of one
+ * devices); frames without such a tuple (including IPv4 fragments: MF set
+ * or a fragment offset) go to table[0]. All frames of one
  * flow therefore land on one device, in arrival order. `flags` (and the
  * summed `counters`) come back in arrival order; `device_of` (host uint16[n],
  * may be NULL) receives each frame's device index. All arrays are host
@@ -383,6 +384,19 @@ int tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
                                      const uint64_t* offsets,
                                      const uint16_t* lengths, uint32_t n,
                                      uint8_t* flags, uint32_t* counters);
+
+/*
+ * The same flags and counters for host-resident frames computed on the
+ * calling thread with the host scalar drop-ins (tulips_csum_ipv4_host,
+ * tulips_csum_tcp_host; no GPU involved), as the reference verifies each
+ * frame in its poll loop (src/stack/ipv4/Processor.cpp:94-103,
+ * src/stack/tcpv4/Processor.cpp:120-132). For poll bursts too small to pay
+ * for a PCIe round trip: the gpucsum decorator takes it below its measured
+ * crossover (a few dozen 1514 B frames). All arrays are host arrays.
+ */
+int tulips_csum_validate_frames_cpu(const uint8_t* base, const uint64_t* offsets,
+                                    const uint16_t* lengths, uint32_t n,
+                                    uint8_t* flags, uint32_t* counters);
 
 /*
  * Low-latency (zero-copy) form of tulips_csum_validate_frames_host for poll

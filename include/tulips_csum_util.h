@@ -108,7 +108,8 @@ int tulips_csum_stream_read_slots(const uint8_t* p, uint64_t slot_bytes, uint32_
 /* Latency of `reps` back-to-back receive validations of one burst of
  * host-resident frames, timed in C with a steady clock around each call
  * (no interpreter in the loop): path 0 = tulips_csum_validate_frames_host
- * (staged), 1 = tulips_csum_validate_frames_zc. out[0..4] = median, p99,
+ * (staged), 1 = tulips_csum_validate_frames_zc, 2 =
+ * tulips_csum_validate_frames_cpu (host code, no GPU). out[0..4] = median, p99,
  * min, mean (us) and, for path 1, the median GPU service time (request
  * picked up -> flags out, from the server's realtime clock; 0 otherwise).
  * `flags` (n bytes) holds the last call's flags. */
@@ -116,6 +117,17 @@ typedef struct tulips_csum_ctx tulips_csum_ctx;
 int tulips_csum_time_validate(tulips_csum_ctx* ctx, int path, const uint8_t* base,
                               const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
                               uint32_t reps, uint8_t* flags, double* out);
+
+/* Test hooks. tulips_csum_ctx_debug_set_seq: the sequence number of the
+ * context's last zero-copy request (its low 16 bits tag the next request's
+ * doorbell and completion words), to reach tag wrap-around in a test.
+ * tulips_csum_mctx_set_peer_mode: how device-resident mctx calls move a
+ * piece to a device other than the source: 0 = over xGMI (peer DMA) where
+ * hipDeviceCanAccessPeer allows it, else staged through page-locked host
+ * memory (the default); 1 = always staged. */
+int tulips_csum_ctx_debug_set_seq(tulips_csum_ctx* ctx, uint64_t seq);
+typedef struct tulips_csum_mctx tulips_csum_mctx;
+int tulips_csum_mctx_set_peer_mode(tulips_csum_mctx* ctx, int mode);
 
 #ifdef __cplusplus
 }

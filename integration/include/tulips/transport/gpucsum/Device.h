@@ -7,9 +7,12 @@
  * (include/tulips/transport/check/Device.h, src/transport/check/Device.cpp:
  * 14-36): it wraps any transport::Device, drains up to `burst` frames per
  * poll from it into a page-locked staging arena, validates the whole burst
- * in one GPU launch (tulips_csum_validate_frames_host: Ethernet -> IPv4
- * header checksum -> TCP pseudo-header checksum, include/tulips_csum.h),
- * and forwards to the stack only the frames that pass, in arrival order.
+ * in one GPU launch (tulips_csum_validate_frames_zc / _host: Ethernet ->
+ * IPv4 header checksum -> TCP pseudo-header checksum, include/tulips_csum.h;
+ * bursts below Config::cpu_below frames on the polling thread with the
+ * library's host code, tulips_csum_validate_frames_cpu, as the reference
+ * would per frame), and forwards to the stack only the frames that pass, in
+ * arrival order.
  *
  * It realises the Device::VALIDATE_IP_CSUM / VALIDATE_L4_CSUM hints
  * (include/tulips/transport/Device.h:29-30) the way the ENA and OFED
@@ -67,6 +70,7 @@ public:
     uint64_t bad_ip = 0;     // dropped: IPv4 header checksum
     uint64_t bad_l4 = 0;     // dropped: TCP checksum / truncation
     uint64_t batches = 0;    // GPU launches
+    uint64_t cpu_batches = 0; // bursts below the crossover, validated on the host
     uint64_t tx_frames = 0;  // committed by the stack (tx)
     uint64_t tx_segments = 0; // frames committed to the inner device (tx)
     uint64_t tx_batches = 0; // GPU batches on the transmit side
@@ -77,6 +81,12 @@ public:
   // staged one at every burst size up to its 1,024-frame limit: DESIGN.md §5
   // "Latency per poll burst")
   static constexpr uint32_t DEFAULT_LOWLAT = 1024;
+  // bursts of fewer frames are validated on the polling thread by the
+  // library's host code (tulips_csum_validate_frames_cpu): below this size a
+  // PCIe round trip to the GPU costs more than the per-frame checks do on
+  // the CPU (DESIGN.md §5 "Latency per poll burst": ~0.2 us per 1514 B frame
+  // on the host against ~10 us for a zero-copy launch)
+  static constexpr uint32_t DEFAULT_CPU_BELOW = 32;
 
   struct Config
   {
@@ -92,6 +102,8 @@ public:
     uint32_t lowlat = DEFAULT_LOWLAT;
     // ... served by workgroups resident on the GPU (no launch per burst)
     bool lowlat_resident = false;
+    // receive: bursts of fewer frames stay on the CPU; 0 = always the GPU
+    uint32_t cpu_below = DEFAULT_CPU_BELOW;
   };
 
   static Ref allocate(system::Logger& log, transport::Device::Ref device,
@@ -113,7 +125,10 @@ public:
 
   /*
    * Throws std::runtime_error when the GPU context cannot be created (no
-   * device, no libtulips_csum): there is no CPU fallback.
+   * device, no libtulips_csum). Bursts below Config::cpu_below are a latency
+   * choice made per burst, not a fallback: every larger burst goes to the
+   * GPU, and a GPU failure is reported as HardwareError, never retried on
+   * the CPU.
    */
   Device(system::Logger& log, transport::Device::Ref device, Config const& config);
   ~Device() override;
@@ -214,6 +229,7 @@ private:
   uint32_t m_tx_burst;
   uint32_t m_tso;
   uint32_t m_lowlat;
+  uint32_t m_cpu_below;
   std::vector<Pending> m_pending;
   std::unordered_set<uint8_t*> m_own;        // our TSO send buffers
   std::vector<uint8_t*> m_free;              // ... not handed out

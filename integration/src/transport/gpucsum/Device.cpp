@@ -44,6 +44,7 @@ Device::Device(system::Logger& log, transport::Device::Ref device,
   , m_tx_burst(std::max<uint32_t>(config.tx_burst, 1))
   , m_tso(config.tso ? std::max<uint32_t>(config.tso, m_device->mss()) : 0)
   , m_lowlat(config.lowlat)
+  , m_cpu_below(config.cpu_below)
 {
   m_hints |= config.hints;
   // Room for a whole burst of 2 KiB receive buffers (the OFED RX layout,
@@ -355,14 +356,22 @@ Device::flush()
   if (n == 0) {
     return Status::Ok;
   }
-  // small bursts: the resident server reads the pinned arena in place
-  const int rc =
-    n <= m_lowlat
-      ? tulips_csum_validate_frames_zc(m_ctx, m_arena, m_offsets.data(),
-                                       m_lengths.data(), n, m_flags.data(), nullptr)
-      : tulips_csum_validate_frames_host(m_ctx, m_arena, m_offsets.data(),
-                                         m_lengths.data(), n, m_flags.data(), nullptr);
-  m_stats.batches += 1;
+  // tiny bursts on this thread (cheaper than a PCIe round trip), small
+  // ones read in place from the pinned arena by the zero-copy path, large
+  // ones staged through the context's DMA pipeline
+  int rc;
+  if (n < m_cpu_below) {
+    rc = tulips_csum_validate_frames_cpu(m_arena, m_offsets.data(), m_lengths.data(), n,
+                                         m_flags.data(), nullptr);
+    m_stats.cpu_batches += 1;
+  } else {
+    rc = n <= m_lowlat
+           ? tulips_csum_validate_frames_zc(m_ctx, m_arena, m_offsets.data(),
+                                            m_lengths.data(), n, m_flags.data(), nullptr)
+           : tulips_csum_validate_frames_host(m_ctx, m_arena, m_offsets.data(),
+                                              m_lengths.data(), n, m_flags.data(), nullptr);
+    m_stats.batches += 1;
+  }
   Status ret = Status::Ok;
   if (rc != TULIPS_STATUS_OK) {
     m_log.error("GPUCSUM", "batch validation failed: ",

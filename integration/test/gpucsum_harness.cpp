@@ -49,12 +49,35 @@ struct Recorder : transport::Processor
 
 constexpr uint32_t LIST_MTU = 65536;
 
+int run_cfg(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens, uint32_t n,
+            uint32_t burst, uint16_t hints, int use_wait, int64_t cpu_below,
+            uint8_t* forwarded, uint64_t* stats);
+
 }
 
 extern "C" int
 gpucsum_run(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
             uint32_t n, uint32_t burst, uint16_t hints, int use_wait,
             uint8_t* forwarded, uint64_t* stats)
+{
+  return run_cfg(arena, offs, lens, n, burst, hints, use_wait, -1, forwarded, stats);
+}
+
+// gpucsum_run with Config::cpu_below set (stats[5] = cpu_batches).
+extern "C" int
+gpucsum_run_cpu_below(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
+                      uint32_t n, uint32_t burst, uint16_t hints, uint32_t cpu_below,
+                      uint8_t* forwarded, uint64_t* stats)
+{
+  return run_cfg(arena, offs, lens, n, burst, hints, 0, cpu_below, forwarded, stats);
+}
+
+namespace {
+
+int
+run_cfg(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens, uint32_t n,
+        uint32_t burst, uint16_t hints, int use_wait, int64_t cpu_below,
+        uint8_t* forwarded, uint64_t* stats)
 {
   try {
     system::ConsoleLogger log(system::Logger::Level::Error);
@@ -75,6 +98,9 @@ gpucsum_run(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
     transport::gpucsum::Device::Config cfg;
     cfg.burst = burst;
     cfg.hints = hints;
+    if (cpu_below >= 0) {
+      cfg.cpu_below = uint32_t(cpu_below);
+    }
     transport::gpucsum::Device dev(log, std::move(rx), cfg);
     Recorder rec;
     Status s = Status::Ok;
@@ -106,11 +132,16 @@ gpucsum_run(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
     stats[2] = st.bad_ip;
     stats[3] = st.bad_l4;
     stats[4] = st.batches;
+    if (cpu_below >= 0) {
+      stats[5] = st.cpu_batches;
+    }
     return 0;
   } catch (std::exception const& e) {
     fprintf(stderr, "gpucsum_run: %s\n", e.what());
     return -1;
   }
+}
+
 }
 
 // Transmit side: the stack's frames (arena/offs/lens, checksum fields as the

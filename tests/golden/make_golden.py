@@ -189,14 +189,80 @@ def digests(ref: Reference, orc: Oracle) -> dict:
     for r in range(8):
         arena = orc.splitmix_bytes(shard_n * L, byte_off=r * shard_n * L)
         v = ref.batch(arena, stride=L, fixed_len=L, n=shard_n, mode=MODE_RAW, **kw)
-        shard_digests.append(digest(orc, v))
+        shard_digests.append(dict(digest(orc, v), batches=m8_batch_digests(orc, v)))
         all_out.append(v)
         del arena
     full = np.concatenate(all_out)
     d["batches"]["M8x1500"] = dict(n=8 * shard_n, length=L, stride=L, mode="raw",
                                    shards=shard_digests, **digest(orc, full))
-    # one 65,536-segment batch of each shard: bench.py's rotating F1500 steps
+    d["rotations"] = rotation_digests(ref, orc)
     return d
+
+
+def rotation_digests(ref, orc, n9=4, nz=24):
+    """Digests of the distinct batches bench.py rotates over so that its
+    side measurements stream from HBM: F9000 batch b = SplitMix64 stream
+    bytes [b * 589,824,000, ...) (stride 9000), ZIPF copy c = the golden Zipf
+    lengths over stream bytes [c * 43,772,673, ...). Batch/copy 0 are the
+    F9000 / ZIPF digests."""
+    N = 65536
+    out = {"F9000": [], "ZIPF": []}
+    b9 = N * 9000
+    for b in range(n9):
+        arena = orc.splitmix_bytes(b9, byte_off=b * b9)
+        v = ref.batch(arena, stride=9000, fixed_len=9000, n=N, mode=MODE_RAW,
+                      nthreads=NTHREADS)
+        out["F9000"].append(f"{orc.fnv1a_u16(v):016x}")
+        del arena
+    lens = orc.zipf_lengths(N)
+    offs = packed_offsets(lens)
+    zb = int(lens.astype(np.int64).sum())
+    for c in range(nz):
+        arena = orc.splitmix_bytes(zb, byte_off=c * zb)
+        v = ref.batch(arena, offs, lens, mode=MODE_RAW, nthreads=NTHREADS)
+        out["ZIPF"].append(f"{orc.fnv1a_u16(v):016x}")
+    return out
+
+
+def patch_rotations():
+    """Add rotation_digests() to an existing digests.json."""
+    ref, orc = Reference(), Oracle()
+    path = os.path.join(HERE, "digests.json")
+    with open(path) as f:
+        d = json.load(f)
+    d["rotations"] = rotation_digests(ref, orc)
+    assert d["rotations"]["F9000"][0] == d["batches"]["F9000"]["fnv1a64"]
+    assert d["rotations"]["ZIPF"][0] == d["batches"]["ZIPF"]["fnv1a64"]
+    with open(path, "w") as f:
+        json.dump(d, f, indent=1)
+
+
+def m8_batch_digests(orc, shard_out):
+    """FNV-1a-64 of each 65,536-segment batch of one M8 shard's results:
+    bench.py's rotating F1500 steps (a step writes one batch), so a timed run
+    of fewer than 16 steps still has a reference digest per batch written."""
+    return [f"{orc.fnv1a_u16(shard_out[b * 65536:(b + 1) * 65536]):016x}"
+            for b in range(len(shard_out) // 65536)]
+
+
+def patch_m8_batches():
+    """Add the per-batch digests to an existing digests.json (same reference
+    build, same arenas as digests())."""
+    ref, orc = Reference(), Oracle()
+    path = os.path.join(HERE, "digests.json")
+    with open(path) as f:
+        d = json.load(f)
+    shard_n, L = 1 << 20, 1500
+    m8 = d["batches"]["M8x1500"]
+    for r in range(8):
+        arena = orc.splitmix_bytes(shard_n * L, byte_off=r * shard_n * L)
+        v = ref.batch(arena, stride=L, fixed_len=L, n=shard_n, mode=MODE_RAW,
+                      nthreads=NTHREADS)
+        assert f"{orc.fnv1a_u16(v):016x}" == m8["shards"][r]["fnv1a64"]
+        m8["shards"][r]["batches"] = m8_batch_digests(orc, v)
+        del arena
+    with open(path, "w") as f:
+        json.dump(d, f, indent=1)
 
 
 RSS_KEYS = {
@@ -357,4 +423,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    if sys.argv[1:] == ["--m8-batches"]:
+        patch_m8_batches()
+    elif sys.argv[1:] == ["--rotations"]:
+        patch_rotations()
+    else:
+        main()

@@ -1,0 +1,76 @@
+"""bench.py's multi-rank launch (the driver runs `python bench.py --gpus N`
+with no launcher of its own): with WORLD_SIZE unset and --gpus N > 1, the
+script starts `torch.distributed.run --nproc-per-node N` itself as a child
+process, every rank checks that the process group holds N ranks, and rank 0
+prints the one JSON line.
+
+The CPU test drives that launch path with --dry-run (the ranks form the gloo
+group and report it, no GPU call); the GPU test runs the whole bench with 4
+ranks sharing the one GPU of the test box (--one-device, gloo), every rank's
+measured shard checked against the reference's digests.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def _json_lines(out):
+    return [json.loads(x) for x in out.splitlines() if x.startswith("{")]
+
+
+def test_self_launch_forms_the_group_without_a_launcher():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4",
+                        "--dist-backend", "gloo", "--one-device", "--dry-run"],
+                       capture_output=True, text=True, env=_env(), timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 4 and line["dist"]["world_size"] == 4
+    assert sorted(line["dist"]["ranks"]) == [0, 1, 2, 3]
+
+
+def test_single_rank_dry_run_and_world_mismatch():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"],
+                       capture_output=True, text=True, env=_env(), timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _json_lines(r.stdout)[0]["n_gpus"] == 1
+    # a launcher that gives the group a different size than --gpus is refused
+    env = _env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run"], capture_output=True, text=True, env=env, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode != 0 and "process group has 1 rank" in r.stderr
+
+
+@pytest.mark.gpu
+def test_self_launched_four_ranks_on_one_gpu():
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "4",
+                        "--dist-backend", "gloo", "--one-device", "--steps", "32",
+                        "--warmup", "4", "--no-extras"],
+                       capture_output=True, text=True, env=_env(), timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = lines[0]
+    assert line["n_gpus"] == 4 and line["dist"]["world_size"] == 4
+    assert line["parity"] == "ok", line.get("parity_checked")
+    assert line["value"] > 0
+    mg = line["multi_gpu"]
+    assert mg["library_scatter_from_gpu0"]["parity"] == "ok", mg["library_scatter_from_gpu0"]
+    assert mg["library_scatter_from_gpu0"]["kernel_only"]["parity"] == "ok"
+    for leg in ("exchange_overlapped", "scatter_from_gpu0", "zipf_byte_balanced"):
+        assert mg[leg].get("parity") == "ok", (leg, mg[leg])

@@ -109,6 +109,37 @@ def test_capi_arguments_without_gpu():
             csum.FRAME_TRUNCATED) == (IPV4, IP_OK, TCP, L4_OK, TRUNC)
 
 
+def test_cpu_validation_matches_fixture():
+    """tulips_csum_validate_frames_cpu (the library's host code, used by the
+    gpucsum decorator below its crossover) against the reference-computed
+    flags, and its counters."""
+    from tulips_amd import csum
+    fx = frames_fixture()
+    got, cnt = csum.validate_frames_cpu(fx["arena"], fx["offsets"], fx["lengths"],
+                                        with_counters=True)
+    np.testing.assert_array_equal(got, fx["expect"])
+    np.testing.assert_array_equal(cnt, counters_of(fx["expect"]))
+
+
+def test_cpu_validation_mutations_and_jumbo(oracle):
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(404)
+    for _ in range(4):
+        arena = mutate(fx, rng, 2500)
+        exp = oracle.validate_frames(arena, fx["offsets"], fx["lengths"])
+        np.testing.assert_array_equal(
+            csum.validate_frames_cpu(arena, fx["offsets"], fx["lengths"]), exp)
+    fr = [make_frame(oracle, rng, p) for p in (0, 1, 8946, 65535 - 54)]
+    for lead in (0, 1, 3):
+        arena, offs, lens = pack(fr, rng, lead=lead)
+        assert list(csum.validate_frames_cpu(arena, offs, lens)) == [0x0F] * 4
+    # arguments: n == 0 is a no-op; neither flags nor counters
+    L = csum.lib
+    assert L.tulips_csum_validate_frames_cpu(None, None, None, 0, None, None) == 0
+    assert L.tulips_csum_validate_frames_cpu(0x1000, 0x1000, 0x1000, 3, None, None) == 1
+
+
 # ---------------------------------------------------------------- GPU -----
 def _dev(*arrs):
     import torch
@@ -294,6 +325,63 @@ def test_gpu_zero_copy_bursts(oracle, pinned, resident):
             got = ctx.validate_frames(arena, fx["offsets"][k:k + 1], fx["lengths"][k:k + 1],
                                       low_latency=True)
             assert got[0] == exp[k], k
+
+
+@pytest.mark.gpu
+def test_gpu_zero_copy_tag_wraparound(oracle):
+    """One launch per burst publishes a 16-bit tag per answering workgroup.
+    A 1,024-frame burst (16 workgroups) under tag T, then 1-frame bursts,
+    then the sequence moved so the next 1,024-frame burst is tagged T again:
+    its flags must be its own (the words of the earlier T are cleared before
+    each launch), not the earlier burst's (csum_host.hip)."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(65535)
+    buf = torch.empty(len(fx["arena"]), dtype=torch.uint8).pin_memory()
+    arena = buf.numpy()
+    o, ln = fx["offsets"][:1024], fx["lengths"][:1024]
+    with csum.HostContext(0) as ctx:
+        for wrap in range(3):
+            seq = 65530 + 977 * wrap                    # tag T = (seq + 1) & 0xffff
+            arena[:] = fx["arena"]
+            ctx.debug_set_seq(seq)
+            got = ctx.validate_frames(arena, o, ln, low_latency=True)
+            np.testing.assert_array_equal(got, fx["expect"][:1024])
+            for _ in range(3):
+                ctx.validate_frames(arena, o[:1], ln[:1], low_latency=True)
+            # the same tag again, different bytes (every frame's IP header hit)
+            arena[:] = fx["arena"]
+            arena[o.astype(np.int64) + 15] ^= 0xFF
+            exp = oracle.validate_frames(arena, o, ln)
+            assert not np.array_equal(exp, fx["expect"][:1024])
+            ctx.debug_set_seq(seq + 65536)              # the next request is tagged T
+            for _ in range(5):
+                got = ctx.validate_frames(arena, o, ln, low_latency=True)
+                np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.gpu
+def test_gpu_zero_copy_pinned_range_reused(oracle):
+    """The zero-copy path looks the page-locked allocation up on every call:
+    an arena freed and replaced by another allocation (page-locked or
+    pageable) at the same or another address is read from where it is now
+    (csum_host.hip zc_validate)."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(12)
+    o, ln = fx["offsets"][:200], fx["lengths"][:200]
+    with csum.HostContext(0) as ctx:
+        for rnd in range(6):
+            data = mutate(fx, rng, 400)
+            exp = oracle.validate_frames(data, o, ln)
+            buf = torch.from_numpy(data.copy())
+            if rnd % 2 == 0:
+                buf = buf.pin_memory()
+            got = ctx.validate_frames(buf.numpy(), o, ln, low_latency=True)
+            np.testing.assert_array_equal(got, exp, err_msg=str(rnd))
+            del buf
 
 
 @pytest.mark.gpu

@@ -100,6 +100,55 @@ def test_burst_sizes(burst):
         assert int(st[4]) == 1          # the whole poll burst in one launch
 
 
+def run_cpu_below(fx, burst, cpu_below, n=None):
+    from tulips_amd import csum  # noqa: F401
+    lib = C.CDLL(HARNESS)
+    f = lib.gpucsum_run_cpu_below
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint16,
+                  C.c_uint32, C.c_void_p, C.c_void_p]
+    n = len(fx["offsets"]) if n is None else n
+    arena = np.ascontiguousarray(fx["arena"])
+    offs = np.ascontiguousarray(fx["offsets"][:n])
+    lens = np.ascontiguousarray(fx["lengths"][:n])
+    fwd = np.zeros(n, dtype=np.uint8)
+    stats = np.zeros(6, dtype=np.uint64)
+    rc = f(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, burst, 3, cpu_below,
+           fwd.ctypes.data, stats.ctypes.data)
+    assert rc == 0, f"gpucsum_run_cpu_below rc={rc}"
+    return fwd, stats
+
+
+@needs_harness
+@pytest.mark.gpu
+@pytest.mark.parametrize("burst", [1, 2, 8, 31, 32, 64, 256, 1024, 4096])
+def test_cpu_crossover_by_burst(burst):
+    """Config::cpu_below (default 32): bursts below it are validated on the
+    polling thread by tulips_csum_validate_frames_cpu, the rest on the GPU;
+    either way the frames forwarded are exactly those the reference-derived
+    flags pass, in arrival order."""
+    fx = fixture()
+    n = min(len(fx["offsets"]), max(64 * burst, 600) if burst < 32 else len(fx["offsets"]))
+    fwd, st = run_cpu_below(fx, burst, 32, n=n)
+    exp, bad_ip, bad_l4 = expected_forwarded(fx["expect"][:n], 3)
+    np.testing.assert_array_equal(fwd, exp)
+    assert (int(st[2]), int(st[3])) == (bad_ip, bad_l4)
+    full, rest = divmod(n, burst)         # one poll burst per `burst` frames
+    gpu = (full if burst >= 32 else 0) + (1 if rest >= 32 else 0)
+    cpu = (full if burst < 32 else 0) + (1 if 0 < rest < 32 else 0)
+    assert (int(st[4]), int(st[5])) == (gpu, cpu)
+
+
+@needs_harness
+@pytest.mark.gpu
+def test_cpu_crossover_off_keeps_every_burst_on_the_gpu():
+    fx = fixture()
+    fwd, st = run_cpu_below(fx, 1, 0, n=300)
+    exp, _, _ = expected_forwarded(fx["expect"][:300], 3)
+    np.testing.assert_array_equal(fwd, exp)
+    assert int(st[4]) == 300 and int(st[5]) == 0
+
+
 # ------------------------------------------------------------ transmit -----
 def tx_run(arena, offs, lens, mss, tx_burst, tso, wire_mtu=1514):
     from tulips_amd import csum  # noqa: F401

@@ -238,6 +238,75 @@ def test_mctx_device_fixed_m8_from_gpu0(oracle):
     assert f"{oracle.fnv1a_u16(out.cpu().numpy().view(np.uint16)):016x}" == bt["fnv1a64"]
 
 
+@pytest.mark.gpu
+def test_mctx_device_staged_copies(oracle):
+    """The staged form (no peer access between two devices, here forced with
+    tulips_csum_mctx_set_peer_mode): pieces go source HBM -> page-locked
+    bounce -> the device's HBM and results back the same way. F1500, F1500-tcp
+    and ZIPF digests over 3 logical devices; then the same context switched
+    back to peer copies (slots reused both ways)."""
+    import torch
+    from tulips_amd import csum
+    from oracle import ip4
+    g = golden()
+    n = 65536
+    arena = torch.empty(n * 1500 + 64, dtype=torch.uint8, device="cuda:0")
+    csum.fill_splitmix(arena, n * 1500)
+    src = _dev(np.full(n, ip4(10, 1, 0, 1), np.uint32))
+    dst = _dev(np.full(n, ip4(10, 1, 0, 2), np.uint32))
+    lens = oracle.zipf_lengths(n)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    ztot = int(lens.astype(np.int64).sum())
+    za = torch.empty(ztot + 64, dtype=torch.uint8, device="cuda:0")
+    csum.fill_splitmix(za, ztot)
+    do, dl = _dev(offs.view(np.int64)), _dev(lens)
+
+    def dig(t):
+        return f"{oracle.fnv1a_u16(t.cpu().numpy().view(np.uint16)):016x}"
+    with csum.MultiContext([0, 0, 0], chunk_bytes=1 << 20) as m:
+        for staged in (True, False, True):
+            m.set_peer_mode(staged)
+            out = m.batch_fixed_device(arena, 1500, 1500, n)
+            torch.cuda.synchronize()
+            assert dig(out) == g["F1500"]["fnv1a64"], staged
+            out = m.batch_fixed_device(arena, 1500, 1500, n, src=src, dst=dst, mode=2)
+            torch.cuda.synchronize()
+            assert dig(out) == g["F1500-tcp"]["fnv1a64"], staged
+            out = m.batch_arena_device(za, do, dl, arena_bytes=ztot)
+            torch.cuda.synchronize()
+            assert dig(out) == g["ZIPF"]["fnv1a64"], staged
+        assert list(m.bounds()) != [0, 0, 0, 0]
+
+
+@pytest.mark.gpu
+def test_mctx_device_every_visible_gpu(oracle):
+    """With more than one GPU visible, the device-resident path over real
+    peers (xGMI peer DMA where hipDeviceCanAccessPeer allows it, staged
+    otherwise): F1500 digest from GPU 0 over every device, both forms."""
+    import torch
+    from tulips_amd import csum
+    nd = torch.cuda.device_count()
+    if nd < 2:
+        pytest.skip("one GPU visible")
+    g = golden()
+    n = 65536
+    arena = torch.empty(n * 1500 + 64, dtype=torch.uint8, device="cuda:0")
+    csum.fill_splitmix(arena, n * 1500)
+    with csum.MultiContext(list(range(nd))) as m:
+        for staged in (False, True):
+            m.set_peer_mode(staged)
+            out = m.batch_fixed_device(arena, 1500, 1500, n)
+            torch.cuda.synchronize()
+            assert f"{oracle.fnv1a_u16(out.cpu().numpy().view(np.uint16)):016x}" == \
+                g["F1500"]["fnv1a64"], staged
+
+
+def test_mctx_peer_mode_arguments_without_gpu():
+    from tulips_amd import csum
+    f = csum.lib.tulips_csum_mctx_set_peer_mode
+    assert f(None, 0) == 1
+
+
 # -- flow-affine validation (tulips_csum_mctx_validate_frames_rss_host) -------
 def _rss_frames(oracle, rng, fx_rss, reps=2):
     """One well-formed TCP frame per rss.npz tuple (addresses and ports set
@@ -303,3 +372,41 @@ def test_mctx_rss_arguments_without_gpu():
     f = csum.lib.tulips_csum_mctx_validate_frames_rss_host
     key = (C.c_uint8 * 40)()
     assert f(None, 1, 1, 1, 1, key, 40, 0, 1, 1, 1, None, None) == 1
+
+
+@pytest.mark.gpu
+def test_mctx_rss_fragments_go_to_slot0(oracle):
+    """IPv4 fragments of a TCP flow (MF set, or a fragment offset) carry no
+    ports a NIC would hash: they go to table[0] like other frames without a
+    4-tuple, never to a device picked by payload bytes; the
+    flow's unfragmented frames stay on one device."""
+    from test_frames import make_frame, pack
+    from tulips_amd import csum
+    rng = np.random.default_rng(31)
+    key = bytes(range(7, 47))
+    frames, kind = [], []
+    for k in range(400):
+        f = bytearray(make_frame(oracle, rng, int(rng.integers(20, 900))))
+        f[26:38] = bytes([10, 0, 0, 1, 10, 0, 0, 2, 0x1f, 0x90, 0x22, 0xb8])
+        r = k % 4
+        if r == 1:
+            f[20] = (f[20] & 0xC0) | 0x20                 # MF: first fragment
+        elif r == 2:
+            f[20], f[21] = 0x00, 0xb9                     # non-first fragment
+            f[34:38] = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+        frames.append(bytes(f))
+        kind.append(r)
+    arena, offs, lens = pack(frames, rng)
+    arena, _ = oracle.generate_frames(arena.copy(), offs, lens)
+    kind = np.array(kind)
+    table = np.array([3, 0, 1, 2] * 32, dtype=np.uint16)
+    with csum.MultiContext([0] * 4, chunk_bytes=1 << 20) as m:
+        flags, dev = m.validate_frames_rss(arena, offs, lens, key, table)
+    np.testing.assert_array_equal(flags, oracle.validate_frames(arena, offs, lens))
+    frag = (kind == 1) | (kind == 2)
+    assert np.all(dev[frag] == table[0])
+    whole = dev[~frag]
+    assert len(set(whole.tolist())) == 1
+    h = csum.toeplitz(int.from_bytes(bytes([10, 0, 0, 1]), "little"),
+                      int.from_bytes(bytes([10, 0, 0, 2]), "little"), 0x1f90, 0x22b8, key)
+    assert whole[0] == table[h % len(table)]

@@ -131,6 +131,69 @@ tulips_csum_tcp_host(uint32_t src, uint32_t dst, uint16_t len,
     inet_post(host_checksum(tcp_seed(src, dst, len), segment, len)));
 }
 
+// Receive validation of host-resident frames on the calling thread: the
+// flags and counters of tulips_csum_validate_frames, computed with the host
+// scalar drop-ins above (ipv4::checksum over bytes 14..33, the tcpv4
+// pseudo-header checksum over the segment), i.e. the reference's per-frame
+// checks (ipv4/Processor.cpp:67-122, tcpv4/Processor.cpp:120-132). Header
+// rules as frame_common.h parse_header.
+int
+tulips_csum_validate_frames_cpu(const uint8_t* base, const uint64_t* offsets,
+                                const uint16_t* lengths, uint32_t n, uint8_t* flags,
+                                uint32_t* counters)
+{
+  if (counters) {
+    memset(counters, 0, 4 * sizeof(uint32_t));
+  }
+  if (n == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths || (!flags && !counters)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  uint32_t cnt[4] = { 0, 0, 0, 0 };
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* f = base + offsets[i];
+    const uint32_t flen = lengths[i];
+    auto byte = [&](uint32_t k) -> uint32_t { return k < flen ? f[k] : 0u; };
+    const uint32_t type = (byte(12) << 8) | byte(13);
+    const uint32_t total = (byte(16) << 8) | byte(17);
+    const bool eth_ip = flen >= 14 && type == 0x0800u;
+    const bool runt = eth_ip && flen < 34;
+    const bool ipv4 = eth_ip && !runt && byte(14) == 0x45u;
+    const bool tcp = ipv4 && (byte(20) & 0x3fu) == 0 && byte(21) == 0 && byte(23) == 6u;
+    const uint32_t tcplen = (total - 20u) & 0xffffu;
+    const bool trunc = tcp && (total < 20u || 34u + tcplen > flen);
+    uint32_t fl = 0;
+    if (runt) {
+      fl = TULIPS_FRAME_TRUNCATED;
+    } else if (ipv4) {
+      const bool ip_ok = tulips_csum_ipv4_host(f + 14) == 0xffffu;
+      bool l4_ok = false;
+      if (tcp && !trunc) {
+        uint32_t src, dst;
+        memcpy(&src, f + 26, 4);
+        memcpy(&dst, f + 30, 4);
+        l4_ok = tulips_csum_tcp_host(src, dst, uint16_t(tcplen), f + 34) == 0xffffu;
+      }
+      fl = TULIPS_FRAME_IPV4 | (ip_ok ? TULIPS_FRAME_IP_CSUM_OK : 0u) |
+           (tcp ? TULIPS_FRAME_TCP : 0u) | (trunc ? TULIPS_FRAME_TRUNCATED : 0u) |
+           (l4_ok ? TULIPS_FRAME_L4_CSUM_OK : 0u);
+      cnt[0] += 1;
+      cnt[1] += ip_ok ? 0u : 1u;
+      cnt[2] += tcp ? 1u : 0u;
+      cnt[3] += (tcp && !l4_ok) ? 1u : 0u;
+    }
+    if (flags) {
+      flags[i] = uint8_t(fl);
+    }
+  }
+  if (counters) {
+    memcpy(counters, cnt, sizeof(cnt));
+  }
+  return TULIPS_STATUS_OK;
+}
+
 } // extern "C"
 
 // ---------------------------------------------------------------------------

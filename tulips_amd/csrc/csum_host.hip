@@ -860,16 +860,23 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
   ZcState& z = ctx->zc;
   ZcMailbox* mb = z.mb;
   const uintptr_t b0 = reinterpret_cast<uintptr_t>(base);
-  if (hi > lo && !z.pin.holds(b0 + lo, b0 + hi)) {
-    z.pin = pinned_range(base + lo);
-    z.pin_dev = 0;
-    void* d = nullptr;
-    if (z.pin.hi > z.pin.lo &&
-        hipHostGetDevicePointer(&d, reinterpret_cast<void*>(z.pin.lo), 0) == hipSuccess) {
-      z.pin_dev = reinterpret_cast<uintptr_t>(d);
-    } else {
-      (void)hipGetLastError();
-      z.pin = PinnedRange();
+  if (hi > lo) {
+    // looked up on every call: the caller may have freed the allocation
+    // cached here and the range been reused by another (pageable or
+    // page-locked) allocation; only an identical [lo, hi) keeps the cached
+    // device address
+    const PinnedRange now_pin = pinned_range(base + lo);
+    if (now_pin.lo != z.pin.lo || now_pin.hi != z.pin.hi || z.pin_dev == 0) {
+      z.pin = now_pin;
+      z.pin_dev = 0;
+      void* d = nullptr;
+      if (z.pin.hi > z.pin.lo &&
+          hipHostGetDevicePointer(&d, reinterpret_cast<void*>(z.pin.lo), 0) == hipSuccess) {
+        z.pin_dev = reinterpret_cast<uintptr_t>(d);
+      } else {
+        (void)hipGetLastError();
+        z.pin = PinnedRange();
+      }
     }
   }
   uint64_t dbase;
@@ -926,6 +933,13 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
     __atomic_store_n(&mb->req[1], zc_word(tag, gbase), __ATOMIC_RELAXED);
     __atomic_store_n(&mb->req[0], zc_word(tag, n), __ATOMIC_RELEASE);
   } else {
+    // done[] of the workgroups about to answer: cleared, so a word left by
+    // a request 65,535 tags ago (a larger burst served by more workgroups)
+    // can never read as this request's completion; every earlier launch has
+    // published all of its words (the host waited for them)
+    for (uint32_t w = 0; w < nwg; ++w) {
+      __atomic_store_n(&mb->done[w], uint64_t(0), __ATOMIC_RELAXED);
+    }
     args.base = gbase;
     args.seq = tag;
     args.n = n;
@@ -1033,6 +1047,16 @@ tulips_csum_ctx_set_lowlat(tulips_csum_ctx* ctx, int resident)
 }
 
 extern "C" int
+tulips_csum_ctx_debug_set_seq(tulips_csum_ctx* ctx, uint64_t seq)
+{
+  if (!ctx) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  ctx->zc.seq = seq;
+  return TULIPS_STATUS_OK;
+}
+
+extern "C" int
 tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,
                                const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
                                uint8_t* flags, uint32_t* counters)
@@ -1068,21 +1092,23 @@ tulips_csum_time_validate(tulips_csum_ctx* ctx, int path, const uint8_t* base,
                           const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
                           uint32_t reps, uint8_t* flags, double* out)
 {
-  if (!ctx || !out || reps == 0 || (path != 0 && path != 1)) {
+  if (!ctx || !out || reps == 0 || path < 0 || path > 2) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   std::vector<double> t(reps), g;
   for (uint32_t r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
     const int rc =
-      path ? tulips_csum_validate_frames_zc(ctx, base, offsets, lengths, n, flags, nullptr)
-           : tulips_csum_validate_frames_host(ctx, base, offsets, lengths, n, flags, nullptr);
+      path == 2   ? tulips_csum_validate_frames_cpu(base, offsets, lengths, n, flags, nullptr)
+      : path == 1 ? tulips_csum_validate_frames_zc(ctx, base, offsets, lengths, n, flags, nullptr)
+                  : tulips_csum_validate_frames_host(ctx, base, offsets, lengths, n, flags,
+                                                     nullptr);
     t[r] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
              .count();
     if (rc != TULIPS_STATUS_OK) {
       return rc;
     }
-    if (path && ctx->zc.mb) {
+    if (path == 1 && ctx->zc.mb) {
       g.push_back(double(ctx->zc.mb->t_done - ctx->zc.mb->t_req) / 100.0); // 100 MHz
     }
   }

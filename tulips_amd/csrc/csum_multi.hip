@@ -137,6 +137,22 @@ struct DevSlot
   uint64_t meta_bytes = 0;
   uint16_t* out = nullptr;      // its results before they go home
   uint64_t out_n = 0;
+  // Staged form (no peer access to the source, or forced): pieces travel
+  // source HBM -> page-locked bounce buffer -> this device's HBM, results
+  // back the same way. `stage` is a stream on the source device; its events
+  // are made there too.
+  int stage_dev = -1;
+  hipStream_t stage = nullptr;
+  uint8_t* hb[2] = { nullptr, nullptr }; // double-buffered bounce (page-locked)
+  uint64_t hb_bytes = 0;
+  uint16_t* hres = nullptr;              // results bounce (page-locked)
+  uint64_t hres_bytes = 0;
+  hipEvent_t staged[2] = { nullptr, nullptr }; // bounce j filled (source device)
+  hipEvent_t bfree[2] = { nullptr, nullptr };  // bounce j drained (this device)
+  bool bfree_used[2] = { false, false };
+  hipEvent_t rdone = nullptr;  // results in hres (this device)
+  hipEvent_t sdone = nullptr;  // results home (source device): the call's end
+  bool sdone_used = false;
 };
 
 } // namespace
@@ -152,6 +168,7 @@ struct tulips_csum_mctx
   uint64_t* plan_dev = nullptr;  // on the last source device
   int plan_device = -1;
   uint32_t plan_cap = 0;
+  int peer_mode = 0;             // tulips_csum_mctx_set_peer_mode
 };
 
 extern "C" {
@@ -246,9 +263,30 @@ tulips_csum_mctx_destroy(tulips_csum_mctx* m)
     if (d.done) {
       (void)hipEventDestroy(d.done);
     }
+    if (d.rdone) {
+      (void)hipEventDestroy(d.rdone);
+    }
     (void)hipFree(d.buf);
     (void)hipFree(d.meta);
     (void)hipFree(d.out);
+    for (int j = 0; j < 2; ++j) {
+      if (d.bfree[j]) {
+        (void)hipEventDestroy(d.bfree[j]);
+      }
+    }
+    if (d.stage) {
+      (void)hipSetDevice(d.stage_dev);
+      (void)hipStreamSynchronize(d.stage);
+      (void)hipStreamDestroy(d.stage);
+      for (int j = 0; j < 2; ++j) {
+        (void)hipEventDestroy(d.staged[j]);
+      }
+      (void)hipEventDestroy(d.sdone);
+    }
+    for (int j = 0; j < 2; ++j) {
+      (void)hipHostFree(d.hb[j]);
+    }
+    (void)hipHostFree(d.hres);
   }
   if (m->plan_dev) {
     (void)hipSetDevice(m->plan_device);
@@ -259,6 +297,16 @@ tulips_csum_mctx_destroy(tulips_csum_mctx* m)
   }
   (void)hipSetDevice(prev);
   delete m;
+  return TULIPS_STATUS_OK;
+}
+
+int
+tulips_csum_mctx_set_peer_mode(tulips_csum_mctx* m, int mode)
+{
+  if (!m || mode < 0 || mode > 1) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  m->peer_mode = mode;
   return TULIPS_STATUS_OK;
 }
 
@@ -398,7 +446,11 @@ tulips_csum_mctx_validate_frames_rss_host(tulips_csum_mctx* m, const uint8_t* ba
   tup_i.reserve(n);
   for (uint32_t i = 0; i < n; ++i) {
     const uint8_t* f = base + offsets[i];
-    if (lengths[i] >= 38 && f[12] == 0x08 && f[13] == 0x00 && f[14] == 0x45 && f[23] == 6) {
+    // non-first fragments carry payload where the ports would be, and a
+    // first fragment's flow must land with the rest: fragments (MF set or a
+    // fragment offset, bytes 20..21) go to table[0] like non-TCP frames
+    if (lengths[i] >= 38 && f[12] == 0x08 && f[13] == 0x00 && f[14] == 0x45 && f[23] == 6 &&
+        (f[20] & 0x3f) == 0 && f[21] == 0) {
       uint32_t s4, d4;
       memcpy(&s4, f + 26, 4);
       memcpy(&d4, f + 30, 4);
@@ -661,6 +713,95 @@ run_piece(const Job& J, const Piece& pc, const uint8_t* local, const uint64_t* o
   return tulips_amd::launch_span(local, pc.hi - pc.lo, offs, lens, a, st);
 }
 
+// Staged-form resources of slot `d` for a call whose source is `src`: a
+// stream and events on the source device, bounce buffers of at least
+// `piece_bytes` and a results bounce of `res_bytes`. Made or grown with the
+// slot's streams idle.
+hipError_t
+ensure_staging(DevSlot& d, int src, uint64_t piece_bytes, uint64_t res_bytes)
+{
+  if (d.stage && d.stage_dev != src) {
+    TCS_TRY(hipSetDevice(d.stage_dev));
+    TCS_TRY(hipStreamSynchronize(d.stage));
+    (void)hipStreamDestroy(d.stage);
+    for (int j = 0; j < 2; ++j) {
+      (void)hipEventDestroy(d.staged[j]);
+      d.staged[j] = nullptr;
+    }
+    (void)hipEventDestroy(d.sdone);
+    d.sdone = nullptr;
+    d.sdone_used = false;
+    d.stage = nullptr;
+  }
+  if (!d.stage) {
+    TCS_TRY(hipSetDevice(src));
+    TCS_TRY(hipStreamCreateWithFlags(&d.stage, hipStreamNonBlocking));
+    d.stage_dev = src;
+    for (int j = 0; j < 2; ++j) {
+      TCS_TRY(hipEventCreateWithFlags(&d.staged[j], hipEventDisableTiming));
+    }
+    TCS_TRY(hipEventCreateWithFlags(&d.sdone, hipEventDisableTiming));
+  }
+  TCS_TRY(hipSetDevice(d.device));
+  if (!d.rdone) {
+    TCS_TRY(hipEventCreateWithFlags(&d.rdone, hipEventDisableTiming));
+  }
+  for (int j = 0; j < 2; ++j) {
+    if (!d.bfree[j]) {
+      TCS_TRY(hipEventCreateWithFlags(&d.bfree[j], hipEventDisableTiming));
+    }
+  }
+  if (piece_bytes > d.hb_bytes || res_bytes > d.hres_bytes) {
+    TCS_TRY(hipStreamSynchronize(d.copy));
+    TCS_TRY(hipStreamSynchronize(d.comp));
+    TCS_TRY(hipSetDevice(d.stage_dev));
+    TCS_TRY(hipStreamSynchronize(d.stage));
+    TCS_TRY(hipSetDevice(d.device));
+  }
+  if (piece_bytes > d.hb_bytes) {
+    for (int j = 0; j < 2; ++j) {
+      (void)hipHostFree(d.hb[j]);
+      d.hb[j] = nullptr;
+    }
+    d.hb_bytes = 0;
+    for (int j = 0; j < 2; ++j) {
+      void* p = nullptr;
+      TCS_TRY(hipHostMalloc(&p, piece_bytes, 0));
+      d.hb[j] = static_cast<uint8_t*>(p);
+    }
+    d.hb_bytes = piece_bytes;
+    d.bfree_used[0] = d.bfree_used[1] = false;
+  }
+  if (res_bytes > d.hres_bytes) {
+    (void)hipHostFree(d.hres);
+    d.hres = nullptr;
+    d.hres_bytes = 0;
+    void* p = nullptr;
+    TCS_TRY(hipHostMalloc(&p, res_bytes, 0));
+    d.hres = static_cast<uint16_t*>(p);
+    d.hres_bytes = res_bytes;
+  }
+  return hipSuccess;
+}
+
+// Whether slot `d` reaches source device `src` by peer DMA (xGMI).
+bool
+peer_reachable(const tulips_csum_mctx* m, const DevSlot& d, int src)
+{
+  if (m->peer_mode == 1) {
+    return false;
+  }
+  if (d.device == src) {
+    return true; // a device listed again: a local copy
+  }
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, d.device, src) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return can != 0;
+}
+
 hipError_t
 spread_device(tulips_csum_mctx* m, const Job& J, const std::vector<Piece>& pieces,
               uint32_t per_dev, hipStream_t caller)
@@ -680,6 +821,10 @@ spread_device(tulips_csum_mctx* m, const Job& J, const std::vector<Piece>& piece
     }
   }
   const bool mtcp = (J.mode & 0xffu) == 2u;
+  // per slot, the event that ends this call's work there (the caller's
+  // stream waits for it), and the slots this call queued work on
+  std::vector<hipEvent_t> fin(nd, nullptr);
+  std::vector<char> touched(nd, 0);
   for (size_t k = 0; k < nd && e == hipSuccess; ++k) {
     DevSlot& d = m->slots[k];
     const size_t p0 = k * per_dev, p1 = std::min(pieces.size(), p0 + per_dev);
@@ -697,6 +842,7 @@ spread_device(tulips_csum_mctx* m, const Job& J, const std::vector<Piece>& piece
           (e = hipStreamWaitEvent(d.comp, start, 0)) != hipSuccess) {
         break;
       }
+      touched[k] = 1;
       for (size_t p = p0; p < p1 && e == hipSuccess; ++p) {
         const Piece& pc = pieces[p];
         if (pc.i1 > pc.i0) {
@@ -710,6 +856,7 @@ spread_device(tulips_csum_mctx* m, const Job& J, const std::vector<Piece>& piece
       if (e == hipSuccess) {
         e = hipEventRecord(d.done, d.comp);
         d.used = true;
+        fin[k] = d.done;
       }
       continue;
     }
@@ -736,14 +883,41 @@ spread_device(tulips_csum_mctx* m, const Job& J, const std::vector<Piece>& piece
       break;
     }
     d.out_n = out_have / 2;
+    // staged: per piece, its bytes and its metadata back to back in a bounce
+    const bool staged = !peer_reachable(m, d, J.src_dev);
+    auto meta_per_seg = [&]() {
+      return (J.arena ? 10u : 0u) + (seeded ? 2u : 0u) + (mtcp ? 8u : 0u);
+    };
+    if (staged) {
+      uint64_t most = 0;
+      for (size_t p = p0; p < p1; ++p) {
+        const Piece& pc = pieces[p];
+        const uint64_t a0 = pc.lo & ~uint64_t(15);
+        most = std::max<uint64_t>(most, ((pc.hi - a0 + 15) & ~uint64_t(15)) +
+                                          (pc.i1 - pc.i0) * meta_per_seg() + 5 * 16);
+      }
+      if ((e = ensure_staging(d, J.src_dev, most, 2 * nseg + 16)) != hipSuccess) {
+        break;
+      }
+    }
     if ((e = hipSetDevice(d.device)) != hipSuccess) {
       break;
     }
+    touched[k] = 1;
     // after the caller's earlier work, and after this slot's previous call
-    // stopped reading its buffers
+    // stopped reading its buffers (and, staged, sent its results home)
     if ((e = hipStreamWaitEvent(d.copy, start, 0)) != hipSuccess ||
-        (d.used && (e = hipStreamWaitEvent(d.copy, d.done, 0)) != hipSuccess)) {
+        (d.used && (e = hipStreamWaitEvent(d.copy, d.done, 0)) != hipSuccess) ||
+        (d.sdone_used && (e = hipStreamWaitEvent(d.copy, d.sdone, 0)) != hipSuccess)) {
       break;
+    }
+    if (staged) {
+      // the stage stream (source device) starts after the caller's work too
+      if ((e = hipSetDevice(J.src_dev)) != hipSuccess ||
+          (e = hipStreamWaitEvent(d.stage, start, 0)) != hipSuccess ||
+          (e = hipSetDevice(d.device)) != hipSuccess) {
+        break;
+      }
     }
     const uint64_t* moffs = reinterpret_cast<const uint64_t*>(d.meta + m_off);
     const uint16_t* mlens = reinterpret_cast<const uint16_t*>(d.meta + m_len);
@@ -757,24 +931,66 @@ spread_device(tulips_csum_mctx* m, const Job& J, const std::vector<Piece>& piece
       }
       const uint64_t c = pc.i1 - pc.i0, r = pc.i0 - s0;
       const uint64_t a0 = pc.lo & ~uint64_t(15);
-      auto pull = [&](const void* from, uint8_t* to, uint64_t bytes) {
-        return bytes ? hipMemcpyPeerAsync(to, d.device, from, J.src_dev, bytes, d.copy)
-                     : hipSuccess;
+      // (from, to, bytes) of this piece's transfers: bytes, then metadata
+      struct Xfer
+      {
+        const void* from;
+        uint8_t* to;
+        uint64_t bytes;
       };
-      e = pull(J.base + a0, d.buf + (a0 - A), pc.hi - a0);
-      if (e == hipSuccess && J.arena) {
-        e = pull(J.offsets + pc.i0, d.meta + m_off + 8 * r, 8 * c);
-        if (e == hipSuccess) {
-          e = pull(J.lengths + pc.i0, d.meta + m_len + 2 * r, 2 * c);
+      Xfer xs[6];
+      int nx = 0;
+      xs[nx++] = { J.base + a0, d.buf + (a0 - A), pc.hi - a0 };
+      if (J.arena) {
+        xs[nx++] = { J.offsets + pc.i0, d.meta + m_off + 8 * r, 8 * c };
+        xs[nx++] = { J.lengths + pc.i0, d.meta + m_len + 2 * r, 2 * c };
+      }
+      if (seeded) {
+        xs[nx++] = { J.seeds + pc.i0, d.meta + m_seed + 2 * r, 2 * c };
+      }
+      if (mtcp) {
+        xs[nx++] = { J.src + pc.i0, d.meta + m_src + 4 * r, 4 * c };
+        xs[nx++] = { J.dst + pc.i0, d.meta + m_dst + 4 * r, 4 * c };
+      }
+      if (!staged) {
+        for (int x = 0; x < nx && e == hipSuccess; ++x) {
+          if (xs[x].bytes) {
+            e = hipMemcpyPeerAsync(xs[x].to, d.device, xs[x].from, J.src_dev, xs[x].bytes,
+                                   d.copy);
+          }
         }
-      }
-      if (e == hipSuccess && seeded) {
-        e = pull(J.seeds + pc.i0, d.meta + m_seed + 2 * r, 2 * c);
-      }
-      if (e == hipSuccess && mtcp) {
-        e = pull(J.src + pc.i0, d.meta + m_src + 4 * r, 4 * c);
-        if (e == hipSuccess) {
-          e = pull(J.dst + pc.i0, d.meta + m_dst + 4 * r, 4 * c);
+      } else {
+        // source HBM -> bounce j on the stage stream (after the bounce's
+        // previous contents reached this device), bounce j -> HBM here
+        const int j = int((p - p0) & 1);
+        uint64_t at[6], pos = 0;
+        for (int x = 0; x < nx; ++x) {
+          at[x] = pos;
+          pos += (xs[x].bytes + 15) & ~uint64_t(15);
+        }
+        if ((e = hipSetDevice(J.src_dev)) != hipSuccess ||
+            (d.bfree_used[j] && (e = hipStreamWaitEvent(d.stage, d.bfree[j], 0)) != hipSuccess)) {
+          break;
+        }
+        for (int x = 0; x < nx && e == hipSuccess; ++x) {
+          if (xs[x].bytes) {
+            e = hipMemcpyAsync(d.hb[j] + at[x], xs[x].from, xs[x].bytes, hipMemcpyDeviceToHost,
+                               d.stage);
+          }
+        }
+        if (e != hipSuccess || (e = hipEventRecord(d.staged[j], d.stage)) != hipSuccess ||
+            (e = hipSetDevice(d.device)) != hipSuccess ||
+            (e = hipStreamWaitEvent(d.copy, d.staged[j], 0)) != hipSuccess) {
+          break;
+        }
+        for (int x = 0; x < nx && e == hipSuccess; ++x) {
+          if (xs[x].bytes) {
+            e = hipMemcpyAsync(xs[x].to, d.hb[j] + at[x], xs[x].bytes, hipMemcpyHostToDevice,
+                               d.copy);
+          }
+        }
+        if (e == hipSuccess && (e = hipEventRecord(d.bfree[j], d.copy)) == hipSuccess) {
+          d.bfree_used[j] = true;
         }
       }
       hipEvent_t ev = d.ev[p - p0];
@@ -785,24 +1001,59 @@ spread_device(tulips_csum_mctx* m, const Job& J, const std::vector<Piece>& piece
                       mtcp ? msrc + r : nullptr, mtcp ? mdst + r : nullptr, d.out + r,
                       d.comp);
       }
-      if (e == hipSuccess) {
+      if (e == hipSuccess && !staged) {
         e = hipMemcpyPeerAsync(J.out + pc.i0, J.src_dev, d.out + r, d.device, 2 * c, d.comp);
       }
     }
     if (e == hipSuccess) {
       e = hipEventRecord(d.done, d.comp);
       d.used = true;
+      fin[k] = d.done;
+    }
+    if (e == hipSuccess && staged) {
+      // all of this device's results in one bounce, then home
+      if ((e = hipMemcpyAsync(d.hres, d.out, 2 * nseg, hipMemcpyDeviceToHost, d.comp)) ==
+            hipSuccess &&
+          (e = hipEventRecord(d.rdone, d.comp)) == hipSuccess &&
+          (e = hipSetDevice(J.src_dev)) == hipSuccess &&
+          (e = hipStreamWaitEvent(d.stage, d.rdone, 0)) == hipSuccess &&
+          (e = hipMemcpyAsync(J.out + s0, d.hres, 2 * nseg, hipMemcpyHostToDevice, d.stage)) ==
+            hipSuccess &&
+          (e = hipEventRecord(d.sdone, d.stage)) == hipSuccess) {
+        d.sdone_used = true;
+        fin[k] = d.sdone;
+      }
     }
   }
   m->bounds[nd] = pieces.empty() ? 0u : uint32_t(pieces.back().i1);
   // the caller's stream continues once every device's results are home
   if (e == hipSuccess && (e = hipSetDevice(J.src_dev)) == hipSuccess) {
     for (size_t k = 0; k < nd && e == hipSuccess; ++k) {
-      if (m->slots[k].used) {
-        e = hipStreamWaitEvent(caller, m->slots[k].done, 0);
+      if (fin[k]) {
+        e = hipStreamWaitEvent(caller, fin[k], 0);
       }
     }
   }
+  if (e != hipSuccess) {
+    // a failure part-way: the work already queued may still write the
+    // caller's `out`; it is drained before the error is reported, so the
+    // caller may free or reuse its buffers at once
+    for (size_t k = 0; k < nd; ++k) {
+      DevSlot& d = m->slots[k];
+      if (!touched[k]) {
+        continue;
+      }
+      (void)hipSetDevice(d.device);
+      (void)hipStreamSynchronize(d.copy);
+      (void)hipStreamSynchronize(d.comp);
+      if (d.stage) {
+        (void)hipSetDevice(d.stage_dev);
+        (void)hipStreamSynchronize(d.stage);
+      }
+    }
+    (void)hipGetLastError();
+  }
+  (void)hipSetDevice(J.src_dev);
   (void)hipEventDestroy(start);
   return e;
 }

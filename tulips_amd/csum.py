@@ -170,6 +170,9 @@ _SIGNATURES = {
                                             C.c_uint32, _vp, _vp]),
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
+    "tulips_csum_validate_frames_cpu": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp]),
+    "tulips_csum_ctx_debug_set_seq": (C.c_int, [_vp, C.c_uint64]),
+    "tulips_csum_mctx_set_peer_mode": (C.c_int, [_vp, C.c_int]),
 }
 
 # include/tulips_csum.h TULIPS_FRAME_* (per-frame validation flags)
@@ -500,6 +503,11 @@ class HostContext:
                "tulips_csum_validate_frames_host")
         return (flags, cnt) if with_counters else flags
 
+    def debug_set_seq(self, seq: int):
+        """Test hook: the last zero-copy request's sequence number
+        (tulips_csum_ctx_debug_set_seq), to reach tag wrap-around."""
+        _check(lib.tulips_csum_ctx_debug_set_seq(self._h, seq), "tulips_csum_ctx_debug_set_seq")
+
     def set_lowlat(self, resident: bool):
         """Low-latency path form: one launch per burst (False) or a resident
         server (True), tulips_csum_ctx_set_lowlat."""
@@ -577,6 +585,13 @@ class MultiContext(HostContext):
         if self._h:
             lib.tulips_csum_mctx_destroy(self._h)
             self._h = None
+
+    def set_peer_mode(self, staged: bool):
+        """Device-resident calls: move pieces by peer DMA where the devices
+        allow it (False, the default) or always through page-locked host
+        bounce buffers (True), tulips_csum_mctx_set_peer_mode."""
+        _check(lib.tulips_csum_mctx_set_peer_mode(self._h, 1 if staged else 0),
+               "tulips_csum_mctx_set_peer_mode")
 
     def bounds(self):
         import numpy as np
@@ -727,6 +742,25 @@ def validate_frames(arena, offsets, lengths, *, flags=None, counters=None,
                                            _stream(stream)),
            "tulips_csum_validate_frames")
     return flags
+
+
+def validate_frames_cpu(arena, offsets, lengths, *, with_counters: bool = False):
+    """Host-resident frames validated on this thread by the library's host
+    code (tulips_csum_validate_frames_cpu; no GPU): the same FRAME_* flags
+    (and counters) as validate_frames."""
+    import numpy as np
+    ar = _host(arena, np.uint8)
+    off = _host(offsets, np.uint64)
+    ln = _host(lengths, np.uint16)
+    n = len(off.keep)
+    if len(ln.keep) != n:
+        raise ValueError("offsets/lengths size mismatch")
+    flags = np.empty(max(n, 1), dtype=np.uint8)
+    cnt = np.zeros(4, dtype=np.uint32)
+    _check(lib.tulips_csum_validate_frames_cpu(ar.ptr, off.ptr, ln.ptr, n, flags.ctypes.data,
+                                               cnt.ctypes.data),
+           "tulips_csum_validate_frames_cpu")
+    return (flags[:n], cnt) if with_counters else flags[:n]
 
 
 def generate_frames(arena, offsets, lengths, *, flags=None, want_flags: bool = True,
