@@ -10,10 +10,11 @@ LIB = tulips_amd/libtulips_csum.so
 SRCS = tulips_amd/csrc/csum_kernels.hip tulips_amd/csrc/csum_capi.hip \
        tulips_amd/csrc/csum_host.hip tulips_amd/csrc/rss_toeplitz.hip \
        tulips_amd/csrc/frames.hip tulips_amd/csrc/segment.hip \
-       tulips_amd/csrc/stream_state.hip tulips_amd/csrc/csum_multi.hip
+       tulips_amd/csrc/stream_state.hip tulips_amd/csrc/csum_multi.hip \
+       tulips_amd/csrc/rss_route.hip
 HDRS = tulips_amd/csrc/csum_common.h tulips_amd/csrc/csum_launch.h \
        tulips_amd/csrc/csum_device.h tulips_amd/csrc/zc_mailbox.h \
-       tulips_amd/csrc/span_kernel.h \
+       tulips_amd/csrc/span_kernel.h tulips_amd/csrc/rss_common.h tulips_amd/csrc/rss_route.h \
        tulips_amd/csrc/frame_common.h tulips_amd/csrc/stream_state.h \
        include/tulips_csum.h include/tulips_csum_util.h
 OBJS = $(patsubst tulips_amd/csrc/%.hip,build/%.o,$(SRCS))

@@ -249,6 +249,31 @@ int tulips_csum_mctx_validate_frames_rss_host(tulips_csum_mctx* ctx, const uint8
                                               uint32_t init, const uint16_t* table,
                                               uint32_t table_len, uint8_t* flags,
                                               uint32_t* counters, uint16_t* device_of);
+/*
+ * The same for frames resident in the HBM of `stream`'s device (the source):
+ * base/offsets/lengths/flags/counters (uint32[4], zeroed then summed) and
+ * device_of (uint16[n], may be NULL) are device pointers on the source; key
+ * and table stay host arrays (table_len <= 65536). On the source, one pass
+ * hashes every frame's tuple (the flags rule above: option-less,
+ * unfragmented IPv4/TCP, else table[0]) and orders the frames by device,
+ * arrival order kept; the frames bound for each other device are gathered
+ * into one packed run that device pulls over xGMI (hipMemcpyPeerAsync; the
+ * HIP runtime stages it through host memory where the two devices have no
+ * peer path). Each device validates its frames (the source's own in place)
+ * and sends the flags home, where they are written in arrival order.
+ * Ordered after the work queued on `stream`, which waits for all of it;
+ * blocks once for the per-device frame counts (one small D2H). Not
+ * capturable. tulips_csum_mctx_shard_bounds then reports the prefix sums of
+ * the per-device frame counts.
+ */
+int tulips_csum_mctx_validate_frames_rss_device(tulips_csum_mctx* ctx, const uint8_t* base,
+                                                const uint64_t* offsets,
+                                                const uint16_t* lengths, uint32_t n,
+                                                const uint8_t* key, size_t key_len,
+                                                uint32_t init, const uint16_t* table,
+                                                uint32_t table_len, uint8_t* flags,
+                                                uint32_t* counters, uint16_t* device_of,
+                                                void* stream);
 /* The shard bounds (ndevices + 1 entries) of the context's last call. */
 int tulips_csum_mctx_shard_bounds(const tulips_csum_mctx* ctx, uint32_t* bounds);
 

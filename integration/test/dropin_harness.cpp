@@ -158,6 +158,7 @@ struct Options
   uint32_t corrupt = 5;
   uint32_t tso = 0;    // client decorator: TSO send buffers of this size
   uint32_t max = 1400; // largest message
+  int64_t cpu_below = -1; // decorator Config::cpu_below (-1: its default)
 };
 
 std::string
@@ -183,6 +184,9 @@ wrap(system::Logger& log, transport::Device::Ref dev, Options const& o,
     cfg.burst = o.burst;
     cfg.tx = o.tx;
     cfg.tso = tso;
+    if (o.cpu_below >= 0) {
+      cfg.cpu_below = uint32_t(o.cpu_below);
+    }
     return transport::gpucsum::Device::allocate(log, std::move(dev), cfg);
   }
 #endif
@@ -202,7 +206,8 @@ decorator_stats(transport::Device& dev)
     std::ostringstream os;
     os << "{\"frames\":" << s.frames << ",\"forwarded\":" << s.forwarded
        << ",\"bad_ip\":" << s.bad_ip << ",\"bad_l4\":" << s.bad_l4
-       << ",\"batches\":" << s.batches << ",\"tx_frames\":" << s.tx_frames
+       << ",\"batches\":" << s.batches << ",\"cpu_batches\":" << s.cpu_batches
+       << ",\"tx_frames\":" << s.tx_frames
        << ",\"tx_segments\":" << s.tx_segments << ",\"tx_batches\":" << s.tx_batches
        << "}";
     return os.str();
@@ -330,6 +335,10 @@ main(int argc, char** argv)
       num(o.tso);
     } else if (a == "--max") {
       num(o.max);
+    } else if (a == "--cpu-below") {
+      uint32_t v = 0;
+      num(v);
+      o.cpu_below = v;
     }
   }
 #ifndef DROPIN_GPUCSUM

@@ -128,20 +128,27 @@ def test_default_gates_clean_exchange():
 
 @pytest.mark.gpu
 @needs_build
-@pytest.mark.parametrize("burst", [1, 64])
-def test_nocheck_gates_with_gpu_validation(burst):
+@pytest.mark.parametrize("burst,cpu_below", [(1, 0), (64, 0), (64, None)])
+def test_nocheck_gates_with_gpu_validation(burst, cpu_below):
     """TULIPS_DISABLE_CHECKSUM_CHECK: the stack checks nothing and hints
     VALIDATE_IP_CSUM / VALIDATE_L4_CSUM (src/api/Client.cpp:39-41); the gpucsum
-    decorator validates every received frame on the GPU and drops the 5
-    corrupted ones (bad_l4), which the client then retransmits."""
-    rc, r = run("nocheck", "--gpucsum", "--burst", str(burst))
+    decorator validates every received frame and drops the 5 corrupted ones
+    (bad_l4), which the client then retransmits. cpu_below 0: every poll
+    burst on the GPU; default (32): the exchange's bursts of a frame or two
+    are validated on the polling thread by the library's host code."""
+    extra = [] if cpu_below is None else ["--cpu-below", str(cpu_below)]
+    rc, r = run("nocheck", "--gpucsum", "--burst", str(burst), *extra)
     assert rc == 0, r
     check_exchange(r)
     assert not r["stack_checks"] and r["stack_generates"]
     assert r["srv_tcp"]["chkerr"] == 0
     sd = r["server_decorator"]
     assert sd["bad_l4"] == 5 and sd["bad_ip"] == 0, sd
-    assert sd["forwarded"] == sd["frames"] - 5 and sd["batches"] > 0, sd
+    assert sd["forwarded"] == sd["frames"] - 5, sd
+    if cpu_below == 0:
+        assert sd["batches"] > 0 and sd["cpu_batches"] == 0, sd
+    else:
+        assert sd["batches"] + sd["cpu_batches"] > 0, sd
     assert r["client_decorator"]["bad_l4"] == 0
 
 

@@ -410,3 +410,92 @@ def test_mctx_rss_fragments_go_to_slot0(oracle):
     h = csum.toeplitz(int.from_bytes(bytes([10, 0, 0, 1]), "little"),
                       int.from_bytes(bytes([10, 0, 0, 2]), "little"), 0x1f90, 0x22b8, key)
     assert whole[0] == table[h % len(table)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_i,init,ndev,lead", [(0, 0, 4, 0), (9, 0xFFFFFFFF, 3, 5),
+                                                  (7, 0, 2, 3), (3, 7, 5, 1)])
+def test_mctx_rss_device_matches_host_and_reference(oracle, key_i, init, ndev, lead):
+    """tulips_csum_mctx_validate_frames_rss_device: frames resident on GPU 0
+    (odd arena bases), hashed and ordered on the device, each device's run
+    pulled and validated there: device_of equals table[reference hash %
+    len] (tests/golden/rss.npz), equals the host form's, flags equal one
+    device's, counters equal the flags', bounds count frames per device."""
+    import torch
+    from test_frames import counters_of
+    from test_rss import rss_fixture
+    from tulips_amd import csum
+    fx = rss_fixture()
+    key = fx[f"key_{key_i}"].tobytes()
+    exp_hash = fx[f"expect_{key_i}_{'init0' if init == 0 else 'initff'}"] if init in (
+        0, 0xFFFFFFFF) else None
+    rng = np.random.default_rng(key_i * 11 + ndev)
+    arena, offs, lens, flow = _rss_frames(oracle, rng, fx)
+    table = (np.arange(128) * 5 % ndev).astype(np.uint16)
+    table[0] = ndev - 1
+    exp_flags = oracle.validate_frames(arena, offs, lens)
+    buf = torch.zeros(len(arena) + lead, dtype=torch.uint8, device="cuda:0")
+    buf[lead:] = torch.from_numpy(arena).to("cuda:0")
+    cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
+    with csum.MultiContext([0] * ndev, chunk_bytes=1 << 20) as m:
+        hflags, hdev = m.validate_frames_rss(arena, offs, lens, key, table, init=init)
+        for rep in range(2):
+            fl, dv = m.validate_frames_rss_device(
+                buf[lead:], _dev(offs.view(np.int64)), _dev(lens.view(np.int16)), key, table,
+                init=init, counters=cnt)
+            torch.cuda.synchronize()
+            dv = dv.cpu().numpy().view(np.uint16)
+            np.testing.assert_array_equal(fl.cpu().numpy(), exp_flags)
+            np.testing.assert_array_equal(dv, hdev)
+            np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),
+                                          counters_of(exp_flags))
+            b = m.bounds()
+            assert list(np.diff(b.astype(np.int64))) == [int((dv == k).sum())
+                                                         for k in range(ndev)]
+    np.testing.assert_array_equal(hflags, exp_flags)
+    if exp_hash is not None:
+        tcp = flow >= 0
+        np.testing.assert_array_equal(dv[tcp],
+                                      table[exp_hash[flow[tcp]].astype(np.int64) % len(table)])
+
+
+@pytest.mark.gpu
+def test_mctx_rss_device_fixture_mutations_and_scale(oracle):
+    """The reference-flagged frames.npz (mutated: bad checksums, fragments,
+    runts, truncation, zero-length frames) routed over 3 devices, and a
+    200,000-frame batch (several scan chunks of block histograms, frames up
+    to 9 KB) over 8: flags equal the oracle's in arrival order."""
+    import torch
+    from test_frames import frames_fixture, make_frame, mutate, pack
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(606)
+    arena = mutate(fx, rng, 1500)
+    exp = oracle.validate_frames(arena, fx["offsets"], fx["lengths"])
+    key = bytes(range(40))
+    with csum.MultiContext([0, 0, 0]) as m:
+        fl, _ = m.validate_frames_rss_device(_dev(arena), _dev(fx["offsets"].view(np.int64)),
+                                             _dev(fx["lengths"].view(np.int16)), key,
+                                             [0, 1, 2, 2, 1])
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(fl.cpu().numpy(), exp)
+    base = [make_frame(oracle, rng, int(p)) for p in rng.integers(0, 9000, 64)]
+    idx = rng.integers(0, 64, 200000)
+    frames = [base[i] for i in idx]
+    arena, offs, lens = pack(frames, rng, gap=4)
+    exp = oracle.validate_frames(arena, offs, lens)
+    with csum.MultiContext(list(range(8)) if torch.cuda.device_count() >= 8 else [0] * 8) as m:
+        fl, dv = m.validate_frames_rss_device(_dev(arena), _dev(offs.view(np.int64)),
+                                              _dev(lens.view(np.int16)), key,
+                                              np.arange(8, dtype=np.uint16))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(fl.cpu().numpy(), exp)
+        assert len(np.unique(dv.cpu().numpy())) > 1
+
+
+def test_mctx_rss_device_arguments_without_gpu():
+    from tulips_amd import csum
+    f = csum.lib.tulips_csum_mctx_validate_frames_rss_device
+    key = (C.c_uint8 * 40)()
+    tab = (C.c_uint16 * 4)()
+    assert f(None, 1, 1, 1, 1, key, 40, 0, tab, 4, 1, None, None, None) == 1

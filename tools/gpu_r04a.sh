@@ -18,4 +18,4 @@ run new 600 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeou
 run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 run bench 600 python -u bench.py
 cp $O/bench.log $O/bench.json
-run suite 1100 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu tests
+run suite 600 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu tests

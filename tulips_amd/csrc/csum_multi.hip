@@ -34,10 +34,12 @@
 #include <mutex>
 #include <new>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/tulips_csum.h"
 #include "csum_launch.h"
+#include "rss_route.h"
 
 namespace tulips_amd {
 int pack_threads();
@@ -157,6 +159,29 @@ struct DevSlot
 
 } // namespace
 
+namespace {
+
+// Device workspace of the flow router (validate_frames_rss_device), on the
+// last source device; grown on demand.
+struct RouteWs
+{
+  int device = -1;
+  uint64_t n_cap = 0, cell_cap = 0, tab_cap = 0, packed_cap = 0;
+  uint16_t* dev_of = nullptr;     // n (when the caller passes no device_of)
+  uint32_t* perm = nullptr;       // n
+  uint64_t* poff = nullptr;       // n
+  uint16_t* plen = nullptr;       // n
+  uint8_t* rflags = nullptr;      // n, routed order
+  uint32_t* cells = nullptr;      // 3 x blocks x devices (counts, bytes, bases)
+  uint64_t* base_bytes = nullptr; // blocks x devices
+  uint64_t* totals = nullptr;     // 2 x tulips_amd::RT_MAX_DEV
+  uint64_t* totals_host = nullptr; // page-locked copy
+  uint16_t* table = nullptr;
+  uint8_t* packed = nullptr;      // frames bound for other devices, by device
+};
+
+} // namespace
+
 struct tulips_csum_mctx
 {
   std::vector<int> devices;
@@ -169,6 +194,7 @@ struct tulips_csum_mctx
   int plan_device = -1;
   uint32_t plan_cap = 0;
   int peer_mode = 0;             // tulips_csum_mctx_set_peer_mode
+  RouteWs route;                 // validate_frames_rss_device
 };
 
 extern "C" {
@@ -295,6 +321,17 @@ tulips_csum_mctx_destroy(tulips_csum_mctx* m)
   if (m->plan_host) {
     (void)hipHostFree(m->plan_host);
   }
+  RouteWs& r = m->route;
+  if (r.device >= 0) {
+    (void)hipSetDevice(r.device);
+    (void)hipDeviceSynchronize();
+    for (void* p : { (void*)r.dev_of, (void*)r.perm, (void*)r.poff, (void*)r.plen,
+                     (void*)r.rflags, (void*)r.cells, (void*)r.base_bytes, (void*)r.totals,
+                     (void*)r.table, (void*)r.packed }) {
+      (void)hipFree(p);
+    }
+  }
+  (void)hipHostFree(r.totals_host);
   (void)hipSetDevice(prev);
   delete m;
   return TULIPS_STATUS_OK;
@@ -1224,3 +1261,273 @@ tulips_csum_mctx_batch_arena_device(tulips_csum_mctx* m, const uint8_t* base,
 }
 
 } // extern "C"
+
+// ---------------------------------------------------------------------------
+// Flow-affine validation of device-resident frames (rss_route.hip).
+// ---------------------------------------------------------------------------
+namespace {
+
+using tulips_amd::launch_rss_gather;
+using tulips_amd::launch_rss_home;
+using tulips_amd::launch_rss_route;
+using tulips_amd::launch_rss_scatter;
+using tulips_amd::rss_route_blocks;
+using tulips_amd::rss_route_windows;
+using tulips_amd::RouteStarts;
+using tulips_amd::RouteWindows;
+using tulips_amd::RT_MAX_DEV;
+
+// (Re)size the router's workspace for n frames / `cells` histogram cells /
+// `tab` table entries / `packed` bytes on device `dev`. Growth waits for the
+// device (and every slot) first: earlier calls may still read these.
+hipError_t
+route_ws(tulips_csum_mctx* m, int dev, uint64_t n, uint64_t cells, uint64_t tab, uint64_t packed)
+{
+  RouteWs& r = m->route;
+  const bool moved = r.device != dev;
+  const bool grow_n = moved || n > r.n_cap, grow_c = moved || cells > r.cell_cap;
+  const bool grow_t = moved || tab > r.tab_cap, grow_p = moved || packed > r.packed_cap;
+  if (!(grow_n || grow_c || grow_t || grow_p || !r.totals_host)) {
+    return hipSuccess;
+  }
+  for (auto& d : m->slots) {
+    TCS_TRY(hipSetDevice(d.device));
+    TCS_TRY(hipStreamSynchronize(d.copy));
+    TCS_TRY(hipStreamSynchronize(d.comp));
+  }
+  if (r.device >= 0) {
+    TCS_TRY(hipSetDevice(r.device));
+    TCS_TRY(hipDeviceSynchronize());
+  }
+  auto realloc_dev = [&](bool grow, auto** p, uint64_t bytes) -> hipError_t {
+    if (!grow) {
+      return hipSuccess;
+    }
+    if (*p) {
+      TCS_TRY(hipSetDevice(r.device));
+      (void)hipFree(*p);
+      *p = nullptr;
+    }
+    TCS_TRY(hipSetDevice(dev));
+    void* q = nullptr;
+    TCS_TRY(hipMalloc(&q, bytes ? bytes : 16));
+    *p = static_cast<std::remove_reference_t<decltype(*p)>>(q);
+    return hipSuccess;
+  };
+  const uint64_t nn = std::max<uint64_t>(n, 1), nc = std::max<uint64_t>(cells, 1);
+  TCS_TRY(realloc_dev(grow_n, &r.dev_of, 2 * nn));
+  TCS_TRY(realloc_dev(grow_n, &r.perm, 4 * nn));
+  TCS_TRY(realloc_dev(grow_n, &r.poff, 8 * nn));
+  TCS_TRY(realloc_dev(grow_n, &r.plen, 2 * nn));
+  TCS_TRY(realloc_dev(grow_n, &r.rflags, nn));
+  TCS_TRY(realloc_dev(grow_c, &r.cells, 12 * nc));
+  TCS_TRY(realloc_dev(grow_c, &r.base_bytes, 8 * nc));
+  TCS_TRY(realloc_dev(moved || !r.totals, &r.totals, 16 * RT_MAX_DEV));
+  TCS_TRY(realloc_dev(grow_t, &r.table, 2 * std::max<uint64_t>(tab, 1)));
+  TCS_TRY(realloc_dev(grow_p, &r.packed, std::max<uint64_t>(packed, 16)));
+  if (grow_n) {
+    r.n_cap = nn;
+  }
+  if (grow_c) {
+    r.cell_cap = nc;
+  }
+  if (grow_t) {
+    r.tab_cap = std::max<uint64_t>(tab, 1);
+  }
+  if (grow_p) {
+    r.packed_cap = std::max<uint64_t>(packed, 16);
+  }
+  if (!r.totals_host) {
+    void* h = nullptr;
+    TCS_TRY(hipHostMalloc(&h, 16 * RT_MAX_DEV, 0));
+    r.totals_host = static_cast<uint64_t*>(h);
+  }
+  r.device = dev;
+  return hipSuccess;
+}
+
+hipError_t
+validate_rss_device(tulips_csum_mctx* m, int sdev, const uint8_t* base, const uint64_t* offsets,
+                    const uint16_t* lengths, uint32_t n, const RouteWindows& win, uint32_t init,
+                    const uint16_t* table, uint32_t table_len, uint8_t* flags,
+                    uint32_t* counters, uint16_t* device_of, hipStream_t st)
+{
+  const uint32_t nd = uint32_t(m->slots.size());
+  DevGuard guard;
+  uint32_t home = nd;
+  for (uint32_t k = 0; k < nd; ++k) {
+    if (m->slots[k].device == sdev) {
+      home = k;
+      break;
+    }
+  }
+  const uint64_t cells = uint64_t(rss_route_blocks(n)) * nd;
+  TCS_TRY(route_ws(m, sdev, n, cells, table_len, 0));
+  RouteWs& r = m->route;
+  TCS_TRY(hipSetDevice(sdev));
+  TCS_TRY(hipMemcpyAsync(r.table, table, 2ull * table_len, hipMemcpyHostToDevice, st));
+  uint16_t* dev_of = device_of ? device_of : r.dev_of;
+  uint32_t* blk_cnt = r.cells;
+  uint32_t* blk_bytes = r.cells + cells;
+  uint32_t* base_cnt = r.cells + 2 * cells;
+  TCS_TRY(launch_rss_route(win, base, offsets, lengths, n, r.table, table_len, init, nd, dev_of,
+                           blk_cnt, blk_bytes, base_cnt, r.base_bytes, r.totals, st));
+  TCS_TRY(hipMemcpyAsync(r.totals_host, r.totals, 16ull * nd, hipMemcpyDeviceToHost, st));
+  TCS_TRY(hipStreamSynchronize(st));
+  // frames per device (bounds) and where each other device's packed run
+  // starts in the gather buffer
+  RouteStarts starts{};
+  uint64_t packed = 0;
+  m->bounds[0] = 0;
+  for (uint32_t k = 0; k < nd; ++k) {
+    m->bounds[k + 1] = m->bounds[k] + uint32_t(r.totals_host[k]);
+    if (k != home) {
+      starts.at[k] = packed;
+      packed += r.totals_host[nd + k];
+    }
+  }
+  std::vector<uint64_t> run_bytes(nd);
+  for (uint32_t k = 0; k < nd; ++k) {
+    run_bytes[k] = r.totals_host[nd + k];
+  }
+  TCS_TRY(route_ws(m, sdev, n, cells, table_len, packed));
+  TCS_TRY(hipSetDevice(sdev));
+  TCS_TRY(launch_rss_scatter(offsets, lengths, n, nd, home, dev_of, base_cnt, r.base_bytes,
+                             r.totals, r.perm, r.poff, r.plen, st));
+  if (packed) {
+    TCS_TRY(launch_rss_gather(base, offsets, n, home, dev_of, r.perm, r.poff, r.plen, starts,
+                              r.packed, st));
+  }
+  hipEvent_t routed = nullptr;
+  TCS_TRY(hipEventCreateWithFlags(&routed, hipEventDisableTiming));
+  hipError_t e = hipEventRecord(routed, st);
+  std::vector<hipEvent_t> fin(nd, nullptr);
+  for (uint32_t k = 0; k < nd && e == hipSuccess; ++k) {
+    DevSlot& d = m->slots[k];
+    const uint32_t b0 = m->bounds[k], cnt = m->bounds[k + 1] - b0;
+    if (cnt == 0) {
+      continue;
+    }
+    int rc = TULIPS_STATUS_OK;
+    if (k == home) {
+      if ((e = hipSetDevice(d.device)) != hipSuccess ||
+          (e = hipStreamWaitEvent(d.comp, routed, 0)) != hipSuccess) {
+        break;
+      }
+      rc = tulips_csum_validate_frames(base, r.poff + b0, r.plen + b0, cnt, r.rflags + b0,
+                                       nullptr, d.comp);
+    } else {
+      // its packed frames, offsets (within the run), lengths, then flags
+      const uint64_t m_len = 8ull * cnt, m_fl = (m_len + 2ull * cnt + 15) & ~uint64_t(15);
+      if ((e = grow(d, reinterpret_cast<void**>(&d.buf), &d.buf_bytes, run_bytes[k] + 64)) !=
+            hipSuccess ||
+          (e = grow(d, reinterpret_cast<void**>(&d.meta), &d.meta_bytes, m_fl + cnt + 16)) !=
+            hipSuccess ||
+          (e = hipSetDevice(d.device)) != hipSuccess ||
+          (e = hipStreamWaitEvent(d.copy, routed, 0)) != hipSuccess ||
+          (d.used && (e = hipStreamWaitEvent(d.copy, d.done, 0)) != hipSuccess)) {
+        break;
+      }
+      // peer DMA over xGMI (the HIP runtime stages through host memory
+      // where the two devices have no peer path)
+      if ((e = hipMemcpyPeerAsync(d.buf, d.device, r.packed + starts.at[k], sdev, run_bytes[k],
+                                  d.copy)) != hipSuccess ||
+          (e = hipMemcpyPeerAsync(d.meta, d.device, r.poff + b0, sdev, 8ull * cnt, d.copy)) !=
+            hipSuccess ||
+          (e = hipMemcpyPeerAsync(d.meta + m_len, d.device, r.plen + b0, sdev, 2ull * cnt,
+                                  d.copy)) != hipSuccess) {
+        break;
+      }
+      if ((e = ensure_events(d, 1)) != hipSuccess || (e = hipSetDevice(d.device)) != hipSuccess ||
+          (e = hipEventRecord(d.ev[0], d.copy)) != hipSuccess ||
+          (e = hipStreamWaitEvent(d.comp, d.ev[0], 0)) != hipSuccess) {
+        break;
+      }
+      rc = tulips_csum_validate_frames(d.buf, reinterpret_cast<const uint64_t*>(d.meta),
+                                       reinterpret_cast<const uint16_t*>(d.meta + m_len), cnt,
+                                       d.meta + m_fl, nullptr, d.comp);
+      if (rc == TULIPS_STATUS_OK) {
+        e = hipMemcpyPeerAsync(r.rflags + b0, sdev, d.meta + m_fl, d.device, cnt, d.comp);
+      }
+    }
+    if (rc != TULIPS_STATUS_OK && e == hipSuccess) {
+      e = rc == TULIPS_STATUS_NO_MORE_RESOURCES ? hipErrorOutOfMemory : hipErrorLaunchFailure;
+    }
+    if (e == hipSuccess && (e = hipEventRecord(d.done, d.comp)) == hipSuccess) {
+      d.used = true;
+      fin[k] = d.done;
+    }
+  }
+  if (e == hipSuccess && (e = hipSetDevice(sdev)) == hipSuccess) {
+    for (uint32_t k = 0; k < nd && e == hipSuccess; ++k) {
+      if (fin[k]) {
+        e = hipStreamWaitEvent(st, fin[k], 0);
+      }
+    }
+  }
+  if (e == hipSuccess) {
+    e = launch_rss_home(r.perm, r.rflags, n, flags, counters, st);
+  }
+  if (e != hipSuccess) {
+    for (auto& d : m->slots) { // drain before reporting (the caller may free)
+      (void)hipSetDevice(d.device);
+      (void)hipStreamSynchronize(d.copy);
+      (void)hipStreamSynchronize(d.comp);
+    }
+    (void)hipSetDevice(sdev);
+    (void)hipStreamSynchronize(st);
+    (void)hipGetLastError();
+  }
+  (void)hipSetDevice(sdev);
+  (void)hipEventDestroy(routed);
+  return e;
+}
+
+} // namespace
+
+extern "C" int
+tulips_csum_mctx_validate_frames_rss_device(tulips_csum_mctx* m, const uint8_t* base,
+                                            const uint64_t* offsets, const uint16_t* lengths,
+                                            uint32_t n, const uint8_t* key, size_t key_len,
+                                            uint32_t init, const uint16_t* table,
+                                            uint32_t table_len, uint8_t* flags,
+                                            uint32_t* counters, uint16_t* device_of,
+                                            void* stream)
+{
+  tulips_amd::RouteWindows win;
+  if (!m || !table || table_len == 0 || table_len > 65536 ||
+      !rss_route_windows(key, key_len, &win)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  const uint32_t nd = uint32_t(m->devices.size());
+  for (uint32_t k = 0; k < table_len; ++k) {
+    if (table[k] >= nd) {
+      return TULIPS_STATUS_INVALID_ARGUMENT;
+    }
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return TULIPS_STATUS_INVALID_ARGUMENT; // the per-device counts need the host
+  }
+  hipDevice_t sd = 0;
+  if (hipStreamGetDevice(st, &sd) != hipSuccess) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (n == 0) {
+    DevGuard g;
+    (void)hipSetDevice(int(sd));
+    return counters ? status_of(hipMemsetAsync(counters, 0, 16, st)) : TULIPS_STATUS_OK;
+  }
+  if (!base || !offsets || !lengths || (!flags && !counters)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  DevGuard guard;
+  hipError_t e = ensure_slots(m);
+  if (e != hipSuccess) {
+    return status_of(e);
+  }
+  return status_of(validate_rss_device(m, int(sd), base, offsets, lengths, n, win, init, table,
+                                       table_len, flags, counters, device_of, st));
+}

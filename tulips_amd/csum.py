@@ -171,6 +171,10 @@ _SIGNATURES = {
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
     "tulips_csum_validate_frames_cpu": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp]),
+    "tulips_csum_mctx_validate_frames_rss_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32,
+                                                              _vp, C.c_size_t, C.c_uint32,
+                                                              _vp, C.c_uint32, _vp, _vp, _vp,
+                                                              _vp]),
     "tulips_csum_ctx_debug_set_seq": (C.c_int, [_vp, C.c_uint64]),
     "tulips_csum_mctx_set_peer_mode": (C.c_int, [_vp, C.c_int]),
 }
@@ -654,6 +658,31 @@ class MultiContext(HostContext):
             cnt.ctypes.data if with_counters else None, dev.ctypes.data),
             "tulips_csum_mctx_validate_frames_rss_host")
         return (flags, dev, cnt) if with_counters else (flags, dev)
+
+    def validate_frames_rss_device(self, arena, offsets, lengths, key: bytes, table, *,
+                                   init: int = 0, counters=None, want_device_of: bool = True,
+                                   stream=None):
+        """Flow-affine validation of frames resident on `stream`'s device
+        (tulips_csum_mctx_validate_frames_rss_device). Returns (flags,
+        device_of) device tensors; `counters` (int32[4] device tensor) is
+        zeroed and filled when given."""
+        import numpy as np
+        import torch
+        n = int(offsets.numel())
+        if int(lengths.numel()) != n:
+            raise ValueError("offsets/lengths size mismatch")
+        dev = offsets.device
+        flags = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        devof = torch.empty(max(n, 1), dtype=torch.int16, device=dev) if want_device_of else None
+        if counters is not None and int(counters.numel()) < 4:
+            raise ValueError("counters needs 4 entries")
+        tb = np.ascontiguousarray(table, dtype=np.uint16)
+        kp, _keep = _buf(key)
+        _check(lib.tulips_csum_mctx_validate_frames_rss_device(
+            self._h, _addr(arena), _addr(offsets), _addr(lengths), n, kp, len(key),
+            init & 0xFFFFFFFF, tb.ctypes.data, len(tb), _addr(flags), _addr(counters),
+            _addr(devof), _stream(stream)), "tulips_csum_mctx_validate_frames_rss_device")
+        return flags[:n], (devof[:n] if devof is not None else None)
 
     def batch_fixed_device(self, arena, stride: int, length: int, n: int, *, seeds=None,
                            src=None, dst=None, mode: int = RAW, out=None, stream=None,
