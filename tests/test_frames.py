@@ -586,6 +586,34 @@ def test_gpu_every_frame_geometry(oracle, geo, nt):
     assert np.array_equal(a.cpu().numpy(), exp_arena)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_blocks", [0, 7, 300])
+def test_gpu_validation_two_frames_per_subgroup(oracle, max_blocks):
+    """Validation at 16 x 6 with two frames per subgroup in flight
+    (tuning.sps = 2): mutated fixture frames at an odd base, an odd frame
+    count (the second frame of the last subgroup absent), grid caps that make
+    subgroups loop; flags and counters vs the oracle."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(2 + max_blocks)
+    arena = np.concatenate([np.zeros(3, np.uint8), mutate(fx, rng, 2000)])
+    for n in (len(fx["offsets"]), 2999, 17, 1):
+        offs = fx["offsets"][:n] + np.uint64(3)
+        lens = fx["lengths"][:n]
+        t = csum.Tuning(group=16, unroll=6, nontemporal=1, max_blocks=max_blocks, sps=2)
+        a, o, l = _dev(arena, offs.astype(np.int64), lens.view(np.int16))
+        fl = torch.full((n,), 0xA5, dtype=torch.uint8, device="cuda:0")
+        cnt = torch.zeros(4, dtype=torch.int32, device="cuda:0")
+        assert csum.lib.tulips_csum_frames_tuned(0, a.data_ptr(), o.data_ptr(), l.data_ptr(), n,
+                                                 fl.data_ptr(), cnt.data_ptr(), t,
+                                                 torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        exp = oracle.validate_frames(arena, offs, lens)
+        np.testing.assert_array_equal(fl.cpu().numpy(), exp, err_msg=str(n))
+        np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32), counters_of(exp))
+
+
 def test_frames_tuned_rejects_bad_geometry():
     from tulips_amd import csum
     f = csum.lib.tulips_csum_frames_tuned

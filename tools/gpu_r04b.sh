@@ -1,7 +1,8 @@
-# round-4 session b: the whole GPU suite (then the 4-rank self-launched bench
-# test, which the suite also holds, is timed there)
+# round-4 session b: the whole GPU suite, then the frame-validation A/B
 set -u
 O=gpurun_out/r04b
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu tests > $O/suite.log 2>&1
-rc=$?; tail -5 $O/suite.log; exit $rc
+rc=$?; tail -5 $O/suite.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u tools/probe_frames_fps.py > $O/frames_fps.log 2>&1
+rc=$?; tail -3 $O/frames_fps.log; exit $rc

@@ -65,15 +65,19 @@ using namespace frame;
 // spills 12 B and is slower. The generation bound applies to the default
 // geometry and smaller (U <= 6): at 16 x 8 and 8 x 8/16 it spilled 12-364 B
 // per lane, so those keep their natural register counts.
-constexpr int FRAME_VAL_WAVES = 0, FRAME_GEN_WAVES = 6;
+constexpr int FRAME_VAL_WAVES = 0, FRAME_GEN_WAVES = 6, FRAME_FPS2_WAVES = 0;
 
 // OP: 0 = validate (flags, counters), 1 = generate in place (the two
 // checksum fields patched into the frame; `fields` optionally gets a copy),
 // 2 = generate compact fields only (frames untouched, one u32 per frame).
 enum { OP_VALIDATE = 0, OP_GENERATE = 1, OP_FIELDS = 2 };
 
-template<int OP, int FG, int FU, bool NT>
-__global__ __launch_bounds__(1024, OP != OP_VALIDATE && FU <= 6 ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
+// FPS: frames per subgroup in flight. With FPS = 2 a subgroup issues the
+// loads of two frames (f and f + nsub) before summing either, so a wave keeps
+// twice the bytes in flight at the same instruction count per byte, and the
+// grid is half as many workgroups.
+template<int OP, int FG, int FU, bool NT, int FPS = 1>
+__global__ __launch_bounds__(1024, FPS == 2 ? FRAME_FPS2_WAVES : OP != OP_VALIDATE && FU <= 6 ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
 frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ shards,
@@ -99,18 +103,8 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
     }
     __syncthreads();
   }
-  if (f < n) {
-  uint64_t o = offs[f];
-  uint32_t flen = lens[f];
-  while (true) {
-    const uintptr_t fa = reinterpret_cast<uintptr_t>(base) + o;
-    FrameChunks<FG, FU> fc;
-    load_frame<FG, FU, NT>(fa, flen, lane, fc);
-    const uint32_t fn = f + nsub;
-    const uint32_t pf = min(fn, n - 1);
-    const uint64_t o_next = offs[pf];
-    const uint32_t l_next = lens[pf];
-
+  // frame `g` at address fa (length flen) from its loaded chunks
+  auto one = [&](const FrameChunks<FG, FU>& fc, uint32_t g, uintptr_t fa, uint32_t flen) {
     const Header h = frame_header(fc, flen, sub0);
     const int h0 = fc.h0;
     const bool do_l4 = h.tcp && !h.trunc && (!GENERATE || h.tcplen >= 18u);
@@ -146,10 +140,10 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
           // the header words gives): what tulips_csum_generate_frames_host
           // patches into the host copy, and tulips_csum_generate_fields'
           // whole output
-          fields[f] = written;
+          fields[g] = written;
         }
         if (flags) {
-          flags[f] = uint8_t(frame_flags(h, h.ipv4, do_l4));
+          flags[g] = uint8_t(frame_flags(h, h.ipv4, do_l4));
         }
       } else {
         const bool ip_ok = h.ipv4 && finish(ip_part, ((fa + 14) & 1) != 0, MODE_INET, 0,
@@ -157,7 +151,7 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
         const bool l4_ok = do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0,
                                            h.src, h.dst, h.tcplen) == 0xffffu;
         if (flags) {
-          flags[f] = uint8_t(frame_flags(h, ip_ok, l4_ok));
+          flags[g] = uint8_t(frame_flags(h, ip_ok, l4_ok));
         }
         if (count) {
           if (h.ipv4) {
@@ -175,13 +169,50 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
         }
       }
     }
-    if (fn >= n) {
-      break;
+  };
+  if (f < n) {
+    // frames f (and f + nsub when FPS == 2) per round; the next round's
+    // offsets and lengths are fetched behind this round's loads
+    static_assert(FPS == 1 || FPS == 2, "frames per subgroup");
+    const uintptr_t b0 = reinterpret_cast<uintptr_t>(base);
+    auto meta = [&](uint32_t g, uint64_t& o, uint32_t& l) {
+      o = offs[min(g, n - 1)];
+      l = g < n ? uint32_t(lens[min(g, n - 1)]) : 0u;
+    };
+    uint64_t o0, o1 = 0;
+    uint32_t l0, l1 = 0;
+    meta(f, o0, l0);
+    if constexpr (FPS == 2) {
+      meta(f + nsub, o1, l1);
     }
-    f = fn;
-    o = o_next;
-    flen = l_next;
-  }
+    while (true) {
+      FrameChunks<FG, FU> fc0, fc1;
+      load_frame<FG, FU, NT>(b0 + o0, l0, lane, fc0);
+      if constexpr (FPS == 2) {
+        load_frame<FG, FU, NT>(b0 + o1, l1, lane, fc1);
+      }
+      const uint32_t fn = f + uint32_t(FPS) * nsub;
+      uint64_t p0, p1 = 0;
+      uint32_t q0, q1 = 0;
+      meta(fn, p0, q0);
+      if constexpr (FPS == 2) {
+        meta(fn + nsub, p1, q1);
+      }
+      one(fc0, f, b0 + o0, l0);
+      if constexpr (FPS == 2) {
+        if (f + nsub < n) {
+          one(fc1, f + nsub, b0 + o1, l1);
+        }
+      }
+      if (fn >= n) {
+        break;
+      }
+      f = fn;
+      o0 = p0;
+      l0 = q0;
+      o1 = p1;
+      l1 = q1;
+    }
   }
   if (count) {
     __syncthreads();
@@ -388,13 +419,21 @@ launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n
            hipStream_t stream)
 {
   const uint32_t block = fl.block ? fl.block : 256;
-  const uint32_t per_block = block / G;
+  const uint32_t fps = (OP == OP_VALIDATE && G == 16 && U == 6 && fl.fps == 2) ? 2u : 1u;
+  const uint32_t per_block = block / G * fps;
   uint64_t blocks = (uint64_t(n) + per_block - 1) / per_block;
   const uint64_t cap = fl.max_blocks ? fl.max_blocks : 65535;
   if (blocks > cap) {
     blocks = cap;
   }
   (void)hipGetLastError();
+  if constexpr (OP == OP_VALIDATE && G == 16 && U == 6) {
+    if (fps == 2) {
+      hipLaunchKernelGGL((frame_kernel<OP, G, U, NT, 2>), dim3(uint32_t(blocks)),
+                         dim3(block), 0, stream, base, offs, lens, n, flags, counters, fields);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((frame_kernel<OP, G, U, NT>), dim3(uint32_t(blocks)),
                      dim3(block), 0, stream, base, offs, lens, n, flags, counters, fields);
   return hipGetLastError();
@@ -609,6 +648,7 @@ tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
   fl.max_blocks = tuning->max_blocks;
   fl.block = uint32_t(tuning->block < 0 ? 0 : tuning->block);
   fl.nontemporal = tuning->nontemporal < 0 ? 1 : (tuning->nontemporal & 1);
+  fl.fps = tuning->sps == 2 ? 2 : 1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipError_t e;
   if (op == 0) {
