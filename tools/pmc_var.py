@@ -10,6 +10,10 @@ times each, for rocprofv3 --pmc instruction/cycle counters:
 Summarise with tools/pmc_var.py --summarise OUT/run_counter_collection.csv
 (per kernel and workload: counters per dispatch, per wave, per segment).
 """
+# archived kinds (round 3): only builds of tools/variants/ accept them; the
+# product library rejects them (InvalidArgument)
+KIND_HYBRID, KIND_BALANCED = 2, 4
+
 import csv
 import json
 import os
@@ -33,7 +37,7 @@ def run():
     sh = torch.cuda.current_stream().cuda_stream
     geoms = {"packed": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=4, nontemporal=1,
                                    block=256, sps=2),
-             "balanced": csum.Tuning(kind=csum.KIND_BALANCED, group=8, unroll=2, nontemporal=1,
+             "balanced": csum.Tuning(kind=KIND_BALANCED, group=8, unroll=2, nontemporal=1,
                                      block=256, sps=2),
              "vpacked": csum.Tuning(kind=csum.KIND_PACKED, group=8, unroll=2, nontemporal=1,
                                     block=256, sps=4),
