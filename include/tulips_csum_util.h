@@ -29,7 +29,11 @@ extern "C" {
                                        bytes; a segment crossing ranges is
                                        summed in parts that meet in a
                                        per-range word of the stream's state.
-                                       `group` 0 (or 7: the same form) */
+                                       `group` 0 (or 7: the same form);
+                                       `group` 9 (unroll 6..8): the
+                                       tail-shaped cut, the last `sps` %
+                                       (0 = 12) of the arena in ranges of
+                                       unroll / 2 rows (measured variant) */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning

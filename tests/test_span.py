@@ -26,7 +26,9 @@ from tulips_amd import csum  # noqa: E402
 DEV = "cuda:0"
 # (chunks per lane, form): the split form, 0 = default (= 7). The library
 # default is 7 chunks per lane (28 KiB ranges).
-GEOMS = ((4, 0), (5, 0), (6, 0), (7, 7), (7, 0), (8, 0))
+GEOMS = ((4, 0), (5, 0), (6, 0), (7, 7), (7, 0), (8, 0),
+         # the tail-shaped cut (group 9; third entry: tail percent, 0 = 12)
+         (7, 9), (8, 9, 50), (6, 9, 3))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -46,8 +48,9 @@ def u16(t):
 
 
 def tuning(geo, nt=1):
-    u, halo = geo
-    return csum.Tuning(kind=csum.KIND_SPAN, unroll=u, group=halo, nontemporal=nt)
+    u, halo = geo[:2]
+    return csum.Tuning(kind=csum.KIND_SPAN, unroll=u, group=halo, nontemporal=nt,
+                       sps=geo[2] if len(geo) > 2 else 0)
 
 
 def in_order(rng, lens, max_gap=0, gap_p=0.0):

@@ -38,9 +38,16 @@ WORKLOADS = [
     # 65,536 frames, 16 per 256-thread block (the host path's small bursts
     # launch the same kernels with smaller grids); frame_kernel<OP, ...>:
     # 0 validate, 1 generate in place, 2 compact fields
+    # (round 4: a fifth template argument, frames per subgroup, 1 by default)
+    ("frame_kernel<0, 16, 6, true, 1>", 1048576, "frames_validate_F1514"),
+    ("frame_kernel<1, 16, 6, true, 1>", 1048576, "frames_generate_F1514"),
+    ("frame_kernel<2, 16, 6, true, 1>", 1048576, "frames_generate_fields_F1514"),
     ("frame_kernel<0, 16, 6, true>", 1048576, "frames_validate_F1514"),
     ("frame_kernel<1, 16, 6, true>", 1048576, "frames_generate_F1514"),
     ("frame_kernel<2, 16, 6, true>", 1048576, "frames_generate_fields_F1514"),
+    # configs[3] as written: one 64-lane wave per segment
+    ("csum_kernel<64, 4, true, tulips_amd::(anonymous namespace)::VarSegs>", None,
+     "ZIPF_one_wave_per_segment"),
     ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
     ("seg_prologue_small_kernel", None, "segment_TSO_64K_mss1460_prologue"),
     ("rss_kernel", None, "rss_toeplitz_16M"),
@@ -50,7 +57,7 @@ WORKLOADS = [
 # read + written by segmentation (super-frames in, segments out); RSS 12 B in
 # + 4 B out per tuple
 ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673,
-              "ZIPF_any_layout": 43772673,
+              "ZIPF_any_layout": 43772673, "ZIPF_one_wave_per_segment": 43772673,
               "frames_validate_F1514": 65536 * 1514, "frames_generate_F1514": 65536 * 1514,
               "frames_generate_fields_F1514": 65536 * 1514 + 65536 * 4,
               "F9000_read_same_bytes": 65536 * 9000,

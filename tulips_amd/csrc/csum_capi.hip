@@ -414,6 +414,7 @@ batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
   if (!span_geometry_ok(a.unroll, a.group)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
+  a.spw = (tuning && a.group == 9) ? tuning->sps : 0; // tail-shaped: tail percent
   const int32_t nt = (tuning && tuning->nontemporal >= 0) ? tuning->nontemporal : 1;
   a.nontemporal = (nt & 1) != 0;
   a.nt_store = (nt & 2) != 0;

@@ -288,6 +288,7 @@ struct SpanArgs
   uint64_t nslots; // words in `slots`
   uint32_t salt;   // xor-ed into the split words' tag (per word array)
   uint64_t bias;   // segment i starts at base + offs[i] - bias
+  uint64_t k1;     // tail-shaped form: ranges k >= k1 are the short tail ranges
 };
 
 typedef const __attribute__((address_space(1))) uint64_t* gu64_ptr;

@@ -272,6 +272,27 @@ launch_span_u(const SpanArgs& sp, hipStream_t stream)
   return hipGetLastError();
 }
 
+// The tail-shaped cut (group 9): ranges of U rows over the first
+// (100 - tail_pct) % of the arena, then ranges of TR = U / 2 rows.
+template<int U>
+hipError_t
+launch_span_tail(SpanArgs sp, uint32_t tail_pct, hipStream_t stream)
+{
+  constexpr int TR = U / 2;
+  constexpr uint64_t W = 4096ull * U, WT = 4096ull * TR;
+  const uint64_t hull = sp.arena + (reinterpret_cast<uintptr_t>(sp.base) & 15u);
+  const uint64_t k1 = hull / 100 * (100 - tail_pct) / W;
+  const uint64_t ranges = k1 + (hull - k1 * W) / WT + 1;
+  if (ranges > 0x7fffffffull || ranges > sp.nslots) {
+    return hipErrorInvalidValue;
+  }
+  sp.k1 = k1;
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((csum_span_kernel<U, NoProbe, 8, 1024, U / 3, true, 256, TR>),
+                     dim3(uint32_t(ranges)), dim3(256), 0, stream, sp, NoProbe{});
+  return hipGetLastError();
+}
+
 template<int G, int U, bool NT, class Segs>
 hipError_t
 launch_one(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
@@ -348,7 +369,8 @@ launch_var(const uint8_t* base, const uint64_t* offs, const uint16_t* lens,
 bool
 span_geometry_ok(int u, int group)
 {
-  return (group == 0 || group == 7) && u >= 4 && u <= 8;
+  return ((group == 0 || group == 7) && u >= 4 && u <= 8) ||
+         (group == 9 && u >= 6 && u <= 8);
 }
 
 hipError_t
@@ -359,7 +381,7 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
     return hipSuccess;
   }
   SpanArgs sp{base, arena, offs, lens, a.seeds, a.src, a.dst, a.out, a.bad,
-              a.n, a.mode, a.nt_store ? 1u : 0u, nullptr, 0, 0, a.offs_bias};
+              a.n, a.mode, a.nt_store ? 1u : 0u, nullptr, 0, 0, a.offs_bias, 0};
   // the stream's per-range words, held for the launch
   std::shared_ptr<StreamState> ss;
   hipError_t e = stream_state(stream, &ss);
@@ -367,10 +389,21 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
     return e;
   }
   std::lock_guard<std::recursive_mutex> g(ss->call);
-  const uint64_t ranges = span_ranges(base, arena, 4096ull * a.unroll);
+  // (the tail-shaped cut has at most twice the ranges of the uniform one)
+  const uint64_t ranges =
+    span_ranges(base, arena, 4096ull * a.unroll) * (a.group == 9 ? 2 : 1);
   e = span_slots(*ss, stream_capturing(stream), ranges, &sp.slots, &sp.nslots, &sp.salt);
   if (e != hipSuccess) {
     return e == hipErrorStreamCaptureUnsupported ? hipErrorInvalidValue : e;
+  }
+  if (a.group == 9) {
+    const uint32_t pct = a.spw > 0 && a.spw < 100 ? uint32_t(a.spw) : 12u;
+    switch (a.unroll) {
+      case 6: return launch_span_tail<6>(sp, pct, stream);
+      case 7: return launch_span_tail<7>(sp, pct, stream);
+      case 8: return launch_span_tail<8>(sp, pct, stream);
+      default: return hipErrorInvalidValue;
+    }
   }
 #define TCS_SCASE(U_)                                                          \
   if (a.unroll == U_) {                                                        \

@@ -103,15 +103,21 @@ struct NoProbe
 // size) meets its other part by one exchange per part, and the word is not
 // re-zeroed: the next launch's tag differs (profiles/probe_span_early_r03.txt:
 // 0.2-0.4 us per ZIPF launch against compare-and-swap + re-zero).
+// TR > 0: the tail-shaped cut (measured against the uniform
+// one by tools/probe_span_tail.py): ranges k < p.k1 hold U rows, the last
+// ones (dispatched last) TR rows, so the final workgroups on each CU finish
+// their data sooner and their tails overlap. TR = 0: every range U rows.
 template<int U, class Probe = NoProbe, uint32_t XC = 8, uint32_t NWIN = 1024, int MH = U / 3,
-         bool XCHG = true, uint32_t TB = 256>
+         bool XCHG = true, uint32_t TB = 256, int TR = 0>
 __global__ __launch_bounds__(TB, 7) void
 csum_span_kernel(SpanArgs p, Probe pr)
 {
   constexpr uint32_t NWV = TB / 64; // waves per workgroup
   static_assert(TB % 64 == 0 && NWV * U <= 64, "row totals fit one wave scan");
+  static_assert(TR >= 0 && TR <= U, "tail rows");
   constexpr uint32_t NC = TB * U;
   constexpr uint64_t W = 16ull * NC;
+  constexpr uint64_t WT = 16ull * TB * uint64_t(TR ? TR : U);
   constexpr int RW = NWIN / TB;
   __shared__ uint32_t s_sc[NC];
   __shared__ uint32_t s_tot[NWV * U];
@@ -127,17 +133,31 @@ csum_span_kernel(SpanArgs p, Probe pr)
   const uintptr_t b = reinterpret_cast<uintptr_t>(p.base);
   const uint64_t d = b & 15u;
   const uintptr_t A = b & ~uintptr_t(15);
-  const uintptr_t x0 = A + uint64_t(k) * W, x1 = x0 + W;
+  // range k = [A + rstart(k), A + rstart(k + 1)); rix(o) = the range of
+  // arena offset o (from A)
+  const uint64_t K1 = TR ? p.k1 : ~0ull;
+  auto rstart = [&](uint64_t kk) -> uint64_t {
+    return (TR && kk > K1) ? K1 * W + (kk - K1) * WT : kk * W;
+  };
+  auto rix = [&](uint64_t o) -> uint64_t {
+    return (TR && o >= K1 * W) ? K1 + (o - K1 * W) / WT : o / W;
+  };
+  const uint32_t rows = (TR && uint64_t(k) >= K1) ? uint32_t(TR) : uint32_t(U);
+  const uintptr_t x0 = A + rstart(k), x1 = A + rstart(uint64_t(k) + 1);
   const uintptr_t aend = b + p.arena;
   const uintptr_t zero = reinterpret_cast<uintptr_t>(k_zero_chunk);
   const uintptr_t last = p.arena ? ((aend - 1) & ~uintptr_t(15)) : zero;
   const uint32_t n = p.n;
   const gu64_ptr offs = reinterpret_cast<gu64_ptr>(reinterpret_cast<uintptr_t>(p.offs));
   const gu16_ptr lens = reinterpret_cast<gu16_ptr>(reinterpret_cast<uintptr_t>(p.lens));
-  const uint64_t tg0 = k ? uint64_t(k) * W - d : 0, tg1 = uint64_t(k + 1) * W - d;
+  const uint64_t tg0 = k ? (x0 - A) - d : 0, tg1 = (x1 - A) - d;
   // a chunk of the range (or zeros), clamped into the arena
   auto chunk_at = [&](uintptr_t a) {
     return reinterpret_cast<gchunk_ptr>(p.arena ? min(a, last) : zero);
+  };
+  // row j of the range (rows past a short tail range's read zeros)
+  auto row_at = [&](uint32_t j, uintptr_t a) {
+    return (TR && j >= rows) ? reinterpret_cast<gchunk_ptr>(zero) : chunk_at(a);
   };
 
   // 1. the offsets window, then the range's chunks (temporal whatever the
@@ -159,7 +179,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
   u32x4 v[U];
 #pragma unroll
   for (uint32_t j = 0; j < uint32_t(MH); ++j) {
-    v[j] = load_chunk<false>(chunk_at(x0 + 16u * (j * TB + t)));
+    v[j] = load_chunk<false>(row_at(j, x0 + 16u * (j * TB + t)));
   }
   __builtin_amdgcn_sched_barrier(0);
   pr.mark(k, w, lane, 1);
@@ -225,7 +245,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
   if constexpr (MH < U) {
 #pragma unroll
     for (uint32_t j = MH; j < uint32_t(U); ++j) {
-      v[j] = load_chunk<false>(chunk_at(x0 + 16u * (j * TB + t)));
+      v[j] = load_chunk<false>(row_at(j, x0 + 16u * (j * TB + t)));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -299,7 +319,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
     }
     // a part goes to a word only for a segment starting inside the arena
     // whose first range has one (always, under the arena contract)
-    const uint64_t ra = (sa - A) / W;
+    const uint64_t ra = rix(sa - A);
     const bool split = act && (sa < x0 || se > x1) && sa >= A && sa < se && ra < p.nslots;
     bool done = act && !split;
     uint32_t r = finish(sum, (sa & 1u) != 0, p.mode, side.seed, side.src, side.dst, sl);
@@ -315,7 +335,7 @@ csum_span_kernel(SpanArgs p, Probe pr)
     pr.mark(k, w, lane, 4);
     if (__builtin_amdgcn_ballot_w64(split) != 0) {
       if (split) {
-        const uint32_t need = uint32_t((se - 1 - A) / W - ra); // arrivals before the last
+        const uint32_t need = uint32_t(rix(se - 1 - A) - ra); // arrivals before the last
         const uint32_t part = fold32(sum);
         const uint64_t mine = (tag << WORD_TAG_SHIFT) | (1ull << WORD_ARR_SHIFT) | part;
         unsigned long long* wp = reinterpret_cast<unsigned long long*>(p.slots + ra);
