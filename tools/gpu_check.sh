@@ -9,7 +9,7 @@
 # script (pytest's rc 1 = "tests failed" is reported and also ends it).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -30,6 +30,8 @@ step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stat
 python tools/trace_bursts.py $OUT/stats/run_kernel_trace.csv --all > $OUT/bursts_all.jsonl
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
 step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
-step rehearsal_w8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 8 --dist-backend gloo --one-device --steps 64 --warmup 16 --no-cpu-baseline
+# (no launcher: bench.py starts torch.distributed.run itself, as under the
+# driver's `python bench.py --gpus 8`)
+step rehearsal_w8 600 python bench.py --gpus 8 --dist-backend gloo --one-device --steps 64 --warmup 16 --no-cpu-baseline
 tail -1 $OUT/rehearsal_w8.log > $OUT/rehearsal_w8.json
 echo "== done"
