@@ -1365,6 +1365,13 @@ validate_rss_device(tulips_csum_mctx* m, int sdev, const uint8_t* base, const ui
   TCS_TRY(route_ws(m, sdev, n, cells, table_len, 0));
   RouteWs& r = m->route;
   TCS_TRY(hipSetDevice(sdev));
+  // the previous call's devices may still read the workspace (its packed
+  // runs, offsets, lengths) when that call was ordered on another stream
+  for (auto& d : m->slots) {
+    if (d.used) {
+      TCS_TRY(hipStreamWaitEvent(st, d.done, 0));
+    }
+  }
   TCS_TRY(hipMemcpyAsync(r.table, table, 2ull * table_len, hipMemcpyHostToDevice, st));
   uint16_t* dev_of = device_of ? device_of : r.dev_of;
   uint32_t* blk_cnt = r.cells;
