@@ -1258,6 +1258,30 @@ def burst_latency(torch, csum):
                 if path == 1:
                     ent[name]["gpu_service_us"] = round(out[4], 2)
             res[str(nf)] = ent
+    # the same bursts cold: a 256 MB page-locked ring of copies of the
+    # burst, one copy per call, so the host code meets frames outside the
+    # CPU caches (as frames a NIC has just written by DMA would be)
+    cold = {}
+    ring_bytes = 256 << 20
+    with csum.HostContext(torch.cuda.current_device(), chunk_bytes=4 << 20) as ctx:
+        for nf in (8, 64, 256, 1024):
+            ar, offs, lens = burst_frames(nf)
+            nb = ring_bytes // len(ar)
+            ring = torch.from_numpy(np.tile(ar, nb)).pin_memory()
+            flags = np.empty(nf, np.uint8)
+            ent = {}
+            for name, path in (("zero_copy", 1), ("cpu_product", 2)):
+                ctx.set_lowlat(False)
+                reps = int(min(nb, 2000))
+                rc = csum.lib.tulips_csum_time_validate_ring(
+                    ctx._h, path, ring.data_ptr(), len(ar), nb, offs.ctypes.data,
+                    lens.ctypes.data, nf, reps, flags.ctypes.data, out)
+                ent[name] = ({"error": rc} if rc else
+                             {"us_median": round(out[0], 2), "us_p99": round(out[1], 2),
+                              "reps": reps, "parity": "ok" if bool((flags == 0x0F).all())
+                              else "MISMATCH"})
+            cold[str(nf)] = ent
+            del ring
     # the burst size from which the zero-copy launch beats the host code
     cross = None
     for nf in BURSTS:
@@ -1271,7 +1295,10 @@ def burst_latency(torch, csum):
                         "cpu_product = tulips_csum_validate_frames_cpu, the library's host "
                         "code the gpucsum decorator uses below its crossover",
             "gpu_beats_cpu_from_burst": cross,
-            "bursts": res}
+            "bursts": res,
+            "cold_ring": {"what": "the same bursts from a 256 MB page-locked ring, a "
+                                  "different copy per call (tulips_csum_time_validate_ring)",
+                          "bursts": cold}}
 
 
 def beside_server(torch, csum, timer, arena, batch_bytes):

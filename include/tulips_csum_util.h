@@ -122,6 +122,14 @@ typedef struct tulips_csum_ctx tulips_csum_ctx;
 int tulips_csum_time_validate(tulips_csum_ctx* ctx, int path, const uint8_t* base,
                               const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
                               uint32_t reps, uint8_t* flags, double* out);
+/* The same over a ring of `nbursts` bursts laid `burst_stride` bytes apart
+ * (call r validates the burst at ring + (r % nbursts) * burst_stride, same
+ * offsets and lengths): with a ring larger than the host caches every call
+ * meets frames that are not in them. */
+int tulips_csum_time_validate_ring(tulips_csum_ctx* ctx, int path, const uint8_t* ring,
+                                   uint64_t burst_stride, uint32_t nbursts,
+                                   const uint64_t* offsets, const uint16_t* lengths,
+                                   uint32_t n, uint32_t reps, uint8_t* flags, double* out);
 
 /* Test hooks. tulips_csum_ctx_debug_set_seq: the sequence number of the
  * context's last zero-copy request (its low 16 bits tag the next request's

@@ -1092,11 +1092,22 @@ tulips_csum_time_validate(tulips_csum_ctx* ctx, int path, const uint8_t* base,
                           const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
                           uint32_t reps, uint8_t* flags, double* out)
 {
-  if (!ctx || !out || reps == 0 || path < 0 || path > 2) {
+  return tulips_csum_time_validate_ring(ctx, path, base, 0, 1, offsets, lengths, n, reps,
+                                        flags, out);
+}
+
+extern "C" int
+tulips_csum_time_validate_ring(tulips_csum_ctx* ctx, int path, const uint8_t* ring,
+                               uint64_t burst_stride, uint32_t nbursts,
+                               const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
+                               uint32_t reps, uint8_t* flags, double* out)
+{
+  if (!ctx || !out || reps == 0 || path < 0 || path > 2 || nbursts == 0) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   std::vector<double> t(reps), g;
   for (uint32_t r = 0; r < reps; ++r) {
+    const uint8_t* base = ring + uint64_t(r % nbursts) * burst_stride;
     const auto t0 = std::chrono::steady_clock::now();
     const int rc =
       path == 2   ? tulips_csum_validate_frames_cpu(base, offsets, lengths, n, flags, nullptr)
