@@ -587,12 +587,14 @@ def test_gpu_every_frame_geometry(oracle, geo, nt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sps", [2, 3])
 @pytest.mark.parametrize("max_blocks", [0, 7, 300])
-def test_gpu_validation_two_frames_per_subgroup(oracle, max_blocks):
+def test_gpu_validation_two_frames_per_subgroup(oracle, max_blocks, sps):
     """Validation at 16 x 6 with two frames per subgroup in flight
-    (tuning.sps = 2): mutated fixture frames at an odd base, an odd frame
-    count (the second frame of the last subgroup absent), grid caps that make
-    subgroups loop; flags and counters vs the oracle."""
+    (tuning.sps = 2) and as a software pipeline (sps = 3): mutated fixture
+    frames at an odd base, odd frame counts (the second frame of the last
+    subgroup absent), grid caps that make subgroups loop; flags and counters
+    vs the oracle."""
     import torch
     from tulips_amd import csum
     fx = frames_fixture()
@@ -601,7 +603,7 @@ def test_gpu_validation_two_frames_per_subgroup(oracle, max_blocks):
     for n in (len(fx["offsets"]), 2999, 17, 1):
         offs = fx["offsets"][:n] + np.uint64(3)
         lens = fx["lengths"][:n]
-        t = csum.Tuning(group=16, unroll=6, nontemporal=1, max_blocks=max_blocks, sps=2)
+        t = csum.Tuning(group=16, unroll=6, nontemporal=1, max_blocks=max_blocks, sps=sps)
         a, o, l = _dev(arena, offs.astype(np.int64), lens.view(np.int16))
         fl = torch.full((n,), 0xA5, dtype=torch.uint8, device="cuda:0")
         cnt = torch.zeros(4, dtype=torch.int32, device="cuda:0")

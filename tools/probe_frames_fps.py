@@ -42,7 +42,8 @@ def main():
     torch.cuda.synchronize()
     alg = nf * flen
     tunings = {"fps1": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=1),
-               "fps2": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=2)}
+               "fps2": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=2),
+               "pipelined": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=3)}
 
     def fval(t):
         def f(i, st):

@@ -67,7 +67,7 @@ struct FrameLaunch
   uint32_t max_blocks = 0; // grid cap
   uint32_t block = 0;      // threads per workgroup
   int nontemporal = 1;     // nt chunk loads
-  int fps = 1;             // validation at 16 x 6: frames per subgroup in flight (1, 2)
+  int fps = 1;             // validation at 16 x 6: 1, 2 (two frames in flight), 3 (pipelined)
 };
 bool frame_geometry_ok(int group, int unroll, uint32_t block);
 // fields (nullable): per frame, the IPv4 (low 16 bits) and TCP (high 16)

@@ -77,7 +77,7 @@ enum { OP_VALIDATE = 0, OP_GENERATE = 1, OP_FIELDS = 2 };
 // twice the bytes in flight at the same instruction count per byte, and the
 // grid is half as many workgroups.
 template<int OP, int FG, int FU, bool NT, int FPS = 1>
-__global__ __launch_bounds__(1024, FPS == 2 ? FRAME_FPS2_WAVES : OP != OP_VALIDATE && FU <= 6 ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
+__global__ __launch_bounds__(FPS == 3 ? 256 : 1024, FPS >= 2 ? FRAME_FPS2_WAVES : OP != OP_VALIDATE && FU <= 6 ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
 frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ shards,
@@ -173,7 +173,7 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
   if (f < n) {
     // frames f (and f + nsub when FPS == 2) per round; the next round's
     // offsets and lengths are fetched behind this round's loads
-    static_assert(FPS == 1 || FPS == 2, "frames per subgroup");
+    static_assert(FPS >= 1 && FPS <= 3, "frames per subgroup");
     const uintptr_t b0 = reinterpret_cast<uintptr_t>(base);
     auto meta = [&](uint32_t g, uint64_t& o, uint32_t& l) {
       o = offs[min(g, n - 1)];
@@ -182,10 +182,30 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
     uint64_t o0, o1 = 0;
     uint32_t l0, l1 = 0;
     meta(f, o0, l0);
+    if constexpr (FPS == 3) {
+      // software pipeline over the subgroup's frames f, f + nsub, ...: the
+      // next frame's loads are issued before this one is summed
+      FrameChunks<FG, FU> fa;
+      load_frame<FG, FU, NT>(b0 + o0, l0, lane, fa);
+      while (true) {
+        const uint32_t fn = f + nsub;
+        meta(fn, o1, l1);
+        FrameChunks<FG, FU> fb;
+        load_frame<FG, FU, NT>(b0 + o1, l1, lane, fb); // (clamped: frame n - 1 past the end)
+        one(fa, f, b0 + o0, l0);
+        if (fn >= n) {
+          break;
+        }
+        f = fn;
+        o0 = o1;
+        l0 = l1;
+        fa = fb;
+      }
+    }
     if constexpr (FPS == 2) {
       meta(f + nsub, o1, l1);
     }
-    while (true) {
+    while (FPS != 3) {
       FrameChunks<FG, FU> fc0, fc1;
       load_frame<FG, FU, NT>(b0 + o0, l0, lane, fc0);
       if constexpr (FPS == 2) {
@@ -419,8 +439,10 @@ launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n
            hipStream_t stream)
 {
   const uint32_t block = fl.block ? fl.block : 256;
-  const uint32_t fps = (OP == OP_VALIDATE && G == 16 && U == 6 && fl.fps == 2) ? 2u : 1u;
-  const uint32_t per_block = block / G * fps;
+  const bool tuned = OP == OP_VALIDATE && G == 16 && U == 6;
+  const uint32_t fps = (tuned && (fl.fps == 2 || fl.fps == 3)) ? uint32_t(fl.fps) : 1u;
+  // fps 3 (pipelined): about four frames per subgroup
+  const uint32_t per_block = block / G * (fps == 1 ? 1u : fps == 2 ? 2u : 4u);
   uint64_t blocks = (uint64_t(n) + per_block - 1) / per_block;
   const uint64_t cap = fl.max_blocks ? fl.max_blocks : 65535;
   if (blocks > cap) {
@@ -430,6 +452,11 @@ launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n
   if constexpr (OP == OP_VALIDATE && G == 16 && U == 6) {
     if (fps == 2) {
       hipLaunchKernelGGL((frame_kernel<OP, G, U, NT, 2>), dim3(uint32_t(blocks)),
+                         dim3(block), 0, stream, base, offs, lens, n, flags, counters, fields);
+      return hipGetLastError();
+    }
+    if (fps == 3) {
+      hipLaunchKernelGGL((frame_kernel<OP, G, U, NT, 3>), dim3(uint32_t(blocks)),
                          dim3(block), 0, stream, base, offs, lens, n, flags, counters, fields);
       return hipGetLastError();
     }
@@ -648,7 +675,7 @@ tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
   fl.max_blocks = tuning->max_blocks;
   fl.block = uint32_t(tuning->block < 0 ? 0 : tuning->block);
   fl.nontemporal = tuning->nontemporal < 0 ? 1 : (tuning->nontemporal & 1);
-  fl.fps = tuning->sps == 2 ? 2 : 1;
+  fl.fps = (tuning->sps == 2 || tuning->sps == 3) ? tuning->sps : 1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipError_t e;
   if (op == 0) {
