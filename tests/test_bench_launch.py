@@ -57,6 +57,7 @@ def test_single_rank_dry_run_and_world_mismatch():
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(600)
 def test_self_launched_four_ranks_on_one_gpu():
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "4",
                         "--dist-backend", "gloo", "--one-device", "--steps", "32",
