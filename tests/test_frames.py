@@ -469,6 +469,38 @@ def test_gpu_generate_matches_oracle(oracle, shift):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("slot,shift", [(2048, 0), (64, 0), (2048, 64), (2048, 32), (128, 0)])
+def test_gpu_generate_in_slots_writes_whole_lines(oracle, slot, shift):
+    """In-place generation on frames in 64-byte-aligned slots (the receive/
+    transmit ring layout), where the kernel writes each frame's first 64-byte
+    line back whole with both fields patched: every byte of the arena equals
+    the oracle's (fields generated, nothing else changed, bytes between the
+    frames untouched), the fixture's short frames and runts included. The
+    32-byte shift keeps the slots off 64-byte alignment (2-byte stores)."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    rng = np.random.default_rng(slot + shift)
+    src = scramble_fields(fx, rng)
+    lens = fx["lengths"].copy()
+    keep = lens <= slot
+    offs_fx, lens = fx["offsets"][keep], lens[keep]
+    n = len(lens)
+    arena = rng.integers(0, 256, shift + n * slot + 64, dtype=np.uint8)
+    offs = (np.arange(n, dtype=np.uint64) * np.uint64(slot) + np.uint64(shift))
+    for i in range(n):
+        o, ln = int(offs_fx[i]), int(lens[i])
+        arena[int(offs[i]):int(offs[i]) + ln] = src[o:o + ln]
+    exp_arena, exp_flags = oracle.generate_frames(arena, offs, lens)
+    a, o, l = _dev(arena, offs.astype(np.int64), lens.view(np.int16))
+    fl = csum.generate_frames(a, o, l)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(fl.cpu().numpy(), exp_flags)
+    got = a.cpu().numpy()
+    assert np.array_equal(got, exp_arena), np.nonzero(got != exp_arena)[0][:10]
+
+
+@pytest.mark.gpu
 def test_gpu_generate_mutated_and_jumbo(oracle):
     import torch
     from tulips_amd import csum
