@@ -471,12 +471,10 @@ def test_gpu_generate_matches_oracle(oracle, shift):
 @pytest.mark.gpu
 @pytest.mark.parametrize("slot,shift", [(2048, 0), (64, 0), (2048, 64), (2048, 32), (128, 0)])
 def test_gpu_generate_in_slots_writes_whole_lines(oracle, slot, shift):
-    """In-place generation on frames in 64-byte-aligned slots (the receive/
-    transmit ring layout), where the kernel writes each frame's first 64-byte
-    line back whole with both fields patched: every byte of the arena equals
-    the oracle's (fields generated, nothing else changed, bytes between the
-    frames untouched), the fixture's short frames and runts included. The
-    32-byte shift keeps the slots off 64-byte alignment (2-byte stores)."""
+    """In-place generation on frames in slots (the receive/transmit ring
+    layout, 64-byte aligned or not): every byte of the arena equals the
+    oracle's (fields generated, nothing else changed, bytes between the
+    frames untouched), the fixture's short frames and runts included."""
     import torch
     from tulips_amd import csum
     fx = frames_fixture()

@@ -128,42 +128,18 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
         l4v = ~finish(p, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst, h.tcplen) & 0xffffu;
       }
     }
-    // In place, a frame whose first 64-byte line is its own (64-byte aligned
-    // start, at least 64 bytes: receive/transmit slots) gets that whole line
-    // written back by lanes 0..3 with both fields patched in, instead of two
-    // 2-byte stores: a partial-line write costs the memory side a
-    // read-modify-write of the line. Frames do not overlap (the contract), so
-    // no other writer touches those bytes.
-    const bool whole_line = OP == OP_GENERATE && FG >= 4 && (fa & 63u) == 0 && flen >= 64;
-    if constexpr (OP == OP_GENERATE) {
-      if (whole_line && lane < 4 && (h.ipv4 || do_l4)) {
-        u32x4 c = fc.v[0];  // chunk `lane` of the frame (h0 == 0)
-        if (lane == 1 && h.ipv4) {
-          c.z = (c.z & 0xffff0000u) | ipv;          // bytes 24..25
-        }
-        if (lane == 3 && do_l4) {
-          c.x = (c.x & 0x0000ffffu) | (l4v << 16);  // bytes 50..51
-        }
-        typedef __attribute__((address_space(1))) u32x4* gchunk_wptr;
-        *reinterpret_cast<gchunk_wptr>(fa + 16u * uint32_t(lane)) = c;
-      }
-    }
     if (lane == 0) {
       if (GENERATE) {
         uint32_t written = 0;
         if (h.ipv4) {
           if constexpr (OP == OP_GENERATE) {
-            if (!whole_line) {
-              store_field(fa + 24, ipv);
-            }
+            store_field(fa + 24, ipv);
           }
           written = ipv;
         }
         if (do_l4) {
           if constexpr (OP == OP_GENERATE) {
-            if (!whole_line) {
-              store_field(fa + 50, l4v);
-            }
+            store_field(fa + 50, l4v);
           }
           written |= l4v << 16;
         }
