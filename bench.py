@@ -69,6 +69,11 @@ def parse():
                         "(batches are independent; 16 = four per hardware queue, "
                         "GPU_MAX_HW_QUEUES being 4 on the box: the next launches are "
                         "already queued when one ends; profiles/probe_branches_r03.txt)")
+    p.add_argument("--start-delay-us", type=int, default=200,
+                   help="a one-wave GPU sleep queued before every timed region's start "
+                        "event (not timed), so the region starts on the GPU only once the "
+                        "host has submitted its graph: host launch latency is not counted "
+                        "as checksum time (0 = off)")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher and process-group check only (no GPU work): ranks form "
                         "the group, assert its size and rank 0 prints the JSON line "
@@ -130,6 +135,18 @@ def golden_digests():
         return {}
 
 
+START_DELAY_US = 200   # bench --start-delay-us
+
+
+def gate(stream):
+    """Queue the untimed start delay (tulips_csum_gpu_sleep) on `stream`."""
+    if START_DELAY_US > 0:
+        from tulips_amd import csum
+        rc = csum.lib.tulips_csum_gpu_sleep(START_DELAY_US, stream.cuda_stream)
+        if rc:
+            raise csum.CsumError(rc, "tulips_csum_gpu_sleep")
+
+
 class Timer:
     """Seconds per launch, from HIP events on the stream the kernels run on.
 
@@ -180,12 +197,14 @@ class Timer:
         if g is not None and replays > 1:
             times = []
             for _ in range(replays):
+                gate(self.stream)
                 a.record(self.stream)
                 g.replay()
                 b.record(self.stream)
                 b.synchronize()
                 times.append(a.elapsed_time(b) / 1e3 / reps)
             return float(np.median(times))
+        gate(self.stream)
         a.record(self.stream)
         if g is not None:
             g.replay()
@@ -217,7 +236,9 @@ def self_launch(args):
 
 
 def main():
+    global START_DELAY_US
     args = parse()
+    START_DELAY_US = max(0, args.start_delay_us)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
     import torch
@@ -317,6 +338,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_wall0 = time.perf_counter()
+    gate(stream)
     ev0.record(stream)
     if graph is not None:
         graph.replay()
@@ -366,6 +388,7 @@ def main():
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
+            gate(stream)
             ev0.record(stream)
             graph.replay()
             ev1.record(stream)
@@ -421,6 +444,9 @@ def main():
         "exchange": exchange,
         "multi_gpu": multi,
         "wall_s_timed": round(t_wall, 4),
+        "timing": "HIP events on the launch stream around the timed graph replay; a "
+                  f"{START_DELAY_US} us one-wave GPU sleep queued before the start event "
+                  "(untimed: the region starts when its launches are on the GPU)",
     }
     if replays:
         result["value_replays"] = {

@@ -91,6 +91,11 @@ int tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
 int tulips_csum_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                               uint64_t byte_off, void* stream);
 
+/* Occupy `stream` for `us` microseconds (<= 1 s) with one sleeping wave: a
+ * timed region queued behind it starts on the GPU only once the host has
+ * submitted it (bench.py), so host-side launch latency is not timed. */
+int tulips_csum_gpu_sleep(uint32_t us, void* stream);
+
 /* Plain 16-byte streaming read of [p, p + nbytes): the measured read
  * ceiling that the checksum kernel's HBM rate is compared against. */
 int tulips_csum_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,

@@ -41,9 +41,16 @@ def main():
                                         lens.data_ptr(), nf, None, stream.cuda_stream)
     torch.cuda.synchronize()
     alg = nf * flen
-    tunings = {"fps1": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=1),
-               "fps2": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=2),
-               "pipelined": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=3)}
+    if os.environ.get("GEOMS"):
+        # GEOMS="16x6 32x4 64x2": one frame per subgroup at each geometry
+        tunings = {}
+        for gu in os.environ["GEOMS"].split():
+            g, u = (int(x) for x in gu.split("x"))
+            tunings[gu] = csum.Tuning(group=g, unroll=u, nontemporal=1, sps=1)
+    else:
+        tunings = {"fps1": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=1),
+                   "fps2": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=2),
+                   "pipelined": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=3)}
 
     def fval(t):
         def f(i, st):

@@ -587,6 +587,32 @@ tulips_csum_batch_tuned(const uint8_t* base, const uint64_t* offsets,
                    mode, tuning, stream);
 }
 
+namespace {
+
+// One wave that returns after `ticks` of the 100 MHz realtime counter.
+__global__ __launch_bounds__(64) void
+gpu_sleep_kernel(uint64_t ticks)
+{
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+} // namespace
+
+int
+tulips_csum_gpu_sleep(uint32_t us, void* stream)
+{
+  if (us > 1000000u) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(gpu_sleep_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     uint64_t(us) * 100u);
+  return status_of(hipGetLastError());
+}
+
 int
 tulips_csum_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                           uint64_t byte_off, void* stream)
