@@ -39,6 +39,44 @@ masked_hsum(u32x4 v, int lo, int hi)
           uint64_t(v.w & byte_mask(lo, hi, 12)));
 }
 
+// The same sum for 0 <= lo, hi <= 16 (zero when lo >= hi) without 64-bit
+// shifts: a 16-bit byte mask, each dword's nibble of it spread to 0x00/0xff
+// bytes (nib * 0x204081 = nib + nib << 7 + nib << 14 + nib << 21 puts bit k
+// at bit 8k with no carries; masked, then x 255), so every row costs the same
+// few VALU ops whatever the range.
+__device__ __forceinline__ uint32_t
+nibble_bytes(uint32_t nib)
+{
+  const uint32_t t = (nib * 0x204081u) & 0x01010101u;
+  return (t << 8) - t;
+}
+
+// End-around-carry add: a sum modulo 2^32 - 1, which 65535 divides, so its
+// 16-bit fold equals that of the exact sum (a non-zero multiple of 65535
+// folds to 0xffff either way; only all-zero input gives 0). One register per
+// accumulator instead of a 64-bit pair.
+__device__ __forceinline__ uint32_t
+add_eac(uint32_t a, uint32_t b)
+{
+  const uint32_t s = a + b;
+  return s + uint32_t(s < b);
+}
+
+__device__ __forceinline__ uint32_t
+masked_hsum16(u32x4 v, int lo, int hi)
+{
+  const uint32_t bm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+  return add_eac(add_eac(v.x & nibble_bytes(bm & 15u), v.y & nibble_bytes((bm >> 4) & 15u)),
+                 add_eac(v.z & nibble_bytes((bm >> 8) & 15u), v.w & nibble_bytes(bm >> 12)));
+}
+
+// range_sum's row form: 1 = every row through masked_hsum16 (no divergent
+// branch), 0 = whole rows by hsum and boundary rows by masked_hsum, each
+// under its own branch.
+#ifndef FRAME_SELECT_ROWS
+#define FRAME_SELECT_ROWS 1
+#endif
+
 // This lane's LE dword sum of [sa, sa+len) over absolute 16-byte chunks
 // (G lanes, U unconditional clamped loads per lane per batch).
 template<int G, int U, bool NT>
@@ -153,6 +191,36 @@ gather_header(uintptr_t fa, uint32_t flen, int lane, int sub0)
     [&](int off) { return __shfl(hb, sub0 + off - 12, 64); }, flen);
 }
 
+// Frame-aligned dwords F[j] = frame bytes 4j .. 4j+3 for j = 3..12 from the
+// 20 dwords w[] of the five aligned chunks holding frame bytes 0..79 (the
+// frame starts h0 = 0..15 bytes into chunk 0). w[j + s] for s = h0 >> 2 is
+// selected in two bit steps by bit blends (one v_bfi each), then funnel-
+// shifted by h0 & 3. Written as a 4-way `s == 0 ? : s == 1 ? ...` chain the
+// compiler formed a switch and lowered it to exec-masked branches, ~70
+// instructions per header word (the subgroups of a wave differ in s); as
+// `?:` on array elements it selected the element's address and went through
+// scratch.
+__device__ __forceinline__ void
+funnel_words(const uint32_t (&w)[20], int h0, uint32_t (&F)[13])
+{
+  const uint32_t m1 = 0u - uint32_t((h0 >> 2) & 1), m2 = 0u - uint32_t((h0 >> 3) & 1);
+  const uint32_t r = uint32_t(h0 & 3);
+  uint32_t x[18], y[14];
+#pragma unroll
+  for (int k = 3; k < 18; ++k) {
+    x[k] = (w[k + 1] & m1) | (w[k] & ~m1);
+  }
+#pragma unroll
+  for (int k = 3; k < 14; ++k) {
+    y[k] = (x[k + 2] & m2) | (x[k] & ~m2);
+  }
+#pragma unroll
+  for (int j = 3; j < 13; ++j) {
+    F[j] = __builtin_amdgcn_alignbyte(y[j + 1], y[j], r);
+  }
+  F[0] = F[1] = F[2] = 0;
+}
+
 // One thread reads the header itself: the five aligned chunks holding frame
 // bytes 0..79 (clamped to the frame's last chunk, so nothing outside a chunk
 // with frame bytes is touched), funnel-shifted to frame-aligned dwords.
@@ -194,17 +262,8 @@ parse_header_chunks(const HeaderChunks& hc, uintptr_t fa, uint32_t flen)
     w[4 * c + 2] = hc.c[c].z;
     w[4 * c + 3] = hc.c[c].w;
   }
-  const int h0 = int(fa - lo), s = h0 >> 2;
-  const uint32_t r = uint32_t(h0 & 3);
   uint32_t D[13];
-#pragma unroll
-  for (int j = 3; j < 13; ++j) {
-    const uint32_t l = s == 0 ? w[j] : s == 1 ? w[j + 1] : s == 2 ? w[j + 2] : w[j + 3];
-    const uint32_t h =
-      s == 0 ? w[j + 1] : s == 1 ? w[j + 2] : s == 2 ? w[j + 3] : w[j + 4];
-    D[j] = __builtin_amdgcn_alignbyte(h, l, r);
-  }
-  D[0] = D[1] = D[2] = 0;
+  funnel_words(w, int(fa - lo), D);
   return parse_header<true>(
     [&](int k) -> uint32_t {
       return uint32_t(k) < flen ? (D[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
@@ -351,22 +410,33 @@ template<int G>
 __device__ __forceinline__ void
 header_words(const u32x4& v0, int h0, int sub0, uint32_t (&F)[13])
 {
-  uint32_t w[20];
-#pragma unroll
-  for (int c = 0; c < 5; ++c) {
-    w[4 * c + 0] = from_lane<G>(v0.x, c, sub0);
-    w[4 * c + 1] = from_lane<G>(v0.y, c, sub0);
-    w[4 * c + 2] = from_lane<G>(v0.z, c, sub0);
-    w[4 * c + 3] = from_lane<G>(v0.w, c, sub0);
-  }
-  const int s = h0 >> 2;
+  // Lane c (c < 4) funnel-shifts its own chunk and the next lane's (one DPP
+  // row_shl:1 per dword) to the frame-aligned words 4c .. 4c+3, then those
+  // ten words are broadcast: a few registers per lane instead of the whole
+  // 80-byte window replicated on every lane.
+  uint32_t e[8] = {v0.x, v0.y, v0.z, v0.w};
+  e[4] = uint32_t(__builtin_amdgcn_update_dpp(0, int(v0.x), 0x101, 0xf, 0xf, false));
+  e[5] = uint32_t(__builtin_amdgcn_update_dpp(0, int(v0.y), 0x101, 0xf, 0xf, false));
+  e[6] = uint32_t(__builtin_amdgcn_update_dpp(0, int(v0.z), 0x101, 0xf, 0xf, false));
+  e[7] = uint32_t(__builtin_amdgcn_update_dpp(0, int(v0.w), 0x101, 0xf, 0xf, false));
+  const uint32_t m1 = 0u - uint32_t((h0 >> 2) & 1), m2 = 0u - uint32_t((h0 >> 3) & 1);
   const uint32_t r = uint32_t(h0 & 3);
+  uint32_t t[7], q[5], o[4];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    t[k] = (e[k + 1] & m1) | (e[k] & ~m1);
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    q[k] = (t[k + 2] & m2) | (t[k] & ~m2);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    o[k] = __builtin_amdgcn_alignbyte(q[k + 1], q[k], r);
+  }
 #pragma unroll
   for (int j = 3; j < 13; ++j) {
-    const uint32_t lo = s == 0 ? w[j] : s == 1 ? w[j + 1] : s == 2 ? w[j + 2] : w[j + 3];
-    const uint32_t hi =
-      s == 0 ? w[j + 1] : s == 1 ? w[j + 2] : s == 2 ? w[j + 3] : w[j + 4];
-    F[j] = __builtin_amdgcn_alignbyte(hi, lo, r);
+    F[j] = from_lane<G>(o[j & 3], j >> 2, sub0);
   }
   F[0] = F[1] = F[2] = 0;
 }
@@ -399,14 +469,19 @@ range_sum(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
 {
   static_assert(UM >= 1 && UM <= U, "rows");
   uint64_t acc = 0;
+  uint32_t acc32 = 0;
 #pragma unroll
   for (int u = 0; u < UM; ++u) {
     const int b = 16 * (lane + u * G);
-    const int l = max(lo - b, 0), h = min(hi - b, 16);
-    if (l < h) {
+    const int l = min(max(lo - b, 0), 16), h = min(max(hi - b, 0), 16);
+    if constexpr (FRAME_SELECT_ROWS && U <= 8) {
+      // every row through one byte-mask select: no divergent branch
+      acc32 = add_eac(acc32, masked_hsum16(fc.v[u], l, h));
+    } else if (l < h) {
       acc += (l == 0 && h == 16) ? hsum(fc.v[u]) : masked_hsum(fc.v[u], l, h);
     }
   }
+  acc += acc32;
   if constexpr (UM == U) {
     constexpr int held = 16 * G * U;
     if (hi > held) {
