@@ -586,16 +586,18 @@ FRAME_GEOMETRIES = [(16, 4), (16, 6), (16, 8), (8, 8), (8, 16), (32, 4), (64, 2)
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("geo", FRAME_GEOMETRIES)
-@pytest.mark.parametrize("nt", [1, 0])
-def test_gpu_every_frame_geometry(oracle, geo, nt):
+@pytest.mark.parametrize("nt,shift", [(1, 5), (0, 5), (1, 14)])
+def test_gpu_every_frame_geometry(oracle, geo, nt, shift):
     """Validation and generation through tulips_csum_frames_tuned at every
-    geometry, on mutated fixture frames shifted to an odd base."""
+    geometry, on mutated fixture frames shifted to an odd base (5: header
+    words one dword and one byte into the chunk; 14: three dwords and two
+    bytes, the other select bit of the per-lane funnel shift)."""
     import torch
     from tulips_amd import csum
     fx = frames_fixture()
-    rng = np.random.default_rng(geo[0] * 100 + geo[1] + nt)
-    arena = np.concatenate([np.zeros(5, np.uint8), mutate(fx, rng, 1500)])
-    offs = fx["offsets"] + np.uint64(5)
+    rng = np.random.default_rng(geo[0] * 100 + geo[1] + nt + shift)
+    arena = np.concatenate([np.zeros(shift, np.uint8), mutate(fx, rng, 1500)])
+    offs = fx["offsets"] + np.uint64(shift)
     t = csum.Tuning(group=geo[0], unroll=geo[1], nontemporal=nt, block=256 if nt else 512)
     a, o, l = _dev(arena, offs.astype(np.int64), fx["lengths"].view(np.int16))
     fl = torch.empty(len(offs), dtype=torch.uint8, device="cuda:0")
