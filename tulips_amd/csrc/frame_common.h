@@ -39,44 +39,6 @@ masked_hsum(u32x4 v, int lo, int hi)
           uint64_t(v.w & byte_mask(lo, hi, 12)));
 }
 
-// The same sum for 0 <= lo, hi <= 16 (zero when lo >= hi) without 64-bit
-// shifts: a 16-bit byte mask, each dword's nibble of it spread to 0x00/0xff
-// bytes (nib * 0x204081 = nib + nib << 7 + nib << 14 + nib << 21 puts bit k
-// at bit 8k with no carries; masked, then x 255), so every row costs the same
-// few VALU ops whatever the range.
-__device__ __forceinline__ uint32_t
-nibble_bytes(uint32_t nib)
-{
-  const uint32_t t = (nib * 0x204081u) & 0x01010101u;
-  return (t << 8) - t;
-}
-
-// End-around-carry add: a sum modulo 2^32 - 1, which 65535 divides, so its
-// 16-bit fold equals that of the exact sum (a non-zero multiple of 65535
-// folds to 0xffff either way; only all-zero input gives 0). One register per
-// accumulator instead of a 64-bit pair.
-__device__ __forceinline__ uint32_t
-add_eac(uint32_t a, uint32_t b)
-{
-  const uint32_t s = a + b;
-  return s + uint32_t(s < b);
-}
-
-__device__ __forceinline__ uint32_t
-masked_hsum16(u32x4 v, int lo, int hi)
-{
-  const uint32_t bm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-  return add_eac(add_eac(v.x & nibble_bytes(bm & 15u), v.y & nibble_bytes((bm >> 4) & 15u)),
-                 add_eac(v.z & nibble_bytes((bm >> 8) & 15u), v.w & nibble_bytes(bm >> 12)));
-}
-
-// range_sum's row form: 1 = every row through masked_hsum16 (no divergent
-// branch), 0 = whole rows by hsum and boundary rows by masked_hsum, each
-// under its own branch.
-#ifndef FRAME_SELECT_ROWS
-#define FRAME_SELECT_ROWS 1
-#endif
-
 // This lane's LE dword sum of [sa, sa+len) over absolute 16-byte chunks
 // (G lanes, U unconditional clamped loads per lane per batch).
 template<int G, int U, bool NT>
@@ -469,19 +431,14 @@ range_sum(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
 {
   static_assert(UM >= 1 && UM <= U, "rows");
   uint64_t acc = 0;
-  uint32_t acc32 = 0;
 #pragma unroll
   for (int u = 0; u < UM; ++u) {
     const int b = 16 * (lane + u * G);
-    const int l = min(max(lo - b, 0), 16), h = min(max(hi - b, 0), 16);
-    if constexpr (FRAME_SELECT_ROWS && U <= 8) {
-      // every row through one byte-mask select: no divergent branch
-      acc32 = add_eac(acc32, masked_hsum16(fc.v[u], l, h));
-    } else if (l < h) {
+    const int l = max(lo - b, 0), h = min(hi - b, 16);
+    if (l < h) {
       acc += (l == 0 && h == 16) ? hsum(fc.v[u]) : masked_hsum(fc.v[u], l, h);
     }
   }
-  acc += acc32;
   if constexpr (UM == U) {
     constexpr int held = 16 * G * U;
     if (hi > held) {

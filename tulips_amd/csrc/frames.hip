@@ -61,32 +61,11 @@ using namespace frame;
 // Minimum waves per SIMD the register allocator must leave room for
 // (0 = no bound). Generation: 94 -> 80 VGPRs, 5 -> 6 waves/SIMD, no spill;
 // 3 alternations on one box (profiles/ab_r01.txt): 21.2-22.0 -> 20.8-21.4 us
-// serial, 19.4-19.7 -> 18.7-19.0 us on 4 branches. The generation bound
-// applies to the default geometry and smaller (U <= 6): at 16 x 8 and
-// 8 x 8/16 it spilled 12-364 B per lane, so those keep their natural register
-// counts. Validation at the default geometry: FRAME_VAL_WAVES (round 4: the
-// header words funnel-shifted per lane instead of a replicated 80-byte
-// window, the next frame's metadata no longer prefetched).
-#ifndef TULIPS_FRAME_VAL_WAVES
-#define TULIPS_FRAME_VAL_WAVES 0
-#endif
-constexpr int FRAME_VAL_WAVES = TULIPS_FRAME_VAL_WAVES, FRAME_GEN_WAVES = 6,
-              FRAME_FPS2_WAVES = 0;
-
-// Dynamic LDS per frame workgroup (0): a diagnostic build knob that caps
-// workgroups per CU, for occupancy sweeps (tools/ab_libs.sh).
-#ifndef TULIPS_FRAME_LDS_PAD
-#define TULIPS_FRAME_LDS_PAD 0
-#endif
-
-constexpr int
-frame_waves(int op, int fg, int fu, int fps)
-{
-  return fps >= 2                ? FRAME_FPS2_WAVES
-         : op != 0 && fu <= 6    ? FRAME_GEN_WAVES
-         : op == 0 && fg * fu == 96 ? FRAME_VAL_WAVES
-                                 : 0;
-}
+// serial, 19.4-19.7 -> 18.7-19.0 us on 4 branches. Validation at 7 waves
+// spills 12 B and is slower. The generation bound applies to the default
+// geometry and smaller (U <= 6): at 16 x 8 and 8 x 8/16 it spilled 12-364 B
+// per lane, so those keep their natural register counts.
+constexpr int FRAME_VAL_WAVES = 0, FRAME_GEN_WAVES = 6, FRAME_FPS2_WAVES = 0;
 
 // OP: 0 = validate (flags, counters), 1 = generate in place (the two
 // checksum fields patched into the frame; `fields` optionally gets a copy),
@@ -98,23 +77,19 @@ enum { OP_VALIDATE = 0, OP_GENERATE = 1, OP_FIELDS = 2 };
 // twice the bytes in flight at the same instruction count per byte, and the
 // grid is half as many workgroups.
 template<int OP, int FG, int FU, bool NT, int FPS = 1>
-__global__ __launch_bounds__(FPS == 3 ? 256 : 1024, frame_waves(OP, FG, FU, FPS)) void
+__global__ __launch_bounds__(FPS == 3 ? 256 : 1024, FPS >= 2 ? FRAME_FPS2_WAVES : OP != OP_VALIDATE && FU <= 6 ? FRAME_GEN_WAVES : FRAME_VAL_WAVES) void
 frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
              const uint16_t* __restrict__ lens, uint32_t n,
              uint8_t* __restrict__ flags, uint32_t* __restrict__ shards,
              uint32_t* __restrict__ fields)
 {
   constexpr bool GENERATE = OP != OP_VALIDATE;
-  // threadIdx.x as (wave, lane): the wave index lives in an SGPR and the
-  // lane is recomputed (v_mbcnt) where needed, so no VGPR holds the thread
-  // id through the frame's work (at 8 waves per SIMD it was the one spill)
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane64 = int(__lane_id());
+  const int lane64 = threadIdx.x & 63;
   const int lane = lane64 & (FG - 1);
   const int sub0 = lane64 - lane; // first lane of this subgroup
   const uint32_t per_block = blockDim.x / FG;
   const uint32_t nsub = gridDim.x * per_block;
-  uint32_t f = xcd_block(blockIdx.x, gridDim.x) * per_block + (wave * 64u + uint32_t(lane64)) / FG;
+  uint32_t f = xcd_block(blockIdx.x, gridDim.x) * per_block + threadIdx.x / FG;
   // counters: per-block totals in LDS, then one atomic per non-zero counter
   // per block into one of CNT_SHARDS line-sized shards (finalised by
   // frame_counters_finalize). Adding every frame to the caller's 4 words
@@ -123,19 +98,15 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
   __shared__ uint32_t s_cnt[4];
   const bool count = !GENERATE && shards != nullptr;   // grid-uniform
   if (count) {
-    if (wave == 0 && lane64 < 4) {
-      s_cnt[lane64] = 0;
+    if (threadIdx.x < 4) {
+      s_cnt[threadIdx.x] = 0;
     }
     __syncthreads();
   }
-  // frame `g` (length flen) from its loaded chunks. The frame's address is
-  // fc.a0 + fc.h0; only generation rebuilds it (validation needs its parity
-  // alone, h0 & 1: both checksum ranges start at even offsets), so no second
-  // copy of it stays live through the frame's work.
-  auto one = [&](const FrameChunks<FG, FU>& fc, uint32_t g, uint32_t flen) {
+  // frame `g` at address fa (length flen) from its loaded chunks
+  auto one = [&](const FrameChunks<FG, FU>& fc, uint32_t g, uintptr_t fa, uint32_t flen) {
     const Header h = frame_header(fc, flen, sub0);
     const int h0 = fc.h0;
-    const bool odd = (h0 & 1) != 0;
     const bool do_l4 = h.tcp && !h.trunc && (!GENERATE || h.tcplen >= 18u);
     const uint32_t ip_part = sub_sum<FG>(
       fold64(h.ipv4 ? range_sum<FG, FU, NT, 1>(fc, lane, h0 + 14, h0 + 34) : 0));
@@ -145,17 +116,16 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
     // generation: both field values, on every lane (the sums and the header
     // are subgroup-uniform)
     uint32_t ipv = 0, l4v = 0;
-    [[maybe_unused]] const uintptr_t fa = fc.a0 + uintptr_t(h0);
     if constexpr (GENERATE) {
       if (h.ipv4) {
         const uint32_t p =
           fold32(ip_part) + (0xffffu - field_contrib(fa + 24, h.ipck0, h.ipck1));
-        ipv = ~finish(p, odd, MODE_INET, 0, 0, 0, 20) & 0xffffu;
+        ipv = ~finish(p, ((fa + 14) & 1) != 0, MODE_INET, 0, 0, 0, 20) & 0xffffu;
       }
       if (do_l4) {
         const uint32_t p =
           fold32(l4_part) + (0xffffu - field_contrib(fa + 50, h.tcpck0, h.tcpck1));
-        l4v = ~finish(p, odd, MODE_TCP, 0, h.src, h.dst, h.tcplen) & 0xffffu;
+        l4v = ~finish(p, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src, h.dst, h.tcplen) & 0xffffu;
       }
     }
     if (lane == 0) {
@@ -184,9 +154,9 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
           flags[g] = uint8_t(frame_flags(h, h.ipv4, do_l4));
         }
       } else {
-        const bool ip_ok = h.ipv4 && finish(ip_part, odd, MODE_INET, 0,
+        const bool ip_ok = h.ipv4 && finish(ip_part, ((fa + 14) & 1) != 0, MODE_INET, 0,
                                             0, 0, 20) == 0xffffu;
-        const bool l4_ok = do_l4 && finish(l4_part, odd, MODE_TCP, 0,
+        const bool l4_ok = do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0,
                                            h.src, h.dst, h.tcplen) == 0xffffu;
         if (flags) {
           flags[g] = uint8_t(frame_flags(h, ip_ok, l4_ok));
@@ -230,7 +200,7 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
         meta(fn, o1, l1);
         FrameChunks<FG, FU> fb;
         load_frame<FG, FU, NT>(b0 + o1, l1, lane, fb); // (clamped: frame n - 1 past the end)
-        one(fa, f, l0);
+        one(fa, f, b0 + o0, l0);
         if (fn >= n) {
           break;
         }
@@ -250,30 +220,16 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
         load_frame<FG, FU, NT>(b0 + o1, l1, lane, fc1);
       }
       const uint32_t fn = f + uint32_t(FPS) * nsub;
-      if constexpr (FPS == 1) {
-        // The next frame's offset and length are fetched after this frame
-        // is done, not behind its loads: at the default grid (one frame per
-        // subgroup) there is no next frame, and the three registers a
-        // prefetch holds across the frame's work are what keeps validation
-        // from 8 waves per SIMD.
-        one(fc0, f, l0);
-        if (fn >= n) {
-          break;
-        }
-        f = fn;
-        meta(f, o0, l0);
-        continue;
-      }
       uint64_t p0, p1 = 0;
       uint32_t q0, q1 = 0;
       meta(fn, p0, q0);
       if constexpr (FPS == 2) {
         meta(fn + nsub, p1, q1);
       }
-      one(fc0, f, l0);
+      one(fc0, f, b0 + o0, l0);
       if constexpr (FPS == 2) {
         if (f + nsub < n) {
-          one(fc1, f + nsub, l1);
+          one(fc1, f + nsub, b0 + o1, l1);
         }
       }
       if (fn >= n) {
@@ -288,14 +244,10 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
   }
   if (count) {
     __syncthreads();
-    // lanes 0..3 of wave 0 (mbcnt_lo with a base of 1 counts lane + 1 for the
-    // low half: a value the compiler cannot share with the lane id above, so
-    // that one is not kept live through the loop just for this)
-    const uint32_t l = __builtin_amdgcn_mbcnt_lo(~0u, 1u) - 1u;
-    if (wave == 0 && l < 4) {
-      const uint32_t v = s_cnt[l];
+    if (threadIdx.x < 4) {
+      const uint32_t v = s_cnt[threadIdx.x];
       if (v) {
-        atomicAdd(shards + CNT_LINE * (blockIdx.x % CNT_SHARDS) + l, v);
+        atomicAdd(shards + CNT_LINE * (blockIdx.x % CNT_SHARDS) + threadIdx.x, v);
       }
     }
   }
@@ -518,8 +470,7 @@ launch_one(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n
     }
   }
   hipLaunchKernelGGL((frame_kernel<OP, G, U, NT>), dim3(uint32_t(blocks)),
-                     dim3(block), TULIPS_FRAME_LDS_PAD, stream, base, offs, lens, n, flags,
-                     counters, fields);
+                     dim3(block), 0, stream, base, offs, lens, n, flags, counters, fields);
   return hipGetLastError();
 }
 
