@@ -64,11 +64,12 @@ def parse():
                    help="torch.distributed backend for N>1 (nccl = RCCL)")
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal only: every rank uses cuda:0 (use with gloo)")
-    p.add_argument("--streams", type=int, default=16,
+    p.add_argument("--streams", type=int, default=0,
                    help="independent graph branches the timed steps round-robin over "
-                        "(batches are independent; 16 = four per hardware queue, "
-                        "GPU_MAX_HW_QUEUES being 4 on the box: the next launches are "
-                        "already queued when one ends; profiles/probe_branches_r03.txt)")
+                        "(batches are independent). 0 = by step count (branches_for): "
+                        "2 below 128 steps, else 16 (four per hardware queue, "
+                        "GPU_MAX_HW_QUEUES being 4 on the box; "
+                        "profiles/probe_branches_r03.txt, profiles/probe_graph_k_r04.txt)")
     p.add_argument("--start-delay-us", type=int, default=200,
                    help="a one-wave GPU sleep queued before every timed region's start "
                         "event (not timed), so the region starts on the GPU only once the "
@@ -136,6 +137,19 @@ def golden_digests():
 
 
 START_DELAY_US = 200   # bench --start-delay-us
+
+
+def branches_for(steps):
+    """Graph branches for a K-step timed replay. A replay costs about a + b K
+    (tools/probe_graph_k.py, profiles/probe_graph_k_r04.txt, one box; b from
+    K = 4..64): 1 branch a = 10 us, b = 15.6 us; 2 branches a = 24 us,
+    b = 13.47 us; 4-16 branches a = 39-40 us, b = 13.36-13.41 us. The
+    per-replay cost grows with the hardware queues the graph spans, so 2
+    branches win the short replays: the driver's K = 20 at 6,224-6,268 GiB/s
+    against 5,860-5,955 with 16 (3 alternations, profiles/ab_branches_k_r04.txt),
+    and K = 64 at 6,608 against 6,538. Long chains on 2 branches lose pace
+    (K = 1,024: 6,368 against 6,743 with 16), so 16 from K = 128 on."""
+    return 2 if steps < 128 else 16
 
 
 def gate(stream):
@@ -239,6 +253,8 @@ def main():
     global START_DELAY_US
     args = parse()
     START_DELAY_US = max(0, args.start_delay_us)
+    if args.streams <= 0:
+        args.streams = branches_for(args.steps)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
     import torch

@@ -2,8 +2,8 @@
 """Replay time of the headline graph against its step count K: the bench's
 F1500 launches (batch i % 16) captured as one graph on B branches, each K
 timed over REPS replays (median) behind the bench's 200 us start gate, for
-each B in $BRANCHES (default 16 and 1). A straight-line fit t = a + b K separates the per-replay
-cost a from the per-step cost b. Measurement only; prints JSON lines."""
+each B in $BRANCHES (default 16 and 1). A straight-line fit t = a + b K
+separates the per-replay cost a from the per-step cost b. Measurement only; prints JSON lines."""
 import json
 import os
 import sys
@@ -21,6 +21,7 @@ from tulips_amd import csum  # noqa: E402
 def main():
     ks = [int(x) for x in os.environ.get("KS", "1 2 4 8 16 20 32 64 128").split()]
     reps = int(os.environ.get("REPS", "7"))
+    mainb = os.environ.get("MAIN_BRANCH", "0") == "1"
     dev = torch.device("cuda", 0)
     lib = csum.lib
     SEG, NSEG, NB = bench.SEG, bench.NSEG, bench.NBATCH
@@ -48,12 +49,17 @@ def main():
             used = min(nbr, k)
             with torch.cuda.graph(g):
                 m = torch.cuda.current_stream()
-                for j in range(used):
-                    side[j].wait_stream(m)
+                # MAIN_BRANCH=1: branch 0 is the capture stream itself (its
+                # launches need no fork edge), the others fork from it
+                br = ([m] + side[:used - 1]) if mainb else side[:used]
+                for sd in br:
+                    if sd is not m:
+                        sd.wait_stream(m)
                 for i in range(k):
-                    launch(i, side[i % used].cuda_stream)
-                for j in range(used):
-                    m.wait_stream(side[j])
+                    launch(i, br[i % used].cuda_stream)
+                for sd in br:
+                    if sd is not m:
+                        m.wait_stream(sd)
             g.replay()
             torch.cuda.synchronize()
             ts = []
@@ -68,7 +74,7 @@ def main():
                 ts.append(a.elapsed_time(b) * 1e3)
             t = float(np.median(ts))
             rows.append((k, t))
-            print(json.dumps({"branches": nbr, "steps": k, "us_median": round(t, 2),
+            print(json.dumps({"branches": nbr, "main_branch": mainb, "steps": k, "us_median": round(t, 2),
                               "us_min": round(min(ts), 2),
                               "gib_s": round(k * bb / (t * 1e-6) / bench.GIB, 1)}), flush=True)
             del g
