@@ -26,6 +26,9 @@ step pytest_gpu 600 python -u -m pytest tests -q -m gpu -x -p no:cacheprovider -
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 400 python bench.py
 tail -1 $OUT/bench.log > $OUT/bench.json
+# the driver's form (python3 bench.py --gpus 1 --steps 20 --warmup 5)
+step bench_driver 400 python bench.py --gpus 1 --steps 20 --warmup 5
+tail -1 $OUT/bench_driver.log > $OUT/bench_driver.json
 step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python bench.py --no-cpu-baseline
 python tools/trace_bursts.py $OUT/stats/run_kernel_trace.csv --all > $OUT/bursts_all.jsonl
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
