@@ -137,6 +137,10 @@ def golden_digests():
 
 
 START_DELAY_US = 200   # bench --start-delay-us
+# launches in the serial chain the roofline's per-launch duration comes from,
+# whatever --steps is: one graph replay costs ~10 us on top of its launches
+# (profiles/probe_graph_k_r04.txt), 0.5 us per launch over the driver's 20
+SERIAL_LAUNCHES = 256
 
 
 def branches_for(steps):
@@ -341,7 +345,7 @@ def main():
             b = i % NBATCH
             fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
                   optr + b * NSEG * 2, NSEG, 0, st)
-        serial_s = Timer(torch, stream)(serial, min(args.steps, 512))
+        serial_s = Timer(torch, stream)(serial, SERIAL_LAUNCHES)
 
     # ---- timed region ------------------------------------------------------
     ev0 = torch.cuda.Event(enable_timing=True)
