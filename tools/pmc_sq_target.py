@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A short workload for instruction-counter passes (run under rocprofv3
---pmc): 16 launches each of the F1500 checksum, frame validation and the
-ZIPF arena kernel, bench.py's shapes. Measurement only."""
+--pmc): 16 launches each of the F1500 checksum, frame validation, the
+frames' slot-read pattern and the ZIPF arena kernel, bench.py's shapes. Measurement only."""
 import os
 import sys
 
@@ -45,6 +45,12 @@ def main():
         b = i % 2
         lib.tulips_csum_validate_frames(ar.data_ptr() + b * nf * slot, offs.data_ptr(),
                                         lens.data_ptr(), nf, flags.data_ptr() + b * nf, None, st)
+    # the frames' own load pattern without their work (the read ceiling)
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    for i in range(16):
+        b = i % 2
+        lib.tulips_csum_stream_read_slots(ar.data_ptr() + b * nf * slot, slot, flen, nf,
+                                          sink.data_ptr(), st)
     lz = bench.zipf_lengths(NSEG)
     zo = np.zeros(NSEG, dtype=np.uint64)
     np.cumsum(lz[:-1], dtype=np.uint64, out=zo[1:])
