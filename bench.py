@@ -543,6 +543,7 @@ def dry_run(args, world, rank):
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": n,
                           "dry_run": True, "parity": "not run (dry run)",
+                          "config": {"streams": args.streams},
                           "dist": {"world_size": n, "backend": "gloo" if n > 1 else None,
                                    "ranks": ranks}}), flush=True)
 

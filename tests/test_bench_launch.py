@@ -75,3 +75,19 @@ def test_self_launched_four_ranks_on_one_gpu():
     assert mg["library_scatter_from_gpu0"]["kernel_only"]["parity"] == "ok"
     for leg in ("exchange_overlapped", "scatter_from_gpu0", "zipf_byte_balanced"):
         assert mg[leg].get("parity") == "ok", (leg, mg[leg])
+
+
+def test_branch_count_follows_step_count():
+    """The timed graph's branches by step count (bench.branches_for): 2 for
+    short replays (the driver's 20 steps), 16 for long ones; an explicit
+    --streams wins (profiles/probe_graph_k_r04.txt, ab_branches_k_r04.txt)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.branches_for(20) == 2 and bench.branches_for(127) == 2
+    assert bench.branches_for(128) == 16 and bench.branches_for(1024) == 16
+    for argv, want in ((["--steps", "20"], 2), (["--steps", "1024"], 16),
+                       (["--steps", "20", "--streams", "8"], 8)):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"] + argv,
+                           capture_output=True, text=True, env=_env(), timeout=300, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert _json_lines(r.stdout)[0]["config"]["streams"] == want, argv
