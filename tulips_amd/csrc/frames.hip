@@ -97,12 +97,6 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
   // launch instead of 18 (tools/probe_counters.py).
   __shared__ uint32_t s_cnt[4];
   const bool count = !GENERATE && shards != nullptr;   // grid-uniform
-  // flags: with one frame per subgroup (the default grid) a workgroup's
-  // frames are contiguous, and their flag bytes meet in LDS and leave in one
-  // store instruction of the first wave; the other waves end with no store
-  // outstanding (grid-uniform)
-  __shared__ uint8_t s_flags[1024 / 8];
-  const bool gather = !GENERATE && flags != nullptr && nsub >= n;
   if (count) {
     if (threadIdx.x < 4) {
       s_cnt[threadIdx.x] = 0;
@@ -164,9 +158,7 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
                                             0, 0, 20) == 0xffffu;
         const bool l4_ok = do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0,
                                            h.src, h.dst, h.tcplen) == 0xffffu;
-        if (gather) {
-          s_flags[threadIdx.x / FG] = uint8_t(frame_flags(h, ip_ok, l4_ok));
-        } else if (flags) {
+        if (flags) {
           flags[g] = uint8_t(frame_flags(h, ip_ok, l4_ok));
         }
         if (count) {
@@ -250,16 +242,8 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
       l1 = q1;
     }
   }
-  if (count || gather) {
-    __syncthreads();
-  }
-  if (gather) {
-    const uint32_t g = xcd_block(blockIdx.x, gridDim.x) * per_block + threadIdx.x;
-    if (threadIdx.x < per_block && g < n) {
-      flags[g] = s_flags[threadIdx.x];
-    }
-  }
   if (count) {
+    __syncthreads();
     if (threadIdx.x < 4) {
       const uint32_t v = s_cnt[threadIdx.x];
       if (v) {
