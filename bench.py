@@ -139,7 +139,10 @@ def golden_digests():
 START_DELAY_US = 200   # bench --start-delay-us
 # launches in the serial chain the roofline's per-launch duration comes from,
 # whatever --steps is: one graph replay costs ~10 us on top of its launches
-# (profiles/probe_graph_k_r04.txt), 0.5 us per launch over the driver's 20
+# (profiles/probe_graph_k_r04.txt), 0.5 us per launch over the driver's 20.
+# The median of 5 timed replays of that chain is taken: right after a short
+# run (the driver's 20 steps) the first replay measured 16.5-16.6 us per
+# launch where the steady state, and rocprofv3's serial bursts, give 16.1-16.3
 SERIAL_LAUNCHES = 256
 
 
@@ -345,7 +348,7 @@ def main():
             b = i % NBATCH
             fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
                   optr + b * NSEG * 2, NSEG, 0, st)
-        serial_s = Timer(torch, stream)(serial, SERIAL_LAUNCHES)
+        serial_s = Timer(torch, stream)(serial, SERIAL_LAUNCHES, replays=5)
 
     # ---- timed region ------------------------------------------------------
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -1074,6 +1077,42 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                    "parity_checked": "outputs poisoned before the timed replays; the "
                                      f"{NB9} batch digests after them vs the reference's"}
     del a9, o9
+
+    # SURVEY.md §8d's aligned-stride layouts: F1500 at stride 2048 (the OFED
+    # RX slots, include/tulips/transport/ofed/Device.h:25) and F9000 at
+    # stride 9216, each as 4 copies of the golden arena at different addresses
+    # (537 MB and 2.42 GB rotated: HBM-resident); rate over the segment bytes
+    # only (65,536 x L), every copy's digest vs the reference's
+    ex["aligned_strides"] = {}
+    for name, L, S in (("F1500s2048", 1500, 2048), ("F9000s9216", 9000, 9216)):
+        ncp = 4
+        cb = NSEG * S
+        ac = torch.empty(ncp * cb + 256, dtype=torch.uint8, device=dev)
+        csum.fill_splitmix(ac, cb)
+        for c in range(1, ncp):
+            ac[c * cb:(c + 1) * cb].copy_(ac[:cb])
+        oc = torch.empty(ncp * NSEG, dtype=torch.uint16, device=dev)
+        pc = poisoner(oc)
+
+        def fs(i, st, ac=ac, oc=oc, L=L, S=S, cb=cb, ncp=ncp):
+            c = i % ncp
+            fixed(ac.data_ptr() + c * cb, S, L, None, None, None,
+                  oc.data_ptr() + c * NSEG * 2, NSEG, 0, st)
+        for i in range(ncp):
+            fs(i, sh)
+        want = gold.get(name, {}).get("fnv1a64")
+        ts = timer(fs, 40, poison=pc)
+        okc = want is not None and row_digests(oc, ncp, NSEG) == [want] * ncp
+        tps = pipe_times(timer, fs, 40, poison=pc)
+        okc = okc and row_digests(oc, ncp, NSEG) == [want] * ncp
+        alg = NSEG * L
+        ex["aligned_strides"][name] = {
+            "avg_launch_us": round(ts * 1e6, 2), "GiBps": round(alg / ts / GIB, 1),
+            "frac_of_peak": round(alg / ts / 1e9 / HBM_PEAK_GBS, 4),
+            "pipeline": pipe_entry(alg, tps),
+            "rotation": f"{ncp} copies ({ncp * cb / 1e9:.2f} GB)",
+            "parity": "ok" if okc else "MISMATCH"}
+        del ac, oc
 
     # ZIPF (configs[3]): 24 copies with the same lengths, different bytes
     # (1.05 GB rotated: HBM-resident), the 8-copy rotation (350 MB) beside it
