@@ -40,7 +40,7 @@ def _gpu():
 
 
 def d(a, dtype=None):
-    t = torch.from_numpy(np.ascontiguousarray(a))
+    t = torch.from_numpy(np.array(a, copy=True, order="C"))  # (writable: from_numpy warns on read-only arrays)
     if dtype is not None:
         t = t.view(dtype)
     return t.to(DEV)
