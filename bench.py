@@ -256,8 +256,17 @@ def self_launch(args):
     return subprocess.run(cmd, env=env).returncode
 
 
+def progress(stage):
+    """One stderr line per bench stage (stdout carries only the JSON line):
+    where a long run is, and where it stopped if it dies."""
+    print(f"[bench {time.strftime('%H:%M:%S')} pid {os.getpid()}] {stage}", file=sys.stderr,
+          flush=True)
+
+
 def main():
     global START_DELAY_US
+    import faulthandler
+    faulthandler.enable(file=sys.stderr, all_threads=True)
     args = parse()
     START_DELAY_US = max(0, args.start_delay_us)
     if args.streams <= 0:
@@ -291,6 +300,7 @@ def main():
     sh = stream.cuda_stream
     lib = csum.lib
 
+    progress("data")
     # ---- data: M8x1500 shard <rank>, 16 batches of 65,536 x 1500 B -------------
     shard = shard_for(rank, world)
     batch_bytes = NSEG * SEG
@@ -340,6 +350,7 @@ def main():
         graph.replay()
         torch.cuda.synchronize()
 
+    progress("timed region")
     # ---- timed region ------------------------------------------------------
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -507,9 +518,11 @@ def main():
     }
 
     if world == 1 and rank == 0 and not args.no_extras:
+        progress("extras")
         result["extras"] = extras(torch, csum, dev, stream, arena, batch_bytes)
 
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        progress("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(arena, batch_bytes, args.cpu_seconds)
 
     if world > 1:
@@ -1084,6 +1097,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     # stride 9216, each as 4 copies of the golden arena at different addresses
     # (537 MB and 2.42 GB rotated: HBM-resident); rate over the segment bytes
     # only (65,536 x L), every copy's digest vs the reference's
+    progress("extras: aligned strides")
     ex["aligned_strides"] = {}
     for name, L, S in (("F1500s2048", 1500, 2048), ("F9000s9216", 9000, 9216)):
         ncp = 4
@@ -1119,6 +1133,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     # (1.05 GB rotated: HBM-resident), the 8-copy rotation (350 MB) beside it
     # as `mall_assisted`. Copy c = stream bytes [c * zb, (c + 1) * zb); copy 0
     # is the golden ZIPF arena.
+    progress("extras: ZIPF")
     lens = zipf_lengths(NSEG)
     offs = np.zeros(NSEG, dtype=np.uint64)
     np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
@@ -1232,6 +1247,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                       "parity": "ok" if ok_any else "MISMATCH"}}
     del az, oz
 
+    progress("extras: end-to-end host path")
     # end-to-end host path: F1500 batch from host memory, results back to host
     host = arena[:batch_bytes].cpu().numpy()
     pinned = torch.from_numpy(host.copy()).pin_memory()
@@ -1251,12 +1267,16 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                          "parity": "ok" if fnv1a_u16(out) == gold.get("F1500", {}).get(
                              "fnv1a64") else "MISMATCH"}
     ex["e2e_host_F1500"] = e2e
+    progress("extras: multi-device host context")
     try:  # every visible device: on a multi-GPU node a failure here must not cost the line
         ex["mctx_host_F1500"] = mctx_leg(torch, csum, pinned, hoffs, hlens, batch_bytes, gold)
     except Exception as e:  # noqa: BLE001
         ex["mctx_host_F1500"] = {"error": repr(e)}
+    progress("extras: burst latency")
     ex["burst_latency_host"] = burst_latency(torch, csum)
+    progress("extras: beside the resident server")
     ex["F1500_beside_resident_server"] = beside_server(torch, csum, timer, arena, batch_bytes)
+    progress("extras: frames, segmentation, RSS")
     ex.update(frame_extras(torch, csum, dev, timer))
     return ex
 
