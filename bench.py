@@ -64,6 +64,7 @@ def parse():
                    help="torch.distributed backend for N>1 (nccl = RCCL)")
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal only: every rank uses cuda:0 (use with gloo)")
+    p.add_argument("--extras-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--streams", type=int, default=0,
                    help="independent graph branches the timed steps round-robin over "
                         "(batches are independent). 0 = by step count (branches_for): "
@@ -269,6 +270,8 @@ def main():
     faulthandler.enable(file=sys.stderr, all_threads=True)
     args = parse()
     START_DELAY_US = max(0, args.start_delay_us)
+    if args.extras_child:
+        return extras_child()
     if args.streams <= 0:
         args.streams = branches_for(args.steps)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -518,8 +521,8 @@ def main():
     }
 
     if world == 1 and rank == 0 and not args.no_extras:
-        progress("extras")
-        result["extras"] = extras(torch, csum, dev, stream, arena, batch_bytes)
+        progress("extras (child process)")
+        result["extras"] = extras_in_child()
 
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         progress("cpu baseline")
@@ -530,6 +533,38 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def extras_in_child():
+    """The side measurements, run in a child process after the timed region
+    (no exec: a fresh interpreter started by subprocess, which touches the GPU
+    on its own), so that a failure there - an exception or a crash - costs
+    the extras, never the headline line. Returns the child's extras dict, or
+    an error entry with its exit status."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--extras-child"],
+                       stdout=subprocess.PIPE, text=True, cwd=ROOT)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode == 0 and lines:
+        return json.loads(lines[-1])["extras"]
+    return {"error": f"extras process exited with status {r.returncode}",
+            "stdout_tail": r.stdout[-500:]}
+
+
+def extras_child():
+    """bench.py --extras-child: rank 0's data (M8x1500 shard 0, the same
+    bytes as the headline's) and every side measurement; one JSON line."""
+    import torch
+    from tulips_amd import csum
+    from tulips_amd.shard import shard_for
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    shard = shard_for(0, 1)
+    arena = torch.empty(shard.nbytes + 256, dtype=torch.uint8, device=dev)
+    csum.fill_splitmix(arena, shard.nbytes, seed=DATA_SEED, byte_off=shard.byte_offset)
+    torch.cuda.synchronize()
+    ex = extras(torch, csum, dev, torch.cuda.current_stream(), arena, NSEG * SEG)
+    print(json.dumps({"extras": ex}), flush=True)
 
 
 def check_world(dist, args):
