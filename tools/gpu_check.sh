@@ -29,10 +29,21 @@ tail -1 $OUT/bench.log > $OUT/bench.json
 # the driver's form (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 step bench_driver 400 python bench.py --gpus 1 --steps 20 --warmup 5
 tail -1 $OUT/bench_driver.log > $OUT/bench_driver.json
-step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python bench.py --no-cpu-baseline
+# bench.py runs its side measurements in a child process, which rocprofv3
+# does not follow: the headline (--no-extras) and the extras child
+# (--extras-child) are profiled as two programs and their CSVs merged
+step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_h -o run -- python bench.py --no-cpu-baseline --no-extras
+step stats_x 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_x -o run -- python bench.py --extras-child
+step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_h -o run -- python bench.py --no-cpu-baseline --no-extras --steps 64 --warmup 16
+step pmc_fetch_x 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_x -o run -- python bench.py --extras-child
+step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_h -o run -- python bench.py --no-cpu-baseline --no-extras --steps 64 --warmup 16
+step pmc_write_x 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_x -o run -- python bench.py --extras-child
+python tools/merge_csv.py $OUT/stats/run_kernel_trace.csv $OUT/stats_h/run_kernel_trace.csv $OUT/stats_x/run_kernel_trace.csv
+python tools/merge_csv.py $OUT/stats/run_kernel_stats.csv $OUT/stats_h/run_kernel_stats.csv $OUT/stats_x/run_kernel_stats.csv
+python tools/merge_csv.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_fetch_h/run_counter_collection.csv $OUT/pmc_fetch_x/run_counter_collection.csv
+python tools/merge_csv.py $OUT/pmc_write/run_counter_collection.csv $OUT/pmc_write_h/run_counter_collection.csv $OUT/pmc_write_x/run_counter_collection.csv
+rm -rf $OUT/stats_h $OUT/stats_x $OUT/pmc_fetch_h $OUT/pmc_fetch_x $OUT/pmc_write_h $OUT/pmc_write_x
 python tools/trace_bursts.py $OUT/stats/run_kernel_trace.csv --all > $OUT/bursts_all.jsonl
-step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
-step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --no-cpu-baseline --steps 64 --warmup 16
 # (no launcher: bench.py starts torch.distributed.run itself, as under the
 # driver's `python bench.py --gpus 8`)
 step rehearsal_w8 600 python bench.py --gpus 8 --dist-backend gloo --one-device --steps 64 --warmup 16 --no-cpu-baseline

@@ -116,7 +116,20 @@ def main():
                       "separate rocprofv3 --pmc passes, mean over dispatches",
             "source": f"{prof} ({tag})",
         }
-    with open(os.path.join(outdir, "pmc_traffic.json"), "w") as f:
+    # bench.py reads pmc_traffic.json for every workload's `traffic`: a run
+    # that covered fewer workloads than the committed file (e.g. a trace that
+    # missed the extras child) goes beside it instead of replacing it
+    dst = os.path.join(outdir, "pmc_traffic.json")
+    try:
+        with open(dst) as f:
+            have = set(json.load(f))
+    except (OSError, ValueError):
+        have = set()
+    if not have <= set(res):
+        dst = os.path.join(outdir, f"pmc_traffic_{tag}_partial.json")
+        print(f"pmc_traffic: {sorted(have - set(res))} missing from this run; wrote {dst}",
+              file=sys.stderr)
+    with open(dst, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
 
