@@ -41,7 +41,11 @@ def main():
                                         lens.data_ptr(), nf, None, stream.cuda_stream)
     torch.cuda.synchronize()
     alg = nf * flen
-    if os.environ.get("GEOMS"):
+    if os.environ.get("BLOCKS"):
+        # BLOCKS="256 512 1024": the default geometry at each workgroup size
+        tunings = {f"b{b}": csum.Tuning(group=16, unroll=6, nontemporal=1, sps=1, block=int(b))
+                   for b in os.environ["BLOCKS"].split()}
+    elif os.environ.get("GEOMS"):
         # GEOMS="16x6 32x4 64x2": one frame per subgroup at each geometry
         tunings = {}
         for gu in os.environ["GEOMS"].split():
