@@ -78,7 +78,7 @@ int tulips_csum_batch_arena_tuned(const uint8_t* base, uint64_t arena_bytes,
  * fields array). Uses tuning->group (lanes per frame, 0 = 16), unroll
  * (chunks in flight per lane, 0 = 6; supported pairs 16x4, 16x6, 16x8, 8x8,
  * 8x16, 32x4, 64x2), nontemporal (bit 0: nt loads, -1 = on), max_blocks and
- * block; sps 2 = two frames per subgroup in flight, 3 = a software pipeline
+ * block (64, 128, 256, 512 or 1024 threads; 0 = 256); sps 2 = two frames per subgroup in flight, 3 = a software pipeline
  * (the next frame's loads issued before this one is summed, ~4 frames per
  * subgroup) (validation at 16 x 6 only; otherwise ignored); kind is ignored. */
 int tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,

@@ -188,7 +188,7 @@ def test_gpu_counters_repeat_streams_and_grid_caps():
     for c in cnts:
         np.testing.assert_array_equal(c.cpu().numpy().view(np.uint32), exp)
     st = torch.cuda.current_stream().cuda_stream
-    for cap, blk in ((1, 256), (3, 1024), (40, 256), (0, 512)):
+    for cap, blk in ((1, 256), (3, 1024), (40, 256), (0, 512), (0, 64), (5, 128)):
         t = csum.Tuning(group=16, unroll=6, nontemporal=1, max_blocks=cap, block=blk)
         c = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
         assert csum.lib.tulips_csum_frames_tuned(0, a.data_ptr(), o.data_ptr(), l.data_ptr(),

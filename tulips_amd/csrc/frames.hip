@@ -509,7 +509,8 @@ frame_geometry_ok(int group, int unroll, uint32_t block)
   const bool geo = (g == 16 && (u == 4 || u == 6 || u == 8)) ||
                    (g == 8 && (u == 8 || u == 16)) || (g == 32 && u == 4) ||
                    (g == 64 && u == 2);
-  return geo && (block == 0 || block == 256 || block == 512 || block == 1024);
+  return geo && (block == 0 || block == 64 || block == 128 || block == 256 || block == 512 ||
+                 block == 1024);
 }
 
 hipError_t
