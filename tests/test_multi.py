@@ -133,7 +133,7 @@ def test_mctx_device_arguments_without_gpu():
 
 def _dev(a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+    return torch.from_numpy(np.array(a, copy=True, order="C")).to("cuda:0")
 
 
 @pytest.mark.gpu

@@ -94,7 +94,7 @@ def test_gpu_batch_matches_reference_fixture():
     from tulips_amd import csum
     fx = rss_fixture()
     dev = "cuda:0"
-    t = {k: torch.from_numpy(np.ascontiguousarray(fx[k])).to(dev)
+    t = {k: torch.from_numpy(np.array(fx[k], copy=True, order="C")).to(dev)
          for k in ("saddr", "daddr", "sport", "dport")}
     for i, name, key in keys(fx):
         for init, tag in ((0, "init0"), (0xFFFFFFFF, "initff")):

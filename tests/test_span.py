@@ -39,7 +39,7 @@ def _gpu():
 
 
 def d(a):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return torch.from_numpy(np.array(a, copy=True, order="C")).to(DEV)
 
 
 def u16(t):
