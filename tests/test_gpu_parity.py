@@ -414,3 +414,28 @@ def test_empty_batch_is_noop():
     lens = torch.empty(0, dtype=torch.uint16, device=DEV)
     out = tulips_amd.batch(arena, offs, lens)
     assert out.numel() == 0
+
+
+@pytest.mark.parametrize("length,group,unroll", [(1500, 32, 4), (9000, 64, 12), (64, 16, 2)])
+def test_fixed_small_workgroups(length, group, unroll):
+    """Fixed-length batches also take 64- and 128-thread workgroups (one
+    subgroup per segment, nothing shared in the workgroup): results equal the
+    default launch's, odd counts and a capped grid included."""
+    n = 4099
+    arena = torch.empty(n * length + 64, dtype=torch.uint8, device=DEV)
+    csum.fill_splitmix(arena, n * length, seed=0x5EED + length)
+    st = torch.cuda.current_stream().cuda_stream
+    want = torch.empty(n, dtype=torch.int16, device=DEV)   # u16 results, viewed signed
+    assert csum.lib.tulips_csum_batch_fixed(arena.data_ptr(), length, length, None, None, None,
+                                            want.data_ptr(), n, 0, st) == 0
+    for block, cap in ((64, 0), (128, 0), (64, 5), (128, 9)):
+        got = torch.full((n,), 0xA5A5 - 0x10000, dtype=torch.int16, device=DEV)   # poison
+        t = csum.Tuning(group=group, unroll=unroll, nontemporal=1, block=block, max_blocks=cap)
+        assert csum.lib.tulips_csum_batch_fixed_tuned(arena.data_ptr(), length, length, None,
+                                                      None, None, got.data_ptr(), n, 0, t,
+                                                      st) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), (block, cap)
+    bad = csum.Tuning(group=group, unroll=unroll, block=96)
+    assert csum.lib.tulips_csum_batch_fixed_tuned(arena.data_ptr(), length, length, None, None,
+                                                  None, want.data_ptr(), n, 0, bad, st) == 1

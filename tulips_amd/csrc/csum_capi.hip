@@ -320,6 +320,14 @@ block_ok(int block)
   return block == 256 || block == 512 || block == 1024;
 }
 
+// fixed-length segments (one subgroup per segment, no per-workgroup state)
+// also take 64- and 128-thread workgroups
+inline bool
+fixed_block_ok(int block)
+{
+  return block == 64 || block == 128 || block_ok(block);
+}
+
 int
 batch_fixed(const uint8_t* base, uint64_t stride, uint32_t length,
             const uint16_t* seeds, const uint32_t* src, const uint32_t* dst,
@@ -343,7 +351,7 @@ batch_fixed(const uint8_t* base, uint64_t stride, uint32_t length,
   a.mode = mode;
   apply_tuning(a, default_tuning(length, false), tuning);
   if (!geometry_ok(a.kind, a.group, a.unroll, a.spw, false) ||
-      !block_ok(a.block)) {
+      !fixed_block_ok(a.block)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   return status_of(
