@@ -43,7 +43,8 @@ typedef struct tulips_csum_tuning
   int32_t unroll;      /* see kind */
   int32_t nontemporal; /* bit 0: nt loads, bit 1: nt result stores; -1 = default */
   uint32_t max_blocks; /* grid cap; 0 = default */
-  int32_t block;       /* threads per workgroup: 256, 512 or 1024; 0 = default */
+  int32_t block;       /* threads per workgroup: 256, 512 or 1024 (fixed-length
+                          batches and frames also 64 or 128); 0 = default */
   int32_t sps;         /* PACKED: 2 = double-buffered windows (the only
                           form; 0 = default) */
 } tulips_csum_tuning;
