@@ -169,6 +169,36 @@ def gate(stream):
             raise csum.CsumError(rc, "tulips_csum_gpu_sleep")
 
 
+class CheckedLib:
+    """csum.lib with every status-returning call checked: a non-zero status
+    raises CsumError at the call, which also ends a graph capture in progress
+    (torch.cuda.graph's exit), so no capture can silently miss a launch."""
+
+    def __init__(self, csum):
+        self._csum = csum
+
+    def __getattr__(self, name):
+        f, err = getattr(self._csum.lib, name), self._csum.CsumError
+
+        def call(*a):
+            rc = f(*a)
+            if rc:
+                raise err(rc, name)
+            return rc
+        setattr(self, name, call)
+        return call
+
+
+_CHECKED = None
+
+
+def checked_lib(csum):
+    global _CHECKED
+    if _CHECKED is None:
+        _CHECKED = CheckedLib(csum)
+    return _CHECKED
+
+
 class Timer:
     """Seconds per launch, from HIP events on the stream the kernels run on.
 
@@ -181,6 +211,14 @@ class Timer:
 
     def __init__(self, torch, stream, graph=True):
         self.torch, self.stream, self.graph = torch, stream, graph
+        # the capture stream and the branch streams, made once and reused by
+        # every call (not drawn again from torch's recycled pool per call)
+        self._streams = []
+
+    def streams(self, k):
+        while len(self._streams) < k:
+            self._streams.append(self.torch.cuda.Stream())
+        return self._streams[:k]
 
     def __call__(self, fn, reps, branches=1, replays=1, poison=None):
         """branches > 1: launch i goes to graph branch i % branches (independent
@@ -195,11 +233,10 @@ class Timer:
         g = None
         if self.graph:
             g = t.cuda.CUDAGraph()
-            cap = t.cuda.Stream()
-            side = [t.cuda.Stream() for _ in range(branches)] if branches > 1 else []
-            # one eager launch on every stream the capture uses first:
-            # per-stream library state (the segmentation workspace) is made
-            # outside the capture
+            ss = self.streams(1 + (branches if branches > 1 else 0))
+            cap, side = ss[0], ss[1:]
+            # one eager launch on every stream the capture uses first (the
+            # library needs none: a captured call gets state of its own)
             for j, sd in enumerate([cap] + side):
                 fn(j, sd.cuda_stream)
             t.cuda.synchronize()
@@ -289,6 +326,8 @@ def main():
     from tulips_amd import csum
     from tulips_amd.shard import (all_ranks_ok, gather_results, gather_strings,
                                   max_over_ranks, shard_for)
+    # a native crash names its frames before faulthandler prints Python's
+    checked_lib(csum).tulips_csum_debug_crash_backtrace(1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # control-plane reductions live on the GPU under RCCL, on the CPU under gloo
@@ -301,7 +340,7 @@ def main():
         check_world(dist, args)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
-    lib = csum.lib
+    lib = checked_lib(csum)
 
     progress("data")
     # ---- data: M8x1500 shard <rank>, 16 batches of 65,536 x 1500 B -------------
@@ -557,6 +596,7 @@ def extras_child():
     import torch
     from tulips_amd import csum
     from tulips_amd.shard import shard_for
+    checked_lib(csum).tulips_csum_debug_crash_backtrace(1)
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     shard = shard_for(0, 1)
@@ -735,7 +775,7 @@ def single_process_kernel_only(torch, csum, devs, rotations=4):
     timed replays, then its shard digest vs the reference's."""
     from tulips_amd.shard import SHARD_SEGMENTS
     gold = golden_digests().get("M8x1500", {}).get("shards", [])
-    fixed = csum.lib.tulips_csum_batch_fixed
+    fixed = checked_lib(csum).tulips_csum_batch_fixed
     per = []
     for k, d in enumerate(devs):
         dv = torch.device("cuda", d)
@@ -797,7 +837,7 @@ def exchange_overlapped(torch, dist, csum, cdev, stream, arena, rank, world, arg
     overwriting its buffer. Timed end to end (max over ranks) beside the same
     rotations without the gathers."""
     from tulips_amd.shard import max_over_ranks
-    fixed = csum.lib.tulips_csum_batch_fixed
+    fixed = checked_lib(csum).tulips_csum_batch_fixed
     batch_bytes = NSEG * SEG
     base = arena.data_ptr()
     bufs = [torch.empty(NBATCH * NSEG, dtype=torch.uint16, device=arena.device)
@@ -880,7 +920,7 @@ def scatter_leg(torch, dist, csum, dev, cdev, arena, outs, rank, world):
     out = torch.empty(NSEG, dtype=torch.uint16, device=dev)
     chunks = [arena[b * batch_bytes:(b + 1) * batch_bytes] for b in range(world)] \
         if rank == 0 else None
-    fixed = csum.lib.tulips_csum_batch_fixed
+    fixed = checked_lib(csum).tulips_csum_batch_fixed
     best = None
     for _ in range(3):
         dist.barrier()
@@ -928,7 +968,7 @@ def zipf_sharded_leg(torch, dist, csum, dev, cdev, stream, rank, world):
     doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
     dlens = torch.from_numpy(ll.view(np.int16).copy()).to(dev)
     out = torch.empty(max(1, len(ll)), dtype=torch.uint16, device=dev)
-    batch = csum.lib.tulips_csum_batch_arena   # a shard is a packed, in-order arena
+    batch = checked_lib(csum).tulips_csum_batch_arena   # a shard is a packed, in-order arena
 
     def fz(i, st):
         rc = batch(az.data_ptr(), bs.nbytes, doffs.data_ptr(), dlens.data_ptr(), None, None,
@@ -1029,7 +1069,7 @@ def read_traffic(workload):
 def extras(torch, csum, dev, stream, arena, batch_bytes):
     timer = Timer(torch, stream)
     sh = stream.cuda_stream
-    lib = csum.lib
+    lib = checked_lib(csum)
     ex = {}
 
     # plain streaming read of the whole 1.57 GB shard: the measured ceiling
@@ -1453,7 +1493,7 @@ def beside_server(torch, csum, timer, arena, batch_bytes):
     polling the mailbox, tulips_csum_ctx_set_lowlat) costs a bulk kernel
     sharing the GPU: the F1500 serial launch rate with the server idle-
     polling beside it, against the same launches without it."""
-    fixed = csum.lib.tulips_csum_batch_fixed
+    fixed = checked_lib(csum).tulips_csum_batch_fixed
     outs = torch.empty(NBATCH * NSEG, dtype=torch.uint16, device=arena.device)
 
     def f(i, st):
@@ -1491,7 +1531,7 @@ def frame_extras(torch, csum, dev, timer):
     """§8f rows: frame validation / generation (receive and send sides),
     segmentation offload and the Toeplitz RSS batch, each on device-resident
     synthetic frames with its own parity check."""
-    lib = csum.lib
+    lib = checked_lib(csum)
     ex = {}
     # 8 bursts x 65,536 TCP frames of 1514 B (MTU 1500) in 2 KiB receive
     # slots (the OFED RX layout, include/tulips/transport/ofed/Device.h:25),

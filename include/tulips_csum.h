@@ -391,9 +391,11 @@ int tulips_csum_generate_fields(const uint8_t* base, const uint64_t* offsets,
  *
  * The library keeps a device workspace per (device, stream), made or grown
  * on a call that needs more room; calls on one stream run in order, calls
- * on different streams may overlap. A call inside a stream capture must not
- * need that (returns InvalidArgument): make one call of the same or larger
- * size on that stream before capturing.
+ * on different streams may overlap. The calls a stream capture records on a
+ * stream share a workspace made for that capture and owned by the graph
+ * (freed by tulips_csum_release_stream), so no warm-up call is needed, later
+ * direct calls never free it under the graph, and a replay may overlap
+ * direct calls on the capture stream.
  */
 int tulips_csum_segment_frames(const uint8_t* in_base,
                                const uint64_t* in_offsets,
@@ -402,6 +404,37 @@ int tulips_csum_segment_frames(const uint8_t* in_base,
                                uint64_t out_stride, uint32_t out_capacity,
                                uint16_t* out_lengths, uint32_t* out_first,
                                void* stream);
+
+/*
+ * Segmentation with the caller's plan (the reference's split: the host knows
+ * each super-frame's header length, stack::utils::headerLength,
+ * src/stack/Utils.cpp:67-84, and the MSS it posts with the TSO request,
+ * src/transport/ofed/Device.cpp:688-700). `first` (device, n + 1 entries)
+ * is what tulips_csum_segment_frames would write to out_first: first[i] =
+ * the segments of frames 0..i-1 (ceil(P / mss) for a super-frame as above,
+ * 1 for any other frame; tulips_csum_segment_plan_host computes it from host
+ * headers). The segment kernel then runs alone, with no counting prologue;
+ * outputs, limits and semantics as tulips_csum_segment_frames (segments
+ * j >= min(first[n], out_capacity) are not written). A segment whose frame's
+ * header disagrees with the plan (more segments planned than its payload
+ * makes) gets length 0; reads never leave the frames, writes never leave
+ * out_capacity slots. Needs no per-stream state (capturable as is).
+ */
+int tulips_csum_segment_frames_planned(const uint8_t* in_base, const uint64_t* in_offsets,
+                                       const uint16_t* in_lengths, uint32_t n, uint32_t mss,
+                                       const uint32_t* first, uint8_t* out_base,
+                                       uint64_t out_stride, uint32_t out_capacity,
+                                       uint16_t* out_lengths, void* stream);
+
+/*
+ * The plan for tulips_csum_segment_frames_planned from host-resident frames
+ * (each frame's first 48 bytes are read): first (host, n + 1 entries)
+ * receives the exclusive prefix of the per-frame segment counts, first[n]
+ * the total. The same rule as the device prologue.
+ */
+int tulips_csum_segment_plan_host(const uint8_t* base, const uint64_t* offsets,
+                                  const uint16_t* lengths, uint32_t n, uint32_t mss,
+                                  uint32_t* first);
 
 /* Host-resident frames through a context's pinned pipeline; `flags` is a
  * host array of n bytes, `counters` (may be NULL) a host uint32[4]. */
@@ -481,10 +514,12 @@ int tulips_csum_segment_frames_host(tulips_csum_ctx* ctx, const uint8_t* in_base
  * from its first launch to its last, so host threads sharing a stream (e.g.
  * the NULL stream) never interleave their launch sequences. A counting call
  * captured in a HIP graph gets counter shards of its own, owned by the graph
- * (up to 16 per stream; count once on the stream before capturing).
+ * (up to 16 per stream; count once on the stream before capturing); a
+ * captured segmentation call, a workspace of its own.
  *
  * tulips_csum_release_stream waits for `stream` and frees everything the
- * library holds for it, including shards owned by graphs captured on it
+ * library holds for it, including shards and workspaces owned by graphs
+ * captured on it
  * (destroy those graphs first). Call it before hipStreamDestroy; it must not
  * race calls on the same stream. Later calls on the stream start afresh.
  * tulips_csum_ctx_destroy releases the context's own streams.

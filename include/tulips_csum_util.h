@@ -97,6 +97,15 @@ int tulips_csum_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
  * submitted it (bench.py), so host-side launch latency is not timed. */
 int tulips_csum_gpu_sleep(uint32_t us, void* stream);
 
+/* Diagnostics: on SIGSEGV, SIGBUS, SIGILL, SIGFPE or SIGABRT write the
+ * signal, the faulting address and the native call stack
+ * (backtrace_symbols_fd) to stderr, then hand the signal to the handler that
+ * was installed before (e.g. Python's faulthandler, which adds the
+ * interpreter's stack) and let it terminate the process as it would have.
+ * enable = 0 restores the previous handlers. Not for use in a product
+ * process that installs its own signal handlers after this call. */
+int tulips_csum_debug_crash_backtrace(int enable);
+
 /* Plain 16-byte streaming read of [p, p + nbytes): the measured read
  * ceiling that the checksum kernel's HBM rate is compared against. */
 int tulips_csum_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,

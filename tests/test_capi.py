@@ -238,6 +238,26 @@ def test_missing_library_fails_loudly(tmp_path):
     assert "no CPU fallback" in r.stderr
 
 
+def test_crash_backtrace_names_native_frames(tmp_path):
+    """tulips_csum_debug_crash_backtrace (bench.py installs it): a SIGSEGV in
+    native code prints the native call stack, then Python's faulthandler (the
+    handler installed before) prints the interpreter's, and the process still
+    dies of the signal."""
+    import subprocess
+    import sys
+    prog = ("import faulthandler, sys, ctypes; faulthandler.enable(); "
+            f"sys.path.insert(0, {ROOT!r}); from tulips_amd import csum; "
+            "assert csum.lib.tulips_csum_debug_crash_backtrace(1) == 0; "
+            "assert csum.lib.tulips_csum_debug_crash_backtrace(2) == 1; "
+            "ctypes.string_at(16)")
+    r = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True,
+                       timeout=300, cwd=tmp_path)
+    assert r.returncode == -11, r.stderr[-2000:]
+    assert "tulips_csum: fatal signal 11 (SIGSEGV) at address 0x0000000000000010" in r.stderr
+    assert "native stack:" in r.stderr
+    assert "Fatal Python error: Segmentation fault" in r.stderr   # faulthandler, chained
+
+
 READELF = "/opt/rocm/llvm/bin/llvm-readelf"
 
 

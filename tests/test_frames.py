@@ -656,6 +656,10 @@ def test_frames_tuned_rejects_bad_geometry():
     assert f(2, A, A, A, 4, A, None, csum.Tuning(group=16, unroll=4), None) == 1
     assert f(0, A, A, A, 4, A, None, csum.Tuning(group=16, unroll=4, block=384), None) == 1
     assert f(0, A, A, A, 0, None, None, csum.Tuning(group=16, unroll=6), None) == 0
+    # the pipelined form (sps 3) is built for at most 256 threads per block
+    for blk in (512, 1024):
+        assert f(0, A, A, A, 4, A, None,
+                 csum.Tuning(group=16, unroll=6, sps=3, block=blk), None) == 1
 
 
 @pytest.mark.gpu

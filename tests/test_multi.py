@@ -460,6 +460,44 @@ def test_mctx_rss_device_matches_host_and_reference(oracle, key_i, init, ndev, l
 
 
 @pytest.mark.gpu
+def test_mctx_rss_device_alternating_streams(oracle):
+    """Calls of one context alternated between two streams with no host
+    synchronisation in between: each call overwrites the
+    router's workspace (perm, rflags) that the previous call's last kernel,
+    on the other stream, may still be reading; the context orders them
+    (RouteWs::done), so every call's flags and counters equal the oracle's."""
+    import torch
+    from test_frames import counters_of
+    from test_rss import rss_fixture
+    from tulips_amd import csum
+    fx = rss_fixture()
+    key = fx["key_0"].tobytes()
+    batches = []
+    for seed, nf in ((71, None), (72, None)):
+        rng = np.random.default_rng(seed)
+        arena, offs, lens, _ = _rss_frames(oracle, rng, fx)
+        if seed == 72:     # a different batch: fewer frames, different routing
+            keep = len(offs) // 3
+            offs, lens = offs[:keep], lens[:keep]
+        batches.append((_dev(arena), _dev(offs.view(np.int64)), _dev(lens.view(np.int16)),
+                        oracle.validate_frames(arena, offs, lens)))
+    table = (np.arange(128) * 3 % 4).astype(np.uint16)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    with csum.MultiContext([0] * 4, chunk_bytes=1 << 20) as m:
+        out = []
+        for rep in range(6):
+            a, o, ln, exp = batches[rep % 2]
+            cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
+            fl, _ = m.validate_frames_rss_device(a, o, ln, key, table, counters=cnt,
+                                                 stream=streams[rep % 2])
+            out.append((fl, cnt, exp))
+        torch.cuda.synchronize()
+    for fl, cnt, exp in out:
+        np.testing.assert_array_equal(fl.cpu().numpy(), exp)
+        np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32), counters_of(exp))
+
+
+@pytest.mark.gpu
 def test_mctx_rss_device_fixture_mutations_and_scale(oracle):
     """The reference-flagged frames.npz (mutated: bad checksums, fragments,
     runts, truncation, zero-length frames) routed over 3 devices, and a

@@ -1,10 +1,13 @@
 // csum_capi.hip — the C ABI of include/tulips_csum.h and
 // include/tulips_csum_util.h, plus the host scalar drop-ins that keep the
 // reference's C++ symbols (tulips::stack::utils::checksum & co.).
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <signal.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <memory>
@@ -698,3 +701,91 @@ tulips_csum_version(void)
 }
 
 } // extern "C"
+
+// ---------------------------------------------------------------------------
+// tulips_csum_debug_crash_backtrace: native stack on a fatal signal.
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int CRASH_SIGNALS[] = { SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT };
+struct sigaction g_crash_prev[sizeof(CRASH_SIGNALS) / sizeof(int)];
+bool g_crash_on = false;
+
+// async-signal-safe: write(2) of a decimal / hex number
+void
+crash_write(const char* s)
+{
+  (void)!write(2, s, strlen(s));
+}
+
+void
+crash_hex(uintptr_t v)
+{
+  char b[19] = "0x";
+  for (int i = 0; i < 16; ++i) {
+    const unsigned d = unsigned(v >> (60 - 4 * i)) & 15u;
+    b[2 + i] = char(d < 10 ? '0' + d : 'a' + d - 10);
+  }
+  b[18] = 0;
+  crash_write(b);
+}
+
+void
+crash_handler(int sig, siginfo_t* si, void* uc)
+{
+  crash_write("\ntulips_csum: fatal signal ");
+  char num[4] = { char('0' + (sig / 10) % 10), char('0' + sig % 10), 0, 0 };
+  crash_write(num);
+  crash_write(" (");
+  crash_write(sig == SIGSEGV ? "SIGSEGV" : sig == SIGBUS ? "SIGBUS" : sig == SIGILL ? "SIGILL"
+              : sig == SIGFPE ? "SIGFPE" : "SIGABRT");
+  crash_write(") at address ");
+  crash_hex(si ? reinterpret_cast<uintptr_t>(si->si_addr) : 0);
+  crash_write("; native stack:\n");
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, n, 2);
+  // the earlier handler takes it from here: restored, then the signal is
+  // delivered again (a faulting instruction re-executes on return; abort()
+  // raises SIGABRT a second time once its handler returns)
+  for (size_t k = 0; k < sizeof(CRASH_SIGNALS) / sizeof(int); ++k) {
+    if (CRASH_SIGNALS[k] == sig) {
+      (void)sigaction(sig, &g_crash_prev[k], nullptr);
+    }
+  }
+  if (si && si->si_code <= 0) {
+    (void)raise(sig); // sent by kill/raise: nothing re-executes
+  }
+  (void)uc;
+}
+
+} // namespace
+
+extern "C" int
+tulips_csum_debug_crash_backtrace(int enable)
+{
+  if (enable != 0 && enable != 1) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (enable && !g_crash_on) {
+    void* warm[2];
+    (void)backtrace(warm, 2); // loads the unwinder now, not inside the handler
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = crash_handler;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    for (size_t k = 0; k < sizeof(CRASH_SIGNALS) / sizeof(int); ++k) {
+      if (sigaction(CRASH_SIGNALS[k], &sa, &g_crash_prev[k]) != 0) {
+        return TULIPS_STATUS_HARDWARE_ERROR;
+      }
+    }
+    g_crash_on = true;
+  } else if (!enable && g_crash_on) {
+    for (size_t k = 0; k < sizeof(CRASH_SIGNALS) / sizeof(int); ++k) {
+      (void)sigaction(CRASH_SIGNALS[k], &g_crash_prev[k], nullptr);
+    }
+    g_crash_on = false;
+  }
+  return TULIPS_STATUS_OK;
+}

@@ -178,6 +178,12 @@ struct RouteWs
   uint64_t* totals_host = nullptr; // page-locked copy
   uint16_t* table = nullptr;
   uint8_t* packed = nullptr;      // frames bound for other devices, by device
+  // the last call's final kernel (launch_rss_home reads perm and rflags) done,
+  // recorded on that call's stream: the next call, on any stream, waits for
+  // it before it overwrites the workspace
+  hipEvent_t done = nullptr;
+  int done_device = -1;
+  bool done_used = false;
 };
 
 } // namespace
@@ -330,6 +336,10 @@ tulips_csum_mctx_destroy(tulips_csum_mctx* m)
                      (void*)r.table, (void*)r.packed }) {
       (void)hipFree(p);
     }
+  }
+  if (r.done) {
+    (void)hipSetDevice(r.done_device);
+    (void)hipEventDestroy(r.done);
   }
   (void)hipHostFree(r.totals_host);
   (void)hipSetDevice(prev);
@@ -1366,11 +1376,27 @@ validate_rss_device(tulips_csum_mctx* m, int sdev, const uint8_t* base, const ui
   RouteWs& r = m->route;
   TCS_TRY(hipSetDevice(sdev));
   // the previous call's devices may still read the workspace (its packed
-  // runs, offsets, lengths) when that call was ordered on another stream
+  // runs, offsets, lengths), and its last kernel (perm, rflags), when that
+  // call was ordered on another stream
   for (auto& d : m->slots) {
     if (d.used) {
       TCS_TRY(hipStreamWaitEvent(st, d.done, 0));
     }
+  }
+  if (r.done_used) {
+    TCS_TRY(hipStreamWaitEvent(st, r.done, 0));
+  }
+  if (r.done && r.done_device != sdev) {
+    TCS_TRY(hipSetDevice(r.done_device));
+    TCS_TRY(hipEventSynchronize(r.done));
+    (void)hipEventDestroy(r.done);
+    r.done = nullptr;
+    r.done_used = false;
+    TCS_TRY(hipSetDevice(sdev));
+  }
+  if (!r.done) {
+    TCS_TRY(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+    r.done_device = sdev;
   }
   TCS_TRY(hipMemcpyAsync(r.table, table, 2ull * table_len, hipMemcpyHostToDevice, st));
   uint16_t* dev_of = device_of ? device_of : r.dev_of;
@@ -1474,6 +1500,9 @@ validate_rss_device(tulips_csum_mctx* m, int sdev, const uint8_t* base, const ui
   }
   if (e == hipSuccess) {
     e = launch_rss_home(r.perm, r.rflags, n, flags, counters, st);
+  }
+  if (e == hipSuccess && (e = hipEventRecord(r.done, st)) == hipSuccess) {
+    r.done_used = true;
   }
   if (e != hipSuccess) {
     for (auto& d : m->slots) { // drain before reporting (the caller may free)

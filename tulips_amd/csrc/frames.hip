@@ -671,6 +671,11 @@ tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
                                      uint32_t(tuning->block < 0 ? 0 : tuning->block))) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
+  // the pipelined validation kernel (sps 3) is compiled for at most 256
+  // threads per block (__launch_bounds__ of frame_kernel<..., 3>)
+  if (op == 0 && tuning->sps == 3 && tuning->block > 256) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
   if (n == 0 && !(op == 0 && counters)) {
     return TULIPS_STATUS_OK;
   }

@@ -33,8 +33,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
+#include <vector>
 
 #include "../../include/tulips_csum.h"
 #include "csum_common.h"
@@ -323,24 +325,32 @@ realign(u32x4& d, uint32_t sel)
 // SU chunks per lane is SU + 1 loads. The header chunks 0..6 come from one more load per lane and
 // are parsed through cross-lane shuffles; everything is issued before the
 // first use (the prologue's descriptor is all the addresses need).
-template<int G, int SU>
+//
+// KNOWN: F.si comes from the prologue's descriptor. Otherwise (the planned
+// entry, no prologue) it is derived here from the header this subgroup loads
+// anyway, once the loads are in flight (they need only the frame's address,
+// length and k); a k past the frame's segment count (a caller's plan that
+// disagrees with the header) writes length 0 and nothing else.
+template<int G, int SU, bool KNOWN = true>
 __device__ __forceinline__ void
 build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* out,
               uint64_t stride, uint16_t* __restrict__ out_lens, int lane, int sub0)
 {
   static_assert(G >= 8, "batch slots u > 0 must lie past every header byte");
-  const SegInfo& si = F.si;
-  const uint32_t slice = si.seg_ok ? min(mss, si.payload - k * mss) : 0u;
-  const uint32_t dlen = si.nseg == 1 ? F.flen : si.hlen + slice;
-  if (dlen > stride) {
-    if (lane == 0) {
-      out_lens[j] = 0;
+  SegInfo si = F.si;
+  uint32_t slice = 0, dlen = 0;
+  if constexpr (KNOWN) {
+    slice = si.seg_ok ? min(mss, si.payload - k * mss) : 0u;
+    dlen = si.nseg == 1 ? F.flen : si.hlen + slice;
+    if (dlen > stride) {
+      if (lane == 0) {
+        out_lens[j] = 0;
+      }
+      return;
     }
-    return;
   }
   const uintptr_t shift = uintptr_t(k) * mss;
   const uintptr_t dst = reinterpret_cast<uintptr_t>(out) + uintptr_t(j) * stride;
-  const int nchunks = int((dlen + 15) >> 4);
   const uintptr_t xs = F.fa + shift;          // source of output byte 0
   // Output chunk c is source bytes [xs + 16c, +16): dwords p0 + 16c .. + 20
   // funnel-shifted by r bytes. Each lane loads the 4 dwords of its chunk at
@@ -381,6 +391,18 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
       return uint32_t(b) < F.flen ? (FW[b >> 2] >> (8 * (b & 3))) & 0xffu : 0u;
     },
     F.flen);
+  if constexpr (!KNOWN) {
+    si = seg_info(h, mss);
+    slice = si.seg_ok && k < si.nseg ? min(mss, si.payload - k * mss) : 0u;
+    dlen = si.nseg == 1 ? F.flen : si.hlen + slice;
+    if (k >= si.nseg || dlen > stride) {  // (uniform per subgroup)
+      if (lane == 0) {
+        out_lens[j] = 0;
+      }
+      return;
+    }
+  }
+  const int nchunks = int((dlen + 15) >> 4);
   const bool ip_on = h.ipv4;
   const bool l4_on = si.seg_ok || (h.tcp && !h.trunc && h.tcplen >= 18u);
   const uint32_t total = si.seg_ok ? 20u + 4u * h.doff + slice : h.total;
@@ -606,63 +628,237 @@ segment_kernel(const u32x4* __restrict__ desc, uint32_t mss,
   }
 }
 
+// ---- planned segmentation: the caller's first[], no prologue ---------------
+//
+// The reference decides the TSO split on the host: the transport posts each
+// super-frame with its header length (stack::utils::headerLength,
+// src/stack/Utils.cpp:67-84) and the MSS (src/transport/ofed/Device.cpp:
+// 688-700), and the segment count follows. A caller that has that plan passes
+// first[] (n + 1 entries, the exclusive prefix of the per-frame counts) and
+// the segment kernel runs alone: each block finds the frames of its S output
+// segments in first[] itself and parses their headers from the loads it
+// issues for the segments anyway.
+//
+// Frame search, per block, by wave 0: ONE round trip brings a speculative
+// window of PW frames (first[], offsets, lengths) where an evenly cut batch
+// would put segment jb (frame jb * n / capacity, a few frames of slack
+// before it). A window that does not cover the block's segments (uneven
+// counts, capacity far above the total) falls back to a 64-ary search over
+// first[] (one round trip per 64x, n <= 2^24: at most 4) and then loads the
+// window at the frame found.
+constexpr uint32_t PW = 64;     // window frames
+constexpr uint32_t PW_BACK = 8; // of which before the guessed frame
+
+template<int G, int SU>
+__global__ __launch_bounds__(256) void
+segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
+                       const uint16_t* __restrict__ lens, uint32_t n, uint32_t mss,
+                       const uint32_t* __restrict__ first, uint8_t* out, uint64_t stride,
+                       uint32_t capacity, uint16_t* __restrict__ out_lens)
+{
+  constexpr uint32_t S = 256 / G;
+  static_assert(S + 16 <= PW, "the window holds every frame of a block's segments");
+  __shared__ uint32_t pre[PW + 1];
+  __shared__ uint64_t fadr[PW];
+  __shared__ uint32_t flen[PW];
+  __shared__ uint32_t total_s;
+  const uint32_t tid = threadIdx.x;
+  const int lane = int(tid) & (G - 1);
+  const uint32_t sub = tid / G;
+  const uintptr_t b0 = reinterpret_cast<uintptr_t>(base);
+  for (uint32_t jb = xcd_block(blockIdx.x, gridDim.x) * S; jb < capacity;
+       jb += gridDim.x * S) {
+    if (tid < 64) {
+      // the window at frame w0: lane t holds frame w0 + t (first[], offset,
+      // length), lane 0 also first[w0 + PW] and first[n]
+      auto load_window = [&](uint32_t w0, uint32_t& p, uint32_t& pend, uint64_t& o, uint32_t& l) {
+        const uint32_t f = w0 + tid;
+        p = first[min(f, n)];
+        o = offs[min(f, n - 1)];
+        l = lens[min(f, n - 1)];
+        pend = first[min(w0 + PW, n)];
+      };
+      const uint32_t g = uint32_t(uint64_t(jb) * n / capacity);
+      uint32_t w0 = g > PW_BACK ? g - PW_BACK : 0u;
+      uint32_t p, pend;
+      uint64_t o;
+      uint32_t l;
+      load_window(w0, p, pend, o, l);
+      const uint32_t total = min(first[n], capacity);
+      const uint32_t jl = min(jb + S, max(total, jb + 1)) - 1; // the block's last segment
+      const uint32_t p0 = __shfl(p, 0, 64);
+      if (jb < total && !(p0 <= jb && jl < pend)) {
+        // the window missed: 64-ary search for the frame of jb (first[lo] <=
+        // jb < first[hi]); a span of at most PW - S - 1 frames leaves room
+        // for the block's other segments' frames in the window at lo
+        uint32_t lo = 0, hi = n;
+        while (hi - lo > PW - S - 1) {
+          const uint32_t span = hi - lo;
+          const uint32_t v = first[lo + uint32_t(uint64_t(span) * tid / 64)];
+          const uint64_t m = __ballot(v <= jb);
+          const uint32_t t = m ? 63u - uint32_t(__builtin_clzll(m)) : 0u;
+          const uint32_t nlo = lo + uint32_t(uint64_t(span) * t / 64);
+          hi = t == 63 ? hi : lo + uint32_t(uint64_t(span) * (t + 1) / 64);
+          lo = nlo;
+        }
+        w0 = lo;
+        load_window(w0, p, pend, o, l);
+      }
+      pre[tid] = p;
+      fadr[tid] = b0 + o;
+      flen[tid] = l;
+      if (tid == 0) {
+        pre[PW] = pend;
+        total_s = total;
+      }
+    }
+    __syncthreads();
+    const uint32_t total = total_s;
+    if (jb >= total) {
+      break; // (uniform: later tiles lie further past the total)
+    }
+    const uint32_t j = jb + sub;
+    if (j < total) {
+      uint32_t f = 0; // pre[f] <= j < pre[f + 1] within the window
+#pragma unroll 1
+      while (f + 1 < PW && pre[f + 1] <= j) {
+        ++f;
+      }
+      SegFrame F;
+      F.fa = uintptr_t(fadr[f]);
+      F.flen = flen[f];
+      F.lo = F.fa & ~uintptr_t(15);
+      F.hi = F.flen ? (F.fa + F.flen - 1) & ~uintptr_t(15) : F.lo;
+      const uint32_t k = j - pre[f];
+      const bool inside = pre[f] <= j && f < n;
+      int lv = lane;
+      asm volatile("" : "+v"(lv));
+      if (inside) {
+        build_segment<G, SU, false>(F, k, j, mss, out, stride, out_lens, lv,
+                                    int(tid & 63) & ~(G - 1));
+      } else if (lane == 0) {
+        out_lens[j] = 0; // the caller's first[] is not a prefix for this batch
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Workspace per (device, stream) (stream_state.h): the scan's block totals
 // (MAX_FRAMES / CB words), the run starts (one word per RUN output segments)
-// and the frame descriptors (16 bytes per input frame). Calls on one stream
-// run in order, so they can share one; calls on different streams may
-// overlap, so each stream gets its own. Made on first use and grown when a
-// call's capacity needs a longer map; a call that grows it cannot be captured
-// in a HIP graph (warm it up outside the capture). The caller holds the
-// stream's call mutex.
+// and the frame descriptors (16 bytes per input frame). Direct calls on one
+// stream run in order, so they share one, grown when a call needs more (the
+// old arrays are freed once the stream is idle: no graph holds them). The
+// calls one capture records on a stream share a workspace made for that
+// capture and owned by its graph, so a later direct call can neither free it
+// under the graph nor race a replay on it. The caller holds the stream's call
+// mutex.
 hipError_t
-workspace(StreamState& w, bool capturing, uint32_t capacity, uint32_t n,
+ws_alloc(int device, bool capturing, uint64_t nruns, uint64_t ndesc, StreamState::SegWs* w,
+         std::vector<void*>* made)
+{
+  struct Part
+  {
+    void** p;
+    size_t bytes;
+  };
+  const Part parts[3] = { { reinterpret_cast<void**>(&w->blocks),
+                            sizeof(uint32_t) * (MAX_FRAMES / CB) },
+                          { reinterpret_cast<void**>(&w->runs), sizeof(uint32_t) * nruns },
+                          { &w->desc, sizeof(u32x4) * ndesc } };
+  for (const Part& q : parts) {
+    if (*q.p) {
+      continue;
+    }
+    const hipError_t e = device_malloc_in_capture(device, capturing, q.p, q.bytes);
+    if (e != hipSuccess) {
+      *q.p = nullptr;
+      return e;
+    }
+    made->push_back(*q.p);
+  }
+  w->nruns = nruns;
+  w->ndesc = ndesc;
+  return hipSuccess;
+}
+
+hipError_t
+workspace(StreamState& s, bool capturing, uint32_t capacity, uint32_t n,
           uint32_t** blocks, uint32_t** runs, u32x4** desc)
 {
-  const uint64_t need = (uint64_t(capacity) + RUN - 1) / RUN;
-  if (capturing &&
-      (!w.seg_blocks || need > w.seg_nruns || (capacity && uint64_t(n) > w.seg_ndesc))) {
-    return hipErrorStreamCaptureUnsupported;
+  const uint64_t need_runs = (uint64_t(capacity) + RUN - 1) / RUN;
+  const uint64_t need_desc = capacity ? uint64_t(n) : 0;
+  StreamState::SegWs* w = nullptr;
+  if (capturing) {
+    unsigned long long id = 0;
+    if (!capture_id(s.stream, &id)) {
+      return hipErrorStreamCaptureUnsupported;
+    }
+    // only the capture in progress can add calls to its workspace
+    for (auto it = s.seg_capture.begin(); it != s.seg_capture.end();) {
+      it = it->first == id ? std::next(it) : s.seg_capture.erase(it);
+    }
+    auto it = s.seg_capture.find(id);
+    if (it == s.seg_capture.end() || it->second.nruns < need_runs ||
+        it->second.ndesc < need_desc) {
+      // a fresh one sized for this call (the graph keeps it; an earlier one
+      // of this capture stays with the calls recorded on it)
+      StreamState::SegWs fresh;
+      std::vector<void*> made;
+      const hipError_t e = ws_alloc(s.device, true, need_runs ? need_runs : 1,
+                                    need_desc ? need_desc : 1, &fresh, &made);
+      s.seg_owned.insert(s.seg_owned.end(), made.begin(), made.end());
+      if (e != hipSuccess) {
+        return e;
+      }
+      it = s.seg_capture.insert_or_assign(id, fresh).first;
+    }
+    w = &it->second;
+  } else {
+    w = &s.seg;
+    if (!w->blocks || need_runs > w->nruns || need_desc > w->ndesc) {
+      StreamState::SegWs grown;
+      grown.blocks = w->blocks;
+      if (need_runs <= w->nruns) {
+        grown.runs = w->runs;
+      }
+      if (need_desc <= w->ndesc) {
+        grown.desc = w->desc;
+      }
+      std::vector<void*> made;
+      const uint64_t nr = std::max<uint64_t>(std::max<uint64_t>(need_runs, 65536), w->nruns);
+      const uint64_t nd = std::max<uint64_t>(std::max<uint64_t>(need_desc, 65536), w->ndesc);
+      hipError_t e = ws_alloc(s.device, false, grown.runs ? w->nruns : nr,
+                              grown.desc ? w->ndesc : nd, &grown, &made);
+      if (e == hipSuccess) {
+        e = hipStreamSynchronize(s.stream); // the arrays replaced are idle
+      }
+      if (e != hipSuccess) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(s.device);
+        for (void* p : made) {
+          (void)hipFree(p);
+        }
+        (void)hipSetDevice(prev);
+        return e;
+      }
+      int prev = 0;
+      (void)hipGetDevice(&prev);
+      (void)hipSetDevice(s.device);
+      if (grown.runs != w->runs) {
+        (void)hipFree(w->runs);
+      }
+      if (grown.desc != w->desc) {
+        (void)hipFree(w->desc);
+      }
+      (void)hipSetDevice(prev);
+      *w = grown;
+    }
   }
-  hipError_t e;
-  if (!w.seg_blocks) {
-    void* p = nullptr;
-    e = device_malloc(w.device, &p, sizeof(uint32_t) * (MAX_FRAMES / CB));
-    if (e != hipSuccess) {
-      return e;
-    }
-    w.seg_blocks = static_cast<uint32_t*>(p);
-  }
-  if (need > w.seg_nruns) {
-    const uint64_t want = need < 65536 ? 65536 : need;
-    void* p = nullptr;
-    e = device_malloc(w.device, &p, sizeof(uint32_t) * want);
-    if (e != hipSuccess) {
-      return e;
-    }
-    if (w.seg_runs) {
-      (void)hipStreamSynchronize(w.stream); // the old array may still be in use
-      (void)hipFree(w.seg_runs);
-    }
-    w.seg_runs = static_cast<uint32_t*>(p);
-    w.seg_nruns = want;
-  }
-  if (capacity && uint64_t(n) > w.seg_ndesc) {
-    const uint64_t want = n < 65536 ? 65536 : uint64_t(n);
-    void* p = nullptr;
-    e = device_malloc(w.device, &p, sizeof(u32x4) * want);
-    if (e != hipSuccess) {
-      return e;
-    }
-    if (w.seg_desc) {
-      (void)hipStreamSynchronize(w.stream); // the old array may still be in use
-      (void)hipFree(w.seg_desc);
-    }
-    w.seg_desc = p;
-    w.seg_ndesc = want;
-  }
-  *blocks = w.seg_blocks;
-  *runs = w.seg_runs;
-  *desc = static_cast<u32x4*>(w.seg_desc);
+  *blocks = w->blocks;
+  *runs = w->runs;
+  *desc = static_cast<u32x4*>(w->desc);
   return hipSuccess;
 }
 
@@ -746,4 +942,74 @@ tulips_csum_segment_frames(const uint8_t* in_base, const uint64_t* in_offsets,
   }
   e = hipGetLastError();
   return e == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
+}
+
+extern "C" int
+tulips_csum_segment_frames_planned(const uint8_t* in_base, const uint64_t* in_offsets,
+                                   const uint16_t* in_lengths, uint32_t n, uint32_t mss,
+                                   const uint32_t* first, uint8_t* out_base,
+                                   uint64_t out_stride, uint32_t out_capacity,
+                                   uint16_t* out_lengths, void* stream)
+{
+  using namespace tulips_amd;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (mss == 0 || mss > 0xffffu || n > MAX_FRAMES) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  if (n == 0 || out_capacity == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!in_base || !in_offsets || !in_lengths || !first || !out_base || !out_lengths ||
+      (reinterpret_cast<uintptr_t>(out_base) & 15) || out_stride < 16 || (out_stride & 15)) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  const bool small = mss <= 1460;
+  const uint32_t per_block = small ? 256 / 16 : 256 / 64;
+  const uint64_t want = (uint64_t(out_capacity) + per_block - 1) / per_block;
+  const uint32_t blocks = uint32_t(want > 65535 ? 65535 : want);
+  (void)hipGetLastError();
+  if (small) {
+    hipLaunchKernelGGL((segment_planned_kernel<16, 6>), dim3(blocks), dim3(256), 0, st,
+                       in_base, in_offsets, in_lengths, n, mss, first, out_base, out_stride,
+                       out_capacity, out_lengths);
+  } else {
+    hipLaunchKernelGGL((segment_planned_kernel<64, 6>), dim3(blocks), dim3(256), 0, st,
+                       in_base, in_offsets, in_lengths, n, mss, first, out_base, out_stride,
+                       out_capacity, out_lengths);
+  }
+  return hipGetLastError() == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
+}
+
+extern "C" int
+tulips_csum_segment_plan_host(const uint8_t* base, const uint64_t* offsets,
+                              const uint16_t* lengths, uint32_t n, uint32_t mss,
+                              uint32_t* first)
+{
+  if (!first || mss == 0 || mss > 0xffffu || (n && (!base || !offsets || !lengths))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  // seg_info of the device prologue, on bytes read in place (0 past the frame)
+  uint64_t acc = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* f = base + offsets[i];
+    const uint32_t flen = lengths[i];
+    auto at = [&](uint32_t k) -> uint32_t { return k < flen ? f[k] : 0u; };
+    const bool eth_ip = flen >= 14 && ((at(12) << 8) | at(13)) == 0x0800u;
+    const bool runt = eth_ip && flen < 34;
+    const bool ipv4 = eth_ip && !runt && at(14) == 0x45u;
+    const bool tcp = ipv4 && (at(20) & 0x3fu) == 0 && at(21) == 0 && at(23) == 6u;
+    const uint32_t total = (at(16) << 8) | at(17);
+    const uint32_t tcplen = (total - 20u) & 0xffffu;
+    const bool trunc = tcp && (total < 20u || 34u + tcplen > flen);
+    const uint32_t doff = at(46) >> 4;
+    const bool seg_ok = tcp && !trunc && doff >= 5 && 20u + 4u * doff <= total;
+    const uint32_t payload = seg_ok ? total - 20u - 4u * doff : 0u;
+    first[i] = uint32_t(acc);
+    acc += (seg_ok && payload > mss) ? (payload + mss - 1) / mss : 1u;
+    if (acc > 0xffffffffull) {
+      return TULIPS_STATUS_INVALID_ARGUMENT;
+    }
+  }
+  first[n] = uint32_t(acc);
+  return TULIPS_STATUS_OK;
 }

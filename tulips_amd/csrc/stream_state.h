@@ -15,8 +15,12 @@
 //    the capture stream. A capture cannot allocate: count once on the stream
 //    before capturing (spares are made then), at most SPARE_SHARDS captured
 //    counting calls per stream until tulips_csum_release_stream.
+//  * Segmentation calls captured in a graph run on a workspace made for that
+//    capture and owned by the graph (no warm-up needed, nothing a later
+//    direct call does can free it under the graph).
 //  * tulips_csum_release_stream frees everything a stream holds, including
-//    the shards owned by graphs captured on it (destroy those graphs first).
+//    the shards and workspaces owned by graphs captured on it (destroy those
+//    graphs first).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -43,12 +47,25 @@ struct StreamState
   std::vector<uint32_t*> graph_owned;  // handed to captured calls
   std::vector<uint32_t*> retired;      // dropped after a failed launch
 
-  // segmentation workspace (segment.hip)
-  uint32_t* seg_blocks = nullptr;
-  uint32_t* seg_runs = nullptr;
-  uint64_t seg_nruns = 0;
-  void* seg_desc = nullptr; // 16 B per input frame
-  uint64_t seg_ndesc = 0;
+  // segmentation workspace (segment.hip): the scan's block totals, the run
+  // starts and the per-frame descriptors
+  struct SegWs
+  {
+    uint32_t* blocks = nullptr;
+    uint32_t* runs = nullptr;
+    uint64_t nruns = 0;
+    void* desc = nullptr; // 16 B per input frame
+    uint64_t ndesc = 0;
+  };
+  // direct (uncaptured) calls: grown on demand, the old arrays freed once the
+  // stream is idle (no graph ever holds them)
+  SegWs seg;
+  // a capture's calls on this stream share one workspace made for that
+  // capture (relaxed capture mode), owned by its graph: later direct calls
+  // never free or regrow it, and a replay never shares arrays with direct
+  // calls on this stream or with another graph
+  std::map<unsigned long long, SegWs> seg_capture;
+  std::vector<void*> seg_owned;
 
   // SPAN split-form words (span_kernel.h csum_span_kernel): one 64-bit word
   // per arena range, tagged with the launch's dispatch id and queue, so a word left by
@@ -100,5 +117,12 @@ void drop_shards(StreamState& s, uint32_t* shards);
 
 // hipMalloc on `device` (restores the caller's current device).
 hipError_t device_malloc(int device, void** p, size_t bytes);
+
+// hipMalloc on `device` from inside a capture: the thread's capture mode is
+// relaxed around the allocation (plain device_malloc when not capturing).
+hipError_t device_malloc_in_capture(int device, bool capturing, void** p, size_t bytes);
+
+// The id of the capture in progress on `stream` (false when none can be read).
+bool capture_id(hipStream_t stream, unsigned long long* id);
 
 } // namespace tulips_amd

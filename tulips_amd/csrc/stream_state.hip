@@ -69,6 +69,31 @@ device_malloc(int device, void** p, size_t bytes)
 }
 
 hipError_t
+device_malloc_in_capture(int device, bool capturing, void** p, size_t bytes)
+{
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  if (capturing) {
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+  }
+  const hipError_t e = device_malloc(device, p, bytes);
+  if (capturing) {
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+  }
+  return e;
+}
+
+bool
+capture_id(hipStream_t stream, unsigned long long* id)
+{
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamGetCaptureInfo(stream, &cs, id) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return cs == hipStreamCaptureStatusActive;
+}
+
+hipError_t
 stream_state(hipStream_t stream, std::shared_ptr<StreamState>* out)
 {
   int dev = 0;
@@ -223,10 +248,8 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64
     *salt = 0;
     return hipSuccess;
   }
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   unsigned long long id = 0;
-  if (hipStreamGetCaptureInfo(s.stream, &cs, &id) != hipSuccess) {
-    (void)hipGetLastError();
+  if (!capture_id(s.stream, &id)) {
     return hipErrorStreamCaptureUnsupported;
   }
   // only the capture in progress on this stream can add calls to its array
@@ -310,9 +333,10 @@ tulips_csum_release_stream(void* stream)
     for (auto* p : s->spare) ps.push_back(p);
     for (auto* p : s->graph_owned) ps.push_back(p);
     for (auto* p : s->retired) ps.push_back(p);
-    ps.push_back(s->seg_blocks);
-    ps.push_back(s->seg_runs);
-    ps.push_back(s->seg_desc);
+    ps.push_back(s->seg.blocks);
+    ps.push_back(s->seg.runs);
+    ps.push_back(s->seg.desc);
+    for (auto* p : s->seg_owned) ps.push_back(p);
     ps.push_back(s->span_slots);
     for (auto* p : s->span_spare) ps.push_back(p);
     for (auto* p : s->span_owned) ps.push_back(p);
@@ -321,9 +345,9 @@ tulips_csum_release_stream(void* stream)
     s->spare.clear();
     s->graph_owned.clear();
     s->retired.clear();
-    s->seg_blocks = s->seg_runs = nullptr;
-    s->seg_desc = nullptr;
-    s->seg_nruns = s->seg_ndesc = 0;
+    s->seg = StreamState::SegWs();
+    s->seg_owned.clear();
+    s->seg_capture.clear();
     s->span_slots = nullptr;
     s->span_nslots = 0;
     s->span_spare.clear();

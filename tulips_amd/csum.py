@@ -141,6 +141,10 @@ _SIGNATURES = {
     "tulips_csum_generate_fields": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     "tulips_csum_segment_frames": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp,
                                              C.c_uint64, C.c_uint32, _vp, _vp, _vp]),
+    "tulips_csum_segment_frames_planned": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint32,
+                                                     _vp, _vp, C.c_uint64, C.c_uint32, _vp,
+                                                     _vp]),
+    "tulips_csum_segment_plan_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
     "tulips_csum_frames_tuned": (C.c_int, [C.c_int, _vp, _vp, _vp, C.c_uint32, _vp, _vp,
                                            C.POINTER(Tuning), _vp]),
     "tulips_csum_validate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp,
@@ -172,6 +176,7 @@ _SIGNATURES = {
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
     "tulips_csum_validate_frames_cpu": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp]),
     "tulips_csum_gpu_sleep": (C.c_int, [C.c_uint32, _vp]),
+    "tulips_csum_debug_crash_backtrace": (C.c_int, [C.c_int]),
     "tulips_csum_time_validate_ring": (C.c_int, [_vp, C.c_int, _vp, C.c_uint64, C.c_uint32,
                                                  _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp]),
     "tulips_csum_mctx_validate_frames_rss_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32,
@@ -868,6 +873,46 @@ def segment_frames(arena, offsets, lengths, mss: int, *, stride: int = 2048,
                                           _addr(first), st),
            "tulips_csum_segment_frames")
     return out, out_lengths, first
+
+
+def segment_plan(arena, offsets, lengths, mss: int):
+    """Host frames -> first (uint32[n+1]), the plan of
+    segment_frames_planned (tulips_csum_segment_plan_host)."""
+    import numpy as np
+    ar = _host(arena, np.uint8)
+    off = _host(offsets, np.uint64)
+    ln = _host(lengths, np.uint16)
+    n = len(off.keep)
+    first = np.zeros(n + 1, dtype=np.uint32)
+    _check(lib.tulips_csum_segment_plan_host(ar.ptr, off.ptr, ln.ptr, n, mss,
+                                             first.ctypes.data),
+           "tulips_csum_segment_plan_host")
+    return first
+
+
+def segment_frames_planned(arena, offsets, lengths, mss: int, first, *, stride: int = 2048,
+                           out=None, out_lengths=None, capacity: int | None = None,
+                           stream=None):
+    """Segmentation of device-resident frames with the caller's plan `first`
+    (device int32[n+1], tulips_csum_segment_frames_planned). Returns (out,
+    out_lengths)."""
+    import torch
+    n = int(offsets.numel())
+    if int(lengths.numel()) != n or int(first.numel()) != n + 1:
+        raise ValueError("offsets/lengths/first size mismatch")
+    dev = arena.device
+    if capacity is None:
+        capacity = int(out.numel()) // stride if out is not None else int(first[n].item())
+    if out is None:
+        out = torch.empty(max(capacity, 1) * stride, dtype=torch.uint8, device=dev)
+    if out_lengths is None:
+        out_lengths = torch.zeros(max(capacity, 1), dtype=torch.int16, device=dev)
+    if int(out_lengths.numel()) < capacity or int(out.numel()) < capacity * stride:
+        raise ValueError("output smaller than its capacity")
+    _check(lib.tulips_csum_segment_frames_planned(
+        _addr(arena), _addr(offsets), _addr(lengths), n, mss, _addr(first), _addr(out), stride,
+        capacity, _addr(out_lengths), _stream(stream)), "tulips_csum_segment_frames_planned")
+    return out, out_lengths
 
 
 def release_stream(stream) -> None:
