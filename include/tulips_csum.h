@@ -457,6 +457,22 @@ int tulips_csum_validate_frames_cpu(const uint8_t* base, const uint64_t* offsets
                                     uint8_t* flags, uint32_t* counters);
 
 /*
+ * The CPU / GPU crossover for one receive poll burst, measured on MI355X
+ * with frames a NIC has just written (outside the CPU caches; bench.py
+ * extras.burst_latency_host.cold_ring): 1514 B frames cost the
+ * host code ~0.13-0.16 us each, the zero-copy GPU path ~13 us + ~0.02 us
+ * each (64 frames: 8.5 against 14.4 us; 256: 41.4 against 18.3), so they
+ * cross near 96 frames; the host cost follows the bytes, so larger frames
+ * cross sooner. Returns 1 when a burst of n frames and `bytes` bytes is
+ * cheaper on the calling thread (tulips_csum_validate_frames_cpu): fewer
+ * than TULIPS_CSUM_CPU_BELOW_FRAMES frames and fewer than
+ * TULIPS_CSUM_CPU_BELOW_BYTES bytes. The gpucsum decorator's defaults.
+ */
+#define TULIPS_CSUM_CPU_BELOW_FRAMES 96u
+#define TULIPS_CSUM_CPU_BELOW_BYTES (96u * 1514u)
+int tulips_csum_burst_prefers_cpu(uint32_t n, uint64_t bytes);
+
+/*
  * Low-latency (zero-copy) form of tulips_csum_validate_frames_host for poll
  * bursts (the reference is a latency stack: docs/topics/Test-and-
  * Performance.md:12-15, its OFED poll drains whatever CQ batch is ready,

@@ -130,7 +130,9 @@ int tulips_csum_stream_read_slots(const uint8_t* p, uint64_t slot_bytes, uint32_
  * host-resident frames, timed in C with a steady clock around each call
  * (no interpreter in the loop): path 0 = tulips_csum_validate_frames_host
  * (staged), 1 = tulips_csum_validate_frames_zc, 2 =
- * tulips_csum_validate_frames_cpu (host code, no GPU). out[0..4] = median, p99,
+ * tulips_csum_validate_frames_cpu (host code, no GPU), 3 = the gpucsum
+ * decorator's default choice per burst (2 when
+ * tulips_csum_burst_prefers_cpu, else 1). out[0..4] = median, p99,
  * min, mean (us) and, for path 1, the median GPU service time (request
  * picked up -> flags out, from the server's realtime clock; 0 otherwise).
  * `flags` (n bytes) holds the last call's flags. */

@@ -9,8 +9,8 @@
  * poll from it into a page-locked staging arena, validates the whole burst
  * in one GPU launch (tulips_csum_validate_frames_zc / _host: Ethernet ->
  * IPv4 header checksum -> TCP pseudo-header checksum, include/tulips_csum.h;
- * bursts below Config::cpu_below frames on the polling thread with the
- * library's host code, tulips_csum_validate_frames_cpu, as the reference
+ * bursts below Config::cpu_below frames and Config::cpu_below_bytes bytes
+ * on the polling thread with the library's host code, tulips_csum_validate_frames_cpu, as the reference
  * would per frame), and forwards to the stack only the frames that pass, in
  * arrival order.
  *
@@ -49,6 +49,7 @@
  */
 
 #include <tulips/transport/Device.h>
+#include <tulips_csum.h>
 #include <cstdint>
 #include <unordered_map>
 #include <unordered_set>
@@ -81,12 +82,15 @@ public:
   // staged one at every burst size up to its 1,024-frame limit: DESIGN.md §5
   // "Latency per poll burst")
   static constexpr uint32_t DEFAULT_LOWLAT = 1024;
-  // bursts of fewer frames are validated on the polling thread by the
-  // library's host code (tulips_csum_validate_frames_cpu): below this size a
-  // PCIe round trip to the GPU costs more than the per-frame checks do on
-  // the CPU (DESIGN.md §5 "Latency per poll burst": ~0.2 us per 1514 B frame
-  // on the host against ~10 us for a zero-copy launch)
-  static constexpr uint32_t DEFAULT_CPU_BELOW = 32;
+  // bursts of fewer frames (and bytes) are validated on the polling thread
+  // by the library's host code (tulips_csum_validate_frames_cpu): below
+  // this size a PCIe round trip to the GPU costs more than the per-frame
+  // checks do on the CPU. The library's measured crossover
+  // (tulips_csum_burst_prefers_cpu, include/tulips_csum.h): cold 1514 B
+  // frames cost ~0.15 us each on the host against ~13 us + 0.02 us each on
+  // the zero-copy path, crossing near 96 frames
+  static constexpr uint32_t DEFAULT_CPU_BELOW = TULIPS_CSUM_CPU_BELOW_FRAMES;
+  static constexpr uint64_t DEFAULT_CPU_BELOW_BYTES = TULIPS_CSUM_CPU_BELOW_BYTES;
 
   struct Config
   {
@@ -102,8 +106,10 @@ public:
     uint32_t lowlat = DEFAULT_LOWLAT;
     // ... served by workgroups resident on the GPU (no launch per burst)
     bool lowlat_resident = false;
-    // receive: bursts of fewer frames stay on the CPU; 0 = always the GPU
+    // receive: bursts of fewer frames AND fewer bytes stay on the CPU;
+    // cpu_below 0 = always the GPU
     uint32_t cpu_below = DEFAULT_CPU_BELOW;
+    uint64_t cpu_below_bytes = DEFAULT_CPU_BELOW_BYTES;
   };
 
   static Ref allocate(system::Logger& log, transport::Device::Ref device,
@@ -230,6 +236,7 @@ private:
   uint32_t m_tso;
   uint32_t m_lowlat;
   uint32_t m_cpu_below;
+  uint64_t m_cpu_below_bytes;
   std::vector<Pending> m_pending;
   std::unordered_set<uint8_t*> m_own;        // our TSO send buffers
   std::vector<uint8_t*> m_free;              // ... not handed out

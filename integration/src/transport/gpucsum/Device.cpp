@@ -45,6 +45,7 @@ Device::Device(system::Logger& log, transport::Device::Ref device,
   , m_tso(config.tso ? std::max<uint32_t>(config.tso, m_device->mss()) : 0)
   , m_lowlat(config.lowlat)
   , m_cpu_below(config.cpu_below)
+  , m_cpu_below_bytes(config.cpu_below_bytes)
 {
   m_hints |= config.hints;
   // Room for a whole burst of 2 KiB receive buffers (the OFED RX layout,
@@ -360,7 +361,13 @@ Device::flush()
   // ones read in place from the pinned arena by the zero-copy path, large
   // ones staged through the context's DMA pipeline
   int rc;
+  uint64_t bytes = 0;
   if (n < m_cpu_below) {
+    for (uint32_t i = 0; i < n; ++i) {
+      bytes += m_lengths[i];
+    }
+  }
+  if (n < m_cpu_below && bytes < m_cpu_below_bytes) {
     rc = tulips_csum_validate_frames_cpu(m_arena, m_offsets.data(), m_lengths.data(), n,
                                          m_flags.data(), nullptr);
     m_stats.cpu_batches += 1;

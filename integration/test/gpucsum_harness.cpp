@@ -63,13 +63,18 @@ gpucsum_run(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
   return run_cfg(arena, offs, lens, n, burst, hints, use_wait, -1, forwarded, stats);
 }
 
-// gpucsum_run with Config::cpu_below set (stats[5] = cpu_batches).
+// gpucsum_run with Config::cpu_below set (-1: the decorator's default
+// crossover, frames and bytes; otherwise that many frames and no bytes
+// limit); stats[5] = cpu_batches.
 extern "C" int
 gpucsum_run_cpu_below(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens,
-                      uint32_t n, uint32_t burst, uint16_t hints, uint32_t cpu_below,
+                      uint32_t n, uint32_t burst, uint16_t hints, int64_t cpu_below,
                       uint8_t* forwarded, uint64_t* stats)
 {
-  return run_cfg(arena, offs, lens, n, burst, hints, 0, cpu_below, forwarded, stats);
+  stats[5] = 0;
+  const int rc = run_cfg(arena, offs, lens, n, burst, hints, 0, cpu_below < 0 ? -2 : cpu_below,
+                         forwarded, stats);
+  return rc;
 }
 
 namespace {
@@ -100,6 +105,7 @@ run_cfg(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens, uint32
     cfg.hints = hints;
     if (cpu_below >= 0) {
       cfg.cpu_below = uint32_t(cpu_below);
+      cfg.cpu_below_bytes = UINT64_MAX;
     }
     transport::gpucsum::Device dev(log, std::move(rx), cfg);
     Recorder rec;
@@ -132,7 +138,7 @@ run_cfg(const uint8_t* arena, const uint64_t* offs, const uint16_t* lens, uint32
     stats[2] = st.bad_ip;
     stats[3] = st.bad_l4;
     stats[4] = st.batches;
-    if (cpu_below >= 0) {
+    if (cpu_below >= 0 || cpu_below == -2) { // -2: default crossover, stats[5] wanted
       stats[5] = st.cpu_batches;
     }
     return 0;

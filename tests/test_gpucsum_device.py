@@ -139,6 +139,75 @@ def test_cpu_crossover_by_burst(burst):
     assert (int(st[4]), int(st[5])) == (gpu, cpu)
 
 
+def run_default_crossover(arena, offs, lens, burst):
+    from tulips_amd import csum  # noqa: F401
+    lib = C.CDLL(HARNESS)
+    f = lib.gpucsum_run_cpu_below
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint16,
+                  C.c_int64, C.c_void_p, C.c_void_p]
+    n = len(offs)
+    fwd = np.zeros(n, dtype=np.uint8)
+    stats = np.zeros(6, dtype=np.uint64)
+    rc = f(np.ascontiguousarray(arena).ctypes.data, np.ascontiguousarray(offs).ctypes.data,
+           np.ascontiguousarray(lens).ctypes.data, n, burst, 3, -1, fwd.ctypes.data,
+           stats.ctypes.data)
+    assert rc == 0, f"gpucsum_run_cpu_below rc={rc}"
+    return fwd, stats
+
+
+@needs_harness
+@pytest.mark.gpu
+@pytest.mark.parametrize("burst", [1, 8, 64, 95, 96, 128, 256])
+def test_default_crossover_frames_side(burst):
+    """The decorator's default crossover (tulips_csum_burst_prefers_cpu: fewer
+    than 96 frames and 96 x 1514 bytes, from the cold-frame measurement):
+    fixture bursts (<= 1514 B frames) below 96 frames stay on the CPU, the
+    others go to the GPU; the forwarded frames are exactly those the
+    reference-derived flags pass."""
+    from tulips_amd import csum
+    fx = fixture()
+    n = min(len(fx["offsets"]), 40 * burst)
+    offs, lens = fx["offsets"][:n], fx["lengths"][:n]
+    fwd, st = run_default_crossover(fx["arena"], offs, lens, burst)
+    exp, bad_ip, bad_l4 = expected_forwarded(fx["expect"][:n], 3)
+    np.testing.assert_array_equal(fwd, exp)
+    cpu = gpu = 0
+    for b0 in range(0, n, burst):
+        ln = lens[b0:b0 + burst]
+        if csum.lib.tulips_csum_burst_prefers_cpu(len(ln), int(ln.astype(np.int64).sum())):
+            cpu += 1
+        else:
+            gpu += 1
+    assert (int(st[4]), int(st[5])) == (gpu, cpu)
+    assert (cpu > 0) == (burst < 96) and (gpu > 0) == (burst >= 96)
+
+
+@needs_harness
+@pytest.mark.gpu
+def test_default_crossover_bytes_side(oracle):
+    """Jumbo frames (9,014 B): a burst of 20 frames is past the bytes limit
+    (180 KB > 145 KB) and goes to the GPU, a burst of 12 (108 KB) stays on
+    the CPU; corrupted frames are dropped either way."""
+    from test_frames import make_frame
+    rng = np.random.default_rng(96)
+    frames = [bytearray(make_frame(oracle, rng, 8960)) for _ in range(120)]
+    for k in range(0, 120, 7):
+        frames[k][200] ^= 0x10          # bad TCP checksum
+    offs = np.arange(120, dtype=np.uint64) * np.uint64(9216)
+    arena = np.zeros(120 * 9216, dtype=np.uint8)
+    for k, f in enumerate(frames):
+        arena[k * 9216:k * 9216 + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
+    lens = np.array([len(f) for f in frames], dtype=np.uint16)
+    assert lens[0] > 9000
+    exp, _, bad_l4 = expected_forwarded(oracle.validate_frames(arena, offs, lens), 3)
+    assert bad_l4 == len(range(0, 120, 7))
+    for burst, cpu_bursts in ((20, 0), (12, 10)):
+        fwd, st = run_default_crossover(arena, offs, lens, burst)
+        np.testing.assert_array_equal(fwd, exp)
+        assert int(st[5]) == cpu_bursts and int(st[4]) == 120 // burst - cpu_bursts
+
+
 @needs_harness
 @pytest.mark.gpu
 def test_cpu_crossover_off_keeps_every_burst_on_the_gpu():

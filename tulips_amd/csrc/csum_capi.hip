@@ -141,6 +141,12 @@ tulips_csum_tcp_host(uint32_t src, uint32_t dst, uint16_t len,
 // checks (ipv4/Processor.cpp:67-122, tcpv4/Processor.cpp:120-132). Header
 // rules as frame_common.h parse_header.
 int
+tulips_csum_burst_prefers_cpu(uint32_t n, uint64_t bytes)
+{
+  return n < TULIPS_CSUM_CPU_BELOW_FRAMES && bytes < TULIPS_CSUM_CPU_BELOW_BYTES ? 1 : 0;
+}
+
+int
 tulips_csum_validate_frames_cpu(const uint8_t* base, const uint64_t* offsets,
                                 const uint16_t* lengths, uint32_t n, uint8_t* flags,
                                 uint32_t* counters)

@@ -1102,16 +1102,24 @@ tulips_csum_time_validate_ring(tulips_csum_ctx* ctx, int path, const uint8_t* ri
                                const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
                                uint32_t reps, uint8_t* flags, double* out)
 {
-  if (!ctx || !out || reps == 0 || path < 0 || path > 2 || nbursts == 0) {
+  if (!ctx || !out || reps == 0 || path < 0 || path > 3 || nbursts == 0) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
   std::vector<double> t(reps), g;
   for (uint32_t r = 0; r < reps; ++r) {
     const uint8_t* base = ring + uint64_t(r % nbursts) * burst_stride;
     const auto t0 = std::chrono::steady_clock::now();
+    int use = path;
+    if (use == 3) { // the decorator's default choice, made inside the timed call
+      uint64_t bytes = 0;
+      for (uint32_t k = 0; k < n; ++k) {
+        bytes += lengths[k];
+      }
+      use = tulips_csum_burst_prefers_cpu(n, bytes) ? 2 : 1;
+    }
     const int rc =
-      path == 2   ? tulips_csum_validate_frames_cpu(base, offsets, lengths, n, flags, nullptr)
-      : path == 1 ? tulips_csum_validate_frames_zc(ctx, base, offsets, lengths, n, flags, nullptr)
+      use == 2   ? tulips_csum_validate_frames_cpu(base, offsets, lengths, n, flags, nullptr)
+      : use == 1 ? tulips_csum_validate_frames_zc(ctx, base, offsets, lengths, n, flags, nullptr)
                   : tulips_csum_validate_frames_host(ctx, base, offsets, lengths, n, flags,
                                                      nullptr);
     t[r] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
@@ -1119,7 +1127,7 @@ tulips_csum_time_validate_ring(tulips_csum_ctx* ctx, int path, const uint8_t* ri
     if (rc != TULIPS_STATUS_OK) {
       return rc;
     }
-    if (path == 1 && ctx->zc.mb) {
+    if (use == 1 && ctx->zc.mb) {
       g.push_back(double(ctx->zc.mb->t_done - ctx->zc.mb->t_req) / 100.0); // 100 MHz
     }
   }

@@ -175,6 +175,7 @@ _SIGNATURES = {
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
     "tulips_csum_validate_frames_cpu": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp]),
+    "tulips_csum_burst_prefers_cpu": (C.c_int, [C.c_uint32, C.c_uint64]),
     "tulips_csum_gpu_sleep": (C.c_int, [C.c_uint32, _vp]),
     "tulips_csum_debug_crash_backtrace": (C.c_int, [C.c_int]),
     "tulips_csum_time_validate_ring": (C.c_int, [_vp, C.c_int, _vp, C.c_uint64, C.c_uint32,
