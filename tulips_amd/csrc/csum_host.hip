@@ -1188,24 +1188,33 @@ segment_host(tulips_csum_ctx* ctx, const uint8_t* in_base, const uint64_t* in_of
   uint64_t produced = 0; // segments of the frames before this chunk
   uint32_t i = 0;
   while (i < n) {
-    // frames [i, j) that fit one staging chunk, and the most segments they
-    // can make (a frame of L bytes carries at most L payload bytes: at most
-    // ceil(L / mss) segments, at least 1), which bounds the device output
-    uint64_t bytes = 0, most = 0;
+    // frames [i, j) that fit one staging chunk
+    uint64_t bytes = 0;
     uint32_t j = i;
     while (j < n && j - i < MAX_SEGS_PER_CHUNK && bytes + in_lengths[j] <= ctx->chunk) {
       s.h_offs[j - i] = bytes;
       bytes += in_lengths[j];
-      most += std::max<uint64_t>(1, (uint64_t(in_lengths[j]) + mss - 1) / mss);
       ++j;
     }
     const uint32_t cnt = j - i;
-    pack(ctx->pool, s, in_base, in_offsets, in_lengths, i, j);
-    memcpy(s.h_lens, in_lengths + i, size_t(cnt) * 2);
+    // the plan from the headers, on this thread (the reference's transport
+    // decides the TSO split on the host too): the device runs the segment
+    // kernel alone, and the counts need no read-back
+    int rc = tulips_csum_segment_plan_host(in_base, in_offsets + i, in_lengths + i, cnt, mss,
+                                           ctx->h_first);
+    if (rc != TULIPS_STATUS_OK) {
+      return rc;
+    }
+    const uint32_t made = ctx->h_first[cnt];
     const uint32_t room = produced >= out_capacity
                             ? 0u
-                            : uint32_t(std::min<uint64_t>(out_capacity - produced, most));
+                            : uint32_t(std::min<uint64_t>(out_capacity - produced, made));
+    for (uint32_t k = 0; k < cnt; ++k) {
+      out_first[i + k] = uint32_t(produced + ctx->h_first[k]);
+    }
     if (room) {
+      pack(ctx->pool, s, in_base, in_offsets, in_lengths, i, j);
+      memcpy(s.h_lens, in_lengths + i, size_t(cnt) * 2);
       uint64_t have_lens = ctx->seg_lens_n * 2;
       if ((e = grow(reinterpret_cast<void**>(&ctx->d_seg_out), &ctx->seg_out_bytes,
                     uint64_t(room) * out_stride)) != hipSuccess ||
@@ -1214,38 +1223,28 @@ segment_host(tulips_csum_ctx* ctx, const uint8_t* in_base, const uint64_t* in_of
         return status_of(e);
       }
       ctx->seg_lens_n = have_lens / 2;
-    }
-    if ((e = hipMemcpyAsync(s.d_bytes, s.h_bytes, bytes, hipMemcpyHostToDevice, st)) !=
-          hipSuccess ||
-        (e = hipMemcpyAsync(s.d_offs, s.h_offs, size_t(cnt) * 8, hipMemcpyHostToDevice,
-                            st)) != hipSuccess ||
-        (e = hipMemcpyAsync(s.d_lens, s.h_lens, size_t(cnt) * 2, hipMemcpyHostToDevice,
-                            st)) != hipSuccess) {
-      return status_of(e);
-    }
-    int rc = tulips_csum_segment_frames(s.d_bytes, s.d_offs, s.d_lens, cnt, mss,
-                                        room ? ctx->d_seg_out : nullptr, out_stride, room,
-                                        room ? ctx->d_seg_lens : nullptr, ctx->d_first, st);
-    if (rc != TULIPS_STATUS_OK) {
-      return rc;
-    }
-    if ((e = hipMemcpyAsync(ctx->h_first, ctx->d_first, sizeof(uint32_t) * (cnt + 1),
-                            hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess) {
-      return status_of(e);
-    }
-    const uint32_t made = ctx->h_first[cnt];
-    const uint32_t kept = made < room ? made : room;
-    for (uint32_t k = 0; k < cnt; ++k) {
-      out_first[i + k] = uint32_t(produced + ctx->h_first[k]);
-    }
-    if (kept) {
+      if ((e = hipMemcpyAsync(s.d_bytes, s.h_bytes, bytes, hipMemcpyHostToDevice, st)) !=
+            hipSuccess ||
+          (e = hipMemcpyAsync(s.d_offs, s.h_offs, size_t(cnt) * 8, hipMemcpyHostToDevice,
+                              st)) != hipSuccess ||
+          (e = hipMemcpyAsync(s.d_lens, s.h_lens, size_t(cnt) * 2, hipMemcpyHostToDevice,
+                              st)) != hipSuccess ||
+          (e = hipMemcpyAsync(ctx->d_first, ctx->h_first, sizeof(uint32_t) * (cnt + 1),
+                              hipMemcpyHostToDevice, st)) != hipSuccess) {
+        return status_of(e);
+      }
+      rc = tulips_csum_segment_frames_planned(s.d_bytes, s.d_offs, s.d_lens, cnt, mss,
+                                              ctx->d_first, ctx->d_seg_out, out_stride, room,
+                                              ctx->d_seg_lens, st);
+      if (rc != TULIPS_STATUS_OK) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+      }
       if ((e = hipMemcpyAsync(out_base + produced * out_stride, ctx->d_seg_out,
-                              uint64_t(kept) * out_stride, hipMemcpyDeviceToHost, st)) !=
+                              uint64_t(room) * out_stride, hipMemcpyDeviceToHost, st)) !=
             hipSuccess ||
-          (e = hipMemcpyAsync(out_lengths + produced, ctx->d_seg_lens,
-                              uint64_t(kept) * 2, hipMemcpyDeviceToHost, st)) !=
-            hipSuccess ||
+          (e = hipMemcpyAsync(out_lengths + produced, ctx->d_seg_lens, uint64_t(room) * 2,
+                              hipMemcpyDeviceToHost, st)) != hipSuccess ||
           (e = hipStreamSynchronize(st)) != hipSuccess) {
         return status_of(e);
       }
