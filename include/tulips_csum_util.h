@@ -33,7 +33,11 @@ extern "C" {
                                        `group` 9 (unroll 6..8): the
                                        tail-shaped cut, the last `sps` %
                                        (0 = 12) of the arena in ranges of
-                                       unroll / 2 rows (measured variant) */
+                                       unroll / 2 rows (measured variant);
+                                       `group` 10 (unroll 6..8): the uniform
+                                       cut with each quarter of the ranges at
+                                       instruction priority 3..0 (measured
+                                       variant) */
 
 /* Explicit kernel geometry. Zero fields pick the library default. */
 typedef struct tulips_csum_tuning

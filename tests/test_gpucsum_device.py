@@ -186,9 +186,9 @@ def test_default_crossover_frames_side(burst):
 @needs_harness
 @pytest.mark.gpu
 def test_default_crossover_bytes_side(oracle):
-    """Jumbo frames (9,014 B): a burst of 20 frames is past the bytes limit
-    (180 KB > 145 KB) and goes to the GPU, a burst of 12 (108 KB) stays on
-    the CPU; corrupted frames are dropped either way."""
+    """Jumbo frames (9,014 B): fewer than 96 frames but past the bytes limit
+    (145 KB) goes to the GPU, 12 of them (108 KB) stay on the CPU; corrupted
+    frames are dropped either way."""
     from test_frames import make_frame
     rng = np.random.default_rng(96)
     frames = [bytearray(make_frame(oracle, rng, 8960)) for _ in range(120)]
@@ -202,10 +202,29 @@ def test_default_crossover_bytes_side(oracle):
     assert lens[0] > 9000
     exp, _, bad_l4 = expected_forwarded(oracle.validate_frames(arena, offs, lens), 3)
     assert bad_l4 == len(range(0, 120, 7))
-    for burst, cpu_bursts in ((20, 0), (12, 10)):
+    from tulips_amd import csum
+    for burst in (12, 128):
         fwd, st = run_default_crossover(arena, offs, lens, burst)
         np.testing.assert_array_equal(fwd, exp)
-        assert int(st[5]) == cpu_bursts and int(st[4]) == 120 // burst - cpu_bursts
+        # the decorator's flushes: `burst` frames or a full staging arena
+        # (max(burst x 2 KiB, 128 KiB), frames 16 B-aligned), each sent to
+        # the CPU or the GPU by the crossover
+        cap, used, cur, cpu, gpu = max(burst * 2048, 1 << 17), 0, [], 0, 0
+        for ln in list(lens) + [None]:
+            if ln is None or len(cur) == burst or used + int(ln) > cap:
+                if cur:
+                    if csum.lib.tulips_csum_burst_prefers_cpu(len(cur), sum(cur)):
+                        cpu += 1
+                    else:
+                        gpu += 1
+                used, cur = 0, []
+            if ln is not None:
+                cur.append(int(ln))
+                used = (used + int(ln) + 15) // 16 * 16
+        assert (int(st[4]), int(st[5])) == (gpu, cpu)
+        # 12 jumbo frames (108 KB) stay on the CPU; 128-frame bursts flush
+        # at 29 frames (261 KB, past the bytes limit) and go to the GPU
+        assert (cpu, gpu) == ((10, 0) if burst == 12 else (1, 4))
 
 
 @needs_harness

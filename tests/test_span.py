@@ -28,7 +28,9 @@ DEV = "cuda:0"
 # default is 7 chunks per lane (28 KiB ranges).
 GEOMS = ((4, 0), (5, 0), (6, 0), (7, 7), (7, 0), (8, 0),
          # the tail-shaped cut (group 9; third entry: tail percent, 0 = 12)
-         (7, 9), (8, 9, 50), (6, 9, 3))
+         (7, 9), (8, 9, 50), (6, 9, 3),
+         # ranges prioritised by quarter (group 10, the r05 ZIPF experiment)
+         (7, 10), (6, 10))
 
 
 @pytest.fixture(scope="module", autouse=True)

@@ -257,7 +257,7 @@ launch_packed(const VarSegs& segs, const LaunchArgs& a, hipStream_t stream)
   return hipGetLastError();
 }
 
-template<int U>
+template<int U, bool PRIO = false>
 hipError_t
 launch_span_u(const SpanArgs& sp, hipStream_t stream)
 {
@@ -267,8 +267,13 @@ launch_span_u(const SpanArgs& sp, hipStream_t stream)
     return hipErrorInvalidValue;
   }
   (void)hipGetLastError();
-  hipLaunchKernelGGL((csum_span_kernel<U>), dim3(uint32_t(ranges)), dim3(256), 0, stream, sp,
-                     NoProbe{});
+  if constexpr (PRIO) {
+    hipLaunchKernelGGL((csum_span_kernel<U, NoProbe, 8, 1024, U / 3, true, 256, 0, true>),
+                       dim3(uint32_t(ranges)), dim3(256), 0, stream, sp, NoProbe{});
+  } else {
+    hipLaunchKernelGGL((csum_span_kernel<U>), dim3(uint32_t(ranges)), dim3(256), 0, stream,
+                       sp, NoProbe{});
+  }
   return hipGetLastError();
 }
 
@@ -370,7 +375,7 @@ bool
 span_geometry_ok(int u, int group)
 {
   return ((group == 0 || group == 7) && u >= 4 && u <= 8) ||
-         (group == 9 && u >= 6 && u <= 8);
+         ((group == 9 || group == 10) && u >= 6 && u <= 8);
 }
 
 hipError_t
@@ -402,6 +407,14 @@ launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
       case 6: return launch_span_tail<6>(sp, pct, stream);
       case 7: return launch_span_tail<7>(sp, pct, stream);
       case 8: return launch_span_tail<8>(sp, pct, stream);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (a.group == 10) { // measurement option: ranges prioritised by quarter
+    switch (a.unroll) {
+      case 6: return launch_span_u<6, true>(sp, stream);
+      case 7: return launch_span_u<7, true>(sp, stream);
+      case 8: return launch_span_u<8, true>(sp, stream);
       default: return hipErrorInvalidValue;
     }
   }

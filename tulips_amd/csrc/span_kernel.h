@@ -107,8 +107,14 @@ struct NoProbe
 // one by tools/probe_span_tail.py): ranges k < p.k1 hold U rows, the last
 // ones (dispatched last) TR rows, so the final workgroups on each CU finish
 // their data sooner and their tails overlap. TR = 0: every range U rows.
+// PRIO (the one ZIPF experiment, tools/probe_span_prio.py):
+// a launch is one generation of workgroups whose post-data phases bunch in
+// its last ~2 us; the waves of ranges in the first quarter of the arena run
+// at instruction priority 3, the next quarters 2, 1, 0, so on a CU the
+// earlier ranges issue (and get) their loads first and finish while later
+// ones still stream.
 template<int U, class Probe = NoProbe, uint32_t XC = 8, uint32_t NWIN = 1024, int MH = U / 3,
-         bool XCHG = true, uint32_t TB = 256, int TR = 0>
+         bool XCHG = true, uint32_t TB = 256, int TR = 0, bool PRIO = false>
 __global__ __launch_bounds__(TB, 7) void
 csum_span_kernel(SpanArgs p, Probe pr)
 {
@@ -128,6 +134,16 @@ csum_span_kernel(SpanArgs p, Probe pr)
   const uint32_t t = threadIdx.x, lane = t & 63u;
   const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t k = xcd_block_c<XC>(blockIdx.x, gridDim.x);
+  if constexpr (PRIO) {
+    const uint32_t q = uint32_t(uint64_t(k) * 4u / gridDim.x); // (wave-uniform)
+    if (q == 0) {
+      __builtin_amdgcn_s_setprio(3);
+    } else if (q == 1) {
+      __builtin_amdgcn_s_setprio(2);
+    } else if (q == 2) {
+      __builtin_amdgcn_s_setprio(1);
+    }
+  }
   pr.mark(k, w, lane, 0);
 
   const uintptr_t b = reinterpret_cast<uintptr_t>(p.base);
