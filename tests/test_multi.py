@@ -460,6 +460,40 @@ def test_mctx_rss_device_matches_host_and_reference(oracle, key_i, init, ndev, l
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ndev", [2, 5])
+def test_mctx_rss_device_staged_matches_peer(oracle, ndev):
+    """with staging forced (tulips_csum_mctx_set_peer_mode),
+    each device's packed run, offsets and lengths travel through the
+    page-locked bounce and its flags come home the same way: flags, device_of
+    and counters equal the peer-DMA form's and the oracle's."""
+    import torch
+    from test_frames import counters_of
+    from test_rss import rss_fixture
+    from tulips_amd import csum
+    fx = rss_fixture()
+    key = fx["key_3"].tobytes()
+    rng = np.random.default_rng(300 + ndev)
+    arena, offs, lens, _ = _rss_frames(oracle, rng, fx)
+    table = (np.arange(128) * 7 % ndev).astype(np.uint16)
+    exp = oracle.validate_frames(arena, offs, lens)
+    a, o, ln = _dev(arena), _dev(offs.view(np.int64)), _dev(lens.view(np.int16))
+    got = {}
+    for staged in (False, True):
+        with csum.MultiContext([0] * ndev, chunk_bytes=1 << 20) as m:
+            m.set_peer_mode(staged)
+            for rep in range(2):
+                cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
+                fl, dv = m.validate_frames_rss_device(a, o, ln, key, table, counters=cnt)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(fl.cpu().numpy(), exp)
+                np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),
+                                              counters_of(exp))
+            got[staged] = (dv.cpu().numpy(), m.bounds())
+    np.testing.assert_array_equal(got[True][0], got[False][0])
+    np.testing.assert_array_equal(got[True][1], got[False][1])
+
+
+@pytest.mark.gpu
 def test_mctx_rss_device_alternating_streams(oracle):
     """Calls of one context alternated between two streams with no host
     synchronisation in between: each call overwrites the

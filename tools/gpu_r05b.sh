@@ -16,7 +16,7 @@ step() {  # step <name> <seconds> <cmd...>
   if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
 }
 step new 420 python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpucsum_device.py tests/test_segment.py tests/test_dropin.py tests/test_span.py tests/test_frames.py::test_frames_tuned_rejects_bad_geometry
+  tests/test_gpucsum_device.py tests/test_segment.py tests/test_dropin.py tests/test_span.py tests/test_multi.py tests/test_frames.py::test_frames_tuned_rejects_bad_geometry
 step bench 400 python -u bench.py --gpus 1 --steps 20 --warmup 5
 step suite 700 python -u -m pytest -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -m gpu tests
 step smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()"

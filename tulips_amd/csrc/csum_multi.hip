@@ -1452,24 +1452,59 @@ validate_rss_device(tulips_csum_mctx* m, int sdev, const uint8_t* base, const ui
     } else {
       // its packed frames, offsets (within the run), lengths, then flags
       const uint64_t m_len = 8ull * cnt, m_fl = (m_len + 2ull * cnt + 15) & ~uint64_t(15);
+      // no peer path to the source (or staging forced): the run, offsets and
+      // lengths go source HBM -> page-locked bounce (stage stream, source
+      // device) -> this device's HBM, the flags back the same way, as the
+      // device-resident batches do (spread_device)
+      const bool staged = !peer_reachable(m, d, sdev);
+      const uint64_t run16 = (run_bytes[k] + 15) & ~uint64_t(15);
+      const uint64_t off16 = (8ull * cnt + 15) & ~uint64_t(15);
       if ((e = grow(d, reinterpret_cast<void**>(&d.buf), &d.buf_bytes, run_bytes[k] + 64)) !=
             hipSuccess ||
           (e = grow(d, reinterpret_cast<void**>(&d.meta), &d.meta_bytes, m_fl + cnt + 16)) !=
             hipSuccess ||
+          (staged && (e = ensure_staging(d, sdev, run16 + off16 + 2ull * cnt + 16,
+                                         cnt + 16)) != hipSuccess) ||
           (e = hipSetDevice(d.device)) != hipSuccess ||
           (e = hipStreamWaitEvent(d.copy, routed, 0)) != hipSuccess ||
-          (d.used && (e = hipStreamWaitEvent(d.copy, d.done, 0)) != hipSuccess)) {
+          (d.used && (e = hipStreamWaitEvent(d.copy, d.done, 0)) != hipSuccess) ||
+          (d.sdone_used && (e = hipStreamWaitEvent(d.copy, d.sdone, 0)) != hipSuccess)) {
         break;
       }
-      // peer DMA over xGMI (the HIP runtime stages through host memory
-      // where the two devices have no peer path)
-      if ((e = hipMemcpyPeerAsync(d.buf, d.device, r.packed + starts.at[k], sdev, run_bytes[k],
-                                  d.copy)) != hipSuccess ||
-          (e = hipMemcpyPeerAsync(d.meta, d.device, r.poff + b0, sdev, 8ull * cnt, d.copy)) !=
-            hipSuccess ||
-          (e = hipMemcpyPeerAsync(d.meta + m_len, d.device, r.plen + b0, sdev, 2ull * cnt,
-                                  d.copy)) != hipSuccess) {
-        break;
+      if (!staged) {
+        // peer DMA over xGMI
+        if ((e = hipMemcpyPeerAsync(d.buf, d.device, r.packed + starts.at[k], sdev,
+                                    run_bytes[k], d.copy)) != hipSuccess ||
+            (e = hipMemcpyPeerAsync(d.meta, d.device, r.poff + b0, sdev, 8ull * cnt,
+                                    d.copy)) != hipSuccess ||
+            (e = hipMemcpyPeerAsync(d.meta + m_len, d.device, r.plen + b0, sdev, 2ull * cnt,
+                                    d.copy)) != hipSuccess) {
+          break;
+        }
+      } else {
+        uint8_t* hb = d.hb[0];
+        if ((e = hipSetDevice(sdev)) != hipSuccess ||
+            (e = hipStreamWaitEvent(d.stage, routed, 0)) != hipSuccess ||
+            (d.bfree_used[0] && (e = hipStreamWaitEvent(d.stage, d.bfree[0], 0)) != hipSuccess) ||
+            (run_bytes[k] && (e = hipMemcpyAsync(hb, r.packed + starts.at[k], run_bytes[k],
+                                                 hipMemcpyDeviceToHost, d.stage)) != hipSuccess) ||
+            (e = hipMemcpyAsync(hb + run16, r.poff + b0, 8ull * cnt, hipMemcpyDeviceToHost,
+                                d.stage)) != hipSuccess ||
+            (e = hipMemcpyAsync(hb + run16 + off16, r.plen + b0, 2ull * cnt,
+                                hipMemcpyDeviceToHost, d.stage)) != hipSuccess ||
+            (e = hipEventRecord(d.staged[0], d.stage)) != hipSuccess ||
+            (e = hipSetDevice(d.device)) != hipSuccess ||
+            (e = hipStreamWaitEvent(d.copy, d.staged[0], 0)) != hipSuccess ||
+            (run_bytes[k] && (e = hipMemcpyAsync(d.buf, hb, run_bytes[k], hipMemcpyHostToDevice,
+                                                 d.copy)) != hipSuccess) ||
+            (e = hipMemcpyAsync(d.meta, hb + run16, 8ull * cnt, hipMemcpyHostToDevice,
+                                d.copy)) != hipSuccess ||
+            (e = hipMemcpyAsync(d.meta + m_len, hb + run16 + off16, 2ull * cnt,
+                                hipMemcpyHostToDevice, d.copy)) != hipSuccess ||
+            (e = hipEventRecord(d.bfree[0], d.copy)) != hipSuccess) {
+          break;
+        }
+        d.bfree_used[0] = true;
       }
       if ((e = ensure_events(d, 1)) != hipSuccess || (e = hipSetDevice(d.device)) != hipSuccess ||
           (e = hipEventRecord(d.ev[0], d.copy)) != hipSuccess ||
@@ -1479,8 +1514,29 @@ validate_rss_device(tulips_csum_mctx* m, int sdev, const uint8_t* base, const ui
       rc = tulips_csum_validate_frames(d.buf, reinterpret_cast<const uint64_t*>(d.meta),
                                        reinterpret_cast<const uint16_t*>(d.meta + m_len), cnt,
                                        d.meta + m_fl, nullptr, d.comp);
-      if (rc == TULIPS_STATUS_OK) {
+      if (rc == TULIPS_STATUS_OK && !staged) {
         e = hipMemcpyPeerAsync(r.rflags + b0, sdev, d.meta + m_fl, d.device, cnt, d.comp);
+      }
+      if (rc == TULIPS_STATUS_OK && staged && e == hipSuccess) {
+        // the flags home through the results bounce; the caller's stream
+        // waits for the stage stream's copy (sdone) instead of `done`
+        if ((e = hipMemcpyAsync(d.hres, d.meta + m_fl, cnt, hipMemcpyDeviceToHost, d.comp)) ==
+              hipSuccess &&
+            (e = hipEventRecord(d.done, d.comp)) == hipSuccess &&
+            (e = hipEventRecord(d.rdone, d.comp)) == hipSuccess &&
+            (e = hipSetDevice(sdev)) == hipSuccess &&
+            (e = hipStreamWaitEvent(d.stage, d.rdone, 0)) == hipSuccess &&
+            (e = hipMemcpyAsync(r.rflags + b0, d.hres, cnt, hipMemcpyHostToDevice, d.stage)) ==
+              hipSuccess &&
+            (e = hipEventRecord(d.sdone, d.stage)) == hipSuccess) {
+          d.used = true;
+          d.sdone_used = true;
+          fin[k] = d.sdone;
+        }
+        if (e != hipSuccess) {
+          break;
+        }
+        continue;
       }
     }
     if (rc != TULIPS_STATUS_OK && e == hipSuccess) {
