@@ -297,8 +297,7 @@ def self_launch(args):
 def progress(stage):
     """One stderr line per bench stage (stdout carries only the JSON line):
     where a long run is, and where it stopped if it dies."""
-    print(f"[bench {time.strftime('%H:%M:%S')} pid {os.getpid()}] {stage}", file=sys.stderr,
-          flush=True)
+    print(f"[bench {time.strftime('%H:%M:%S')}] {stage}", file=sys.stderr, flush=True)
 
 
 def main():
@@ -640,13 +639,17 @@ def extras_in_child():
     the extras, never the headline line. Returns the child's extras dict, or
     an error entry with its exit status."""
     import subprocess
+    # the child's progress lines and native/faulthandler stacks are kept and
+    # shown only if it fails (the driver keeps the tail of the output, where
+    # the JSON line's summary should be)
     r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--extras-child"],
-                       stdout=subprocess.PIPE, text=True, cwd=ROOT)
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=ROOT)
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     if r.returncode == 0 and lines:
         return json.loads(lines[-1])["extras"]
+    sys.stderr.write(r.stderr[-4000:])
     return {"error": f"extras process exited with status {r.returncode}",
-            "stdout_tail": r.stdout[-500:]}
+            "stdout_tail": r.stdout[-500:], "stderr_tail": r.stderr[-1500:]}
 
 
 def extras_child():
