@@ -75,6 +75,42 @@ def test_self_launched_four_ranks_on_one_gpu():
     assert mg["library_scatter_from_gpu0"]["kernel_only"]["parity"] == "ok"
     for leg in ("exchange_overlapped", "scatter_from_gpu0", "zipf_byte_balanced"):
         assert mg[leg].get("parity") == "ok", (leg, mg[leg])
+    # §8e host-start form: every rank's shard from page-locked host memory
+    hs = line["host_start"]
+    assert hs["parity"] == "ok", hs
+    assert hs["aggregate_GiBps"] > 0 and hs["bytes_per_rank"] == 16 * 65536 * 1500
+    # the summary is the line's last key (the driver keeps the output's tail)
+    assert list(line)[-1] == "summary"
+    assert line["summary"]["host_start_GiBps"] == hs["aggregate_GiBps"]
+
+
+def test_summary_of_picks_the_judged_figures():
+    """bench.summary_of: per config the serial, 4-branch and read-ceiling
+    fractions with parity, from the line's roofline and extras."""
+    sys.path.insert(0, ROOT)
+    import bench
+    line = {"value": 6000.0, "parity": "ok", "roofline": {"frac": 0.77},
+            "host_start": {"aggregate_GiBps": 380.5},
+            "extras": {"F1500": {"frac_of_peak": 0.76, "pipeline": {"frac_of_peak": 0.89},
+                                 "parity": "ok"},
+                       "stream_read_F1500_batch": {"frac_of_peak": 0.80},
+                       "F9000": {"frac_of_peak": 0.89, "pipeline": {"frac_of_peak": 0.93},
+                                 "read_same_bytes": {"frac_of_peak": 0.88}, "parity": "ok"},
+                       "ZIPF": {"frac_of_peak": 0.49, "pipeline": {"frac_of_peak": 0.64},
+                                "read_same_bytes": {"frac_of_peak": 0.70},
+                                "parity": "MISMATCH"},
+                       "segment_TSO_64K_mss1460": {"planned": {"frac_of_peak": 0.69}}}}
+    s = bench.summary_of(line)
+    assert s["F1500"] == {"serial_frac": 0.77, "branches4_frac": 0.89,
+                          "read_same_bytes_frac": 0.80, "parity": "ok"}
+    assert s["F9000"]["serial_frac"] == 0.89 and s["F9000"]["read_same_bytes_frac"] == 0.88
+    assert s["ZIPF"]["parity"] == "MISMATCH"
+    assert s["segment_planned_serial_frac"] == 0.69 and s["host_start_GiBps"] == 380.5
+    assert len(json.dumps(s)) < 900      # fits the driver's stored tail
+    # extras missing (N > 1, or the child failed): no crash, configs None
+    s = bench.summary_of({"value": 1.0, "parity": "ok", "roofline": {"frac": 0.7},
+                          "extras": {"error": "x"}})
+    assert s["F9000"] is None and s["F1500"] is None
 
 
 def test_branch_count_follows_step_count():
