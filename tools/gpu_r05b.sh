@@ -1,6 +1,6 @@
 # round-5 session b: the decorator / segmentation / drop-in GPU tests, the
-# driver's bench command, the whole GPU suite, smoke, then a rocprofv3
-# kernel-trace + stats pass of the driver's command. Every step has its own
+# driver's bench command, the whole GPU suite, smoke, then the ZIPF
+# priority A/B (tools/probe_span_prio.py). Every step has its own
 # limit; the first failure ends the call.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -20,5 +20,4 @@ step new 420 python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeo
 step bench 400 python -u bench.py --gpus 1 --steps 20 --warmup 5
 step suite 700 python -u -m pytest -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -m gpu tests
 step smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()"
-step rocprof 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
 step span_prio 300 python -u tools/probe_span_prio.py
