@@ -417,8 +417,9 @@ int tulips_csum_segment_frames(const uint8_t* in_base,
  * outputs, limits and semantics as tulips_csum_segment_frames (segments
  * j >= min(first[n], out_capacity) are not written). A segment whose frame's
  * header disagrees with the plan (more segments planned than its payload
- * makes) gets length 0; reads never leave the frames, writes never leave
- * out_capacity slots. Needs no per-stream state (capturable as is).
+ * makes, or a frame planned with none) gets length 0; reads never leave the
+ * frames, writes never leave out_capacity slots. Needs no per-stream state
+ * (capturable as is).
  */
 int tulips_csum_segment_frames_planned(const uint8_t* in_base, const uint64_t* in_offsets,
                                        const uint16_t* in_lengths, uint32_t n, uint32_t mss,

@@ -730,7 +730,9 @@ segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
       F.lo = F.fa & ~uintptr_t(15);
       F.hi = F.flen ? (F.fa + F.flen - 1) & ~uintptr_t(15) : F.lo;
       const uint32_t k = j - pre[f];
-      const bool inside = pre[f] <= j && f < n;
+      // (a plan with a frame of no segments, which the rule never makes, can
+      // put a block's last segments past the window: those get length 0)
+      const bool inside = pre[f] <= j && j < pre[f + 1];
       int lv = lane;
       asm volatile("" : "+v"(lv));
       if (inside) {
