@@ -661,7 +661,7 @@ segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
   __shared__ uint32_t pre[PW + 1];
   __shared__ uint64_t fadr[PW];
   __shared__ uint32_t flen[PW];
-  __shared__ uint32_t total_s;
+  __shared__ uint32_t total_s, f0_s;
   const uint32_t tid = threadIdx.x;
   const int lane = int(tid) & (G - 1);
   const uint32_t sub = tid / G;
@@ -707,9 +707,13 @@ segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
       pre[tid] = p;
       fadr[tid] = b0 + o;
       flen[tid] = l;
+      // the window index of jb's frame (the last entry at or below jb), where
+      // every subgroup's scan starts
+      const uint64_t at_or_below = __ballot(p <= jb);
       if (tid == 0) {
         pre[PW] = pend;
         total_s = total;
+        f0_s = at_or_below ? 63u - uint32_t(__builtin_clzll(at_or_below)) : 0u;
       }
     }
     __syncthreads();
@@ -719,7 +723,7 @@ segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
     }
     const uint32_t j = jb + sub;
     if (j < total) {
-      uint32_t f = 0; // pre[f] <= j < pre[f + 1] within the window
+      uint32_t f = f0_s; // pre[f] <= j < pre[f + 1] within the window
 #pragma unroll 1
       while (f + 1 < PW && pre[f + 1] <= j) {
         ++f;
