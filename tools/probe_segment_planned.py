@@ -81,6 +81,9 @@ def main():
     forms = {"prologue": (prologue, "R")}
     for k in libs:
         forms[f"planned_{k}"] = (planned(k), k)
+    # (slot bytes past a segment's length are never written: the reference
+    # copy carries the same poison byte there as every timed replay's)
+    bench.poisoner(outs["R"], olen["R"])()
     for i in range(sb):
         prologue(i, stream.cuda_stream)
     torch.cuda.synchronize()
