@@ -746,95 +746,15 @@ segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
         out_lens[j] = 0; // the caller's first[] is not a prefix for this batch
       }
     }
+#ifdef TCS_SEG_LAST_BARRIER
     __syncthreads();
-  }
-}
-
-// Wave-independent form: each wave finds the frames of its own 64 / G
-// segments from its own window (no LDS, no barrier), so a wave never waits
-// for another wave's window round trip nor holds its slot at a block barrier.
-template<int G, int SU>
-__global__ __launch_bounds__(256) void
-segment_planned_wave_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
-                            const uint16_t* __restrict__ lens, uint32_t n, uint32_t mss,
-                            const uint32_t* __restrict__ first, uint8_t* out, uint64_t stride,
-                            uint32_t capacity, uint16_t* __restrict__ out_lens)
-{
-  constexpr uint32_t SW = 64 / G; // segments per wave
-  static_assert(SW + 16 <= PW, "the window holds every frame of a wave's segments");
-  const uint32_t lane64 = threadIdx.x & 63u;
-  const int lane = int(lane64) & (G - 1);
-  const uint32_t sub = lane64 / G;
-  const uint32_t wpb = blockDim.x / 64u;
-  const uint32_t nwaves = gridDim.x * wpb;
-  const uintptr_t b0 = reinterpret_cast<uintptr_t>(base);
-  for (uint32_t wt = xcd_block(blockIdx.x, gridDim.x) * wpb + threadIdx.x / 64u;
-       uint64_t(wt) * SW < capacity; wt += nwaves) {
-    const uint32_t jw = wt * SW;
-    auto load_window = [&](uint32_t w0, uint32_t& p, uint32_t& pend, uint64_t& o, uint32_t& l) {
-      const uint32_t f = w0 + lane64;
-      p = first[min(f, n)];
-      o = offs[min(f, n - 1)];
-      l = lens[min(f, n - 1)];
-      pend = first[min(w0 + PW, n)];
-    };
-    const uint32_t g = uint32_t(uint64_t(jw) * n / capacity);
-    uint32_t w0 = g > PW_BACK ? g - PW_BACK : 0u;
-    uint32_t p, pend;
-    uint64_t o;
-    uint32_t l;
-    load_window(w0, p, pend, o, l);
-    const uint32_t total = min(first[n], capacity);
-    if (jw >= total) {
-      break; // (wave-uniform: the wave's later tiles lie further past the total)
+#else
+    // the window is rewritten only by a next tile: a block with none (the
+    // grid covers the capacity) lets each wave leave as soon as it is done
+    if (jb + gridDim.x * S < capacity) {
+      __syncthreads();
     }
-    const uint32_t jl = min(jw + SW, total) - 1; // the wave's last segment
-    if (!(__shfl(p, 0, 64) <= jw && jl < pend)) {
-      // the window missed: 64-ary search for the frame of jw, then the window there
-      uint32_t lo = 0, hi = n;
-      while (hi - lo > PW - SW - 1) {
-        const uint32_t span = hi - lo;
-        const uint32_t v = first[lo + uint32_t(uint64_t(span) * lane64 / 64)];
-        const uint64_t m = __ballot(v <= jw);
-        const uint32_t t = m ? 63u - uint32_t(__builtin_clzll(m)) : 0u;
-        const uint32_t nlo = lo + uint32_t(uint64_t(span) * t / 64);
-        hi = t == 63 ? hi : lo + uint32_t(uint64_t(span) * (t + 1) / 64);
-        lo = nlo;
-      }
-      w0 = lo;
-      load_window(w0, p, pend, o, l);
-    }
-    // each subgroup's frame: the last window entry at or below its segment
-    const uint32_t j = jw + sub;
-    uint32_t f = 0;
-#pragma unroll
-    for (uint32_t s2 = 0; s2 < SW; ++s2) {
-      const uint64_t m = __ballot(p <= jw + s2);
-      const uint32_t fs = m ? 63u - uint32_t(__builtin_clzll(m)) : 0u;
-      f = sub == s2 ? fs : f;
-    }
-    const uint32_t pf = __shfl(p, int(f), 64);
-    const uint32_t pn = __shfl(p, int(min(f + 1u, 63u)), 64);
-    const uint32_t pf1 = f == 63u ? pend : pn;
-    const uint32_t olo = __shfl(uint32_t(o), int(f), 64);
-    const uint32_t ohi = __shfl(uint32_t(o >> 32), int(f), 64);
-    const uint32_t fl = __shfl(l, int(f), 64);
-    if (j < total) {
-      SegFrame F;
-      F.fa = b0 + ((uint64_t(ohi) << 32) | olo);
-      F.flen = fl;
-      F.lo = F.fa & ~uintptr_t(15);
-      F.hi = F.flen ? (F.fa + F.flen - 1) & ~uintptr_t(15) : F.lo;
-      const uint32_t k = j - pf;
-      int lv = lane;
-      asm volatile("" : "+v"(lv));
-      if (pf <= j && j < pf1) {
-        build_segment<G, SU, false>(F, k, j, mss, out, stride, out_lens, lv,
-                                    int(lane64) & ~(G - 1));
-      } else if (lane == 0) {
-        out_lens[j] = 0; // the caller's first[] is not a prefix for this batch
-      }
-    }
+#endif
   }
 }
 
@@ -1062,21 +982,15 @@ tulips_csum_segment_frames_planned(const uint8_t* in_base, const uint64_t* in_of
   const uint64_t want = (uint64_t(out_capacity) + per_block - 1) / per_block;
   const uint32_t blocks = uint32_t(want > 65535 ? 65535 : want);
   (void)hipGetLastError();
-#ifdef TCS_PLANNED_WAVE
-#define TCS_PLANNED segment_planned_wave_kernel
-#else
-#define TCS_PLANNED segment_planned_kernel
-#endif
   if (small) {
-    hipLaunchKernelGGL((TCS_PLANNED<16, 6>), dim3(blocks), dim3(256), 0, st,
+    hipLaunchKernelGGL((segment_planned_kernel<16, 6>), dim3(blocks), dim3(256), 0, st,
                        in_base, in_offsets, in_lengths, n, mss, first, out_base, out_stride,
                        out_capacity, out_lengths);
   } else {
-    hipLaunchKernelGGL((TCS_PLANNED<64, 6>), dim3(blocks), dim3(256), 0, st,
+    hipLaunchKernelGGL((segment_planned_kernel<64, 6>), dim3(blocks), dim3(256), 0, st,
                        in_base, in_offsets, in_lengths, n, mss, first, out_base, out_stride,
                        out_capacity, out_lengths);
   }
-#undef TCS_PLANNED
   return hipGetLastError() == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
 }
 
