@@ -3,8 +3,8 @@
 # rocprofv3 evidence for the bench workload - kernel-trace + stats (timing
 # agreement) and separate --pmc passes (FETCH_SIZE, WRITE_SIZE) for HBM
 # traffic - and the world-8 rehearsal (8 gloo ranks sharing GPU 0, every
-# N>1 leg at world 8). Summarise here afterwards with
-#   python tools/pmc_traffic.py gpurun_out/prof_$TAG profiles $TAG
+# N>1 leg at world 8). The summaries (tools/pmc_traffic.py) are made on the
+# box under gpurun_out/prof_$TAG/summary; copy them into profiles/ here.
 # Each GPU step has its own time limit; a crash / abort / timeout ends the
 # script (pytest's rc 1 = "tests failed" is reported and also ends it).
 set -u
@@ -48,6 +48,12 @@ python tools/merge_csv.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_fet
 python tools/merge_csv.py $OUT/pmc_write/run_counter_collection.csv $OUT/pmc_write_h/run_counter_collection.csv $OUT/pmc_write_x/run_counter_collection.csv
 rm -rf $OUT/stats_h $OUT/stats_x $OUT/pmc_fetch_h $OUT/pmc_fetch_x $OUT/pmc_write_h $OUT/pmc_write_x
 python tools/trace_bursts.py $OUT/stats/run_kernel_trace.csv --all > $OUT/bursts_all.jsonl
+# summaries on the box (the raw traces would push gpurun_out past what gpurun
+# copies back, 64 MiB): profiles-ready files under $OUT/summary, raw CSVs dropped
+mkdir -p $OUT/summary
+python tools/pmc_traffic.py $OUT $OUT/summary $TAG > $OUT/summary/pmc_traffic.log 2>&1 || true
+rm -f $OUT/stats/run_kernel_trace.csv $OUT/pmc_fetch/run_counter_collection.csv \
+      $OUT/pmc_write/run_counter_collection.csv
 # (no launcher: bench.py starts torch.distributed.run itself, as under the
 # driver's `python bench.py --gpus 8`)
 [ -n "${PROF_ONLY:-}" ] && { echo "== done (profiles only)"; exit 0; }
