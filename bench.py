@@ -1799,7 +1799,7 @@ def frame_extras(torch, csum, dev, timer):
             solen.data_ptr() + b * nseg * 2, sfirst.data_ptr() + b * (nsf + 1) * 4, st)
     for i in range(sb):
         fseg(i, torch.cuda.current_stream().cuda_stream)
-    t = timer(fseg, 32, poison=poisoner(sout, solen, sfirst))
+    t = timer(fseg, 32, replays=3, poison=poisoner(sout, solen, sfirst))
     tp = pipe_times(timer, fseg, 32, poison=poisoner(sout, solen, sfirst))
     moved = nsf * sflen + nseg * (54 + mss)       # read super-frames + write segments
     so = torch.arange(nseg, dtype=torch.int64, device=dev) * ostride
@@ -1836,7 +1836,7 @@ def frame_extras(torch, csum, dev, timer):
         segp(sa.data_ptr() + b * nsf * sslot, soffs.data_ptr(), slens.data_ptr(), nsf, mss,
              dplan.data_ptr(), sout.data_ptr() + b * nseg * ostride, ostride, nseg,
              solen.data_ptr() + b * nseg * 2, st)
-    t = timer(fsegp, 32, poison=poisoner(sout, solen))
+    t = timer(fsegp, 32, replays=3, poison=poisoner(sout, solen))
     okp = plan_ok and bool(torch.equal(sout, ref_out)) and bool(torch.equal(solen, ref_len))
     tp = pipe_times(timer, fsegp, 32, poison=poisoner(sout, solen))
     okp = okp and bool(torch.equal(sout, ref_out)) and bool(torch.equal(solen, ref_len))
@@ -1844,6 +1844,7 @@ def frame_extras(torch, csum, dev, timer):
         moved, t, kernel="segment_planned_kernel<16,6> (frames found from the caller's "
                          "first[], headers parsed in the segment kernel, no prologue)",
         entry="tulips_csum_segment_frames_planned",
+        traffic=read_traffic("segment_TSO_64K_mss1460_planned"),
         segments_per_s=round(nseg / t / 1e6, 2) * 1e6, pipeline=pipe_entry(moved, tp),
         parity="ok" if okp else "MISMATCH")
     del sa, sv, sout, ref_out, ref_len
