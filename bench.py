@@ -71,6 +71,9 @@ def parse():
                         "2 below 128 steps, else 16 (four per hardware queue, "
                         "GPU_MAX_HW_QUEUES being 4 on the box; "
                         "profiles/probe_branches_r03.txt, profiles/probe_graph_k_r04.txt)")
+    p.add_argument("--main-branch", type=int, default=0, choices=(0, 1),
+                   help="1: the timed graph's capture stream carries one of its branches "
+                        "(one fork and join fewer per replay)")
     p.add_argument("--start-delay-us", type=int, default=200,
                    help="a one-wave GPU sleep queued before every timed region's start "
                         "event (not timed), so the region starts on the GPU only once the "
@@ -373,7 +376,10 @@ def main():
     graph = None
     if not args.eager:
         graph = torch.cuda.CUDAGraph()
-        side = [torch.cuda.Stream() for _ in range(args.streams)]
+        # --main-branch: the capture stream itself is one of the branches, so
+        # the graph forks to and joins from streams - 1 side streams
+        nside = args.streams - 1 if args.main_branch else args.streams
+        side = [torch.cuda.Stream() for _ in range(nside)]
         with torch.cuda.graph(graph):
             main = torch.cuda.current_stream()
             # Steps round-robin over `streams` independent branches of the
@@ -382,10 +388,11 @@ def main():
             # whole batch. streams=1 is a single serial chain.
             for sd in side:
                 sd.wait_stream(main)
+            lanes = ([main] if args.main_branch else []) + side
             for i in range(args.steps):
                 b = i % NBATCH
                 fixed(base + b * batch_bytes, SEG, SEG, None, None, None,
-                      optr + b * NSEG * 2, NSEG, 0, side[i % len(side)].cuda_stream)
+                      optr + b * NSEG * 2, NSEG, 0, lanes[i % len(lanes)].cuda_stream)
             for sd in side:
                 main.wait_stream(sd)
         graph.replay()
@@ -531,6 +538,7 @@ def main():
             "parallelism": f"shard{world}",
             "launch": "graph" if graph is not None else "eager",
             "streams": args.streams if graph is not None else 1,
+            "main_branch": bool(args.main_branch),
         },
         "parity": parity,
         "parity_checked": parity_checked,
