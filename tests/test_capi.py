@@ -214,7 +214,7 @@ def test_default_tuning():
                           (csum.KIND_PACKED, 64, 4, 2), (csum.KIND_PACKED, 16, 4, 5),
                           (csum.KIND_PACKED, 8, 4, 1), (csum.KIND_PACKED, 8, 4, 3),
                           (csum.KIND_PACKED, 8, 4, 4), (csum.KIND_SUBGROUP, 8, 4, 0),
-                          (csum.KIND_SUBGROUP, 16, 4, 2), (csum.KIND_SUBGROUP, 32, 3, 0),
+                          (csum.KIND_SUBGROUP, 16, 4, 2), (csum.KIND_SUBGROUP, 32, 5, 0),
                           (7, 16, 4, 0)):
         bad = csum.Tuning(kind=kind, group=g, unroll=u, nontemporal=1, sps=s)
         assert csum.lib.tulips_csum_batch_tuned(FAKE, FAKE, FAKE, None, None, None, FAKE, 4,

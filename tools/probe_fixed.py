@@ -39,7 +39,7 @@ def main():
         csum.fill_splitmix(buf, nb * bb)
         out = torch.empty(nb * N, dtype=torch.uint16, device=dev)
         res, ref = {}, None
-        for rnd in range(3):
+        for rnd in range(int(os.environ.get("ROUNDS", "3"))):
             for (g, u, blk), nt in [(gm, nt) for gm in geoms for nt in nts]:
                 t = csum.Tuning(group=g, unroll=u, nontemporal=nt, block=blk)
 
@@ -57,7 +57,8 @@ def main():
                 if ref is None:
                     ref = o
                 assert np.array_equal(o, ref), (g, u, blk, nt)
-                res.setdefault((g, u, blk, nt), []).append(timer(fn, 64))
+                res.setdefault((g, u, blk, nt), []).append(
+                    timer(fn, bench.SERIAL_LAUNCHES, replays=3))
         for (g, u, blk, nt), ts in res.items():
             tm = float(np.median(ts))
             print(json.dumps({"L": L, "geom": f"g{g}u{u}b{blk}nt{nt}", "us": round(tm * 1e6, 2),

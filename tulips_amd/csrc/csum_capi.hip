@@ -253,6 +253,7 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
     case TULIPS_CSUM_KIND_SUBGROUP:
       return spw == 1 && (((group == 16 || group == 32) &&
                            (unroll == 2 || unroll == 4 || unroll == 8)) ||
+                          (group == 32 && unroll == 3) ||
                           (group == 64 && (unroll == 4 || unroll == 8 || unroll == 12)));
     case TULIPS_CSUM_KIND_PACKED:
       // double-buffered windows only (sps 2)

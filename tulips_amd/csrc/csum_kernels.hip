@@ -331,6 +331,7 @@ dispatch(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
   TCS_CASE(16, 4)
   TCS_CASE(16, 8)
   TCS_CASE(32, 2)
+  TCS_CASE(32, 3)
   TCS_CASE(32, 4)
   TCS_CASE(32, 8)
   TCS_CASE(64, 4)
