@@ -31,6 +31,7 @@ from collections import defaultdict
 # ranges = 390,912 threads), the any-layout packed kernel 8 segments per wave
 # (8,192 waves = 524,288 threads).
 WORKLOADS = [
+    ("csum_kernel<32, 3, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
     ("csum_kernel<32, 4, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F1500"),
     ("csum_kernel<64, 12, true, tulips_amd::(anonymous namespace)::FixedSegs>", None, "F9000"),
     ("csum_span_kernel<7,", 390912, "ZIPF"),

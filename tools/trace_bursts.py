@@ -129,7 +129,7 @@ def main():
         for s in summary.values():
             print(json.dumps(dict(s, summary=True)))
         return
-    needle = args[1] if len(args) > 1 else "csum_kernel<32, 4, true"
+    needle = args[1] if len(args) > 1 else "csum_kernel<32, 3, true"
     for b in bursts(args[0], needle, gap * 1e3):
         print(json.dumps(b))
 

@@ -297,9 +297,13 @@ default_tuning(uint32_t len, bool variable)
   } else if (nch > 256) { // > ~4 KiB: whole wave, 8 chunks in flight per lane
     t.group = 64;
     t.unroll = 8;
-  } else if (nch > 64) {  // ~1-4 KiB (F1500): 32 lanes x 4
+  } else if (nch > 96) {  // ~1.5-4 KiB: 32 lanes x 4
     t.group = 32;
     t.unroll = 4;
+  } else if (nch > 64) {  // ~1-1.5 KiB (F1500): 32 lanes x 3, the 96 chunks a
+    t.group = 32;         // 1500 B segment touches at any alignment in one batch
+    t.unroll = 3;         // with no redundant loads (tools/probe_fixed.py,
+                          // profiles/probe_fixed_r05.txt: 15.73 vs 15.95 us)
   } else {
     t.group = 16;
     t.unroll = 4;
