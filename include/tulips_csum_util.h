@@ -17,7 +17,7 @@ extern "C" {
 #define TULIPS_CSUM_KIND_DEFAULT 0
 #define TULIPS_CSUM_KIND_SUBGROUP 1 /* `group` lanes (16/32/64) per segment,
                                        `unroll` chunks per lane in flight
-                                       (16/32: 2/4/8; 32: 3; 64: 4/8/12) */
+                                       (16/32: 2/4/8; 32: 3; 64: 4/8/9/10/12) */
 #define TULIPS_CSUM_KIND_PACKED 3   /* variable only: one wave per `group`
                                        segments (8/16), their chunks packed
                                        end to end, `unroll` 64-chunk windows

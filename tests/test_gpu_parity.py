@@ -25,7 +25,8 @@ SUB, PCK = csum.KIND_SUBGROUP, csum.KIND_PACKED
 # pick SUBGROUP 16x4 / 32x4 / 64x8 / 64x12 by fixed length and PACKED 8x4
 # (double-buffered) for variable lengths at any offsets.
 # (kind, group, unroll, nontemporal bits, sps)
-SUBGROUP = [(16, 2), (16, 4), (16, 8), (32, 2), (32, 3), (32, 4), (32, 8), (64, 4), (64, 8), (64, 12)]
+SUBGROUP = [(16, 2), (16, 4), (16, 8), (32, 2), (32, 3), (32, 4), (32, 8), (64, 4), (64, 8),
+            (64, 9), (64, 10), (64, 12)]
 GEOMETRIES = [(SUB, g, u, nt, 0) for (g, u) in SUBGROUP for nt in (0, 1, 3)]
 # packed kernel: `group` segments per wave, `unroll` 64-chunk windows per batch
 PACKED = [(8, 2), (8, 4), (16, 2), (16, 4)]
@@ -262,7 +263,7 @@ def test_fixed_lengths_and_base_alignment(oracle, L, base_off):
     arena = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
     exp = oracle.batch(arena[base_off:], stride=stride, fixed_len=L, n=n, mode=MODE_RAW)
     da = d(arena)
-    for g, u in ((16, 2), (16, 8), (32, 2), (32, 3), (32, 8), (64, 4), (64, 12)):
+    for g, u in ((16, 2), (16, 8), (32, 2), (32, 3), (32, 8), (64, 4), (64, 9), (64, 10), (64, 12)):
         t = csum.Tuning(group=g, unroll=u, nontemporal=0, max_blocks=0)
         got = tulips_amd.batch_fixed(da, stride, L, n, tuning=t, base_offset=base_off)
         np.testing.assert_array_equal(u16(got), exp, err_msg=f"g{g} u{u}")

@@ -254,7 +254,8 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
       return spw == 1 && (((group == 16 || group == 32) &&
                            (unroll == 2 || unroll == 4 || unroll == 8)) ||
                           (group == 32 && unroll == 3) ||
-                          (group == 64 && (unroll == 4 || unroll == 8 || unroll == 12)));
+                          (group == 64 && (unroll == 4 || unroll == 8 || unroll == 9 ||
+                                           unroll == 10 || unroll == 12)));
     case TULIPS_CSUM_KIND_PACKED:
       // double-buffered windows only (sps 2)
       return variable && spw == 2 && (group == 8 || group == 16) &&

@@ -336,6 +336,8 @@ dispatch(const Segs& segs, const LaunchArgs& a, hipStream_t stream)
   TCS_CASE(32, 8)
   TCS_CASE(64, 4)
   TCS_CASE(64, 8)
+  TCS_CASE(64, 9)
+  TCS_CASE(64, 10)
   TCS_CASE(64, 12)
 #undef TCS_CASE
   return hipErrorInvalidValue;
