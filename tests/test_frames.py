@@ -581,7 +581,7 @@ def test_generate_fields_arguments_without_gpu():
     assert f(1, 1, 1, 4, None, None, None) == 1               # fields required
 
 
-FRAME_GEOMETRIES = [(16, 4), (16, 6), (16, 8), (8, 8), (8, 16), (32, 4), (64, 2)]
+FRAME_GEOMETRIES = [(16, 4), (16, 6), (16, 8), (8, 8), (8, 16), (32, 3), (32, 4), (64, 2)]
 
 
 @pytest.mark.gpu

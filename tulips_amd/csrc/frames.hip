@@ -494,6 +494,7 @@ dispatch(uint8_t* base, const uint64_t* offs, const uint16_t* lens, uint32_t n,
   TCS_F(16, 8)
   TCS_F(8, 8)
   TCS_F(8, 16)
+  TCS_F(32, 3)
   TCS_F(32, 4)
   TCS_F(64, 2)
 #undef TCS_F
@@ -507,7 +508,7 @@ frame_geometry_ok(int group, int unroll, uint32_t block)
 {
   const int g = group ? group : DEFAULT_G, u = unroll ? unroll : DEFAULT_U;
   const bool geo = (g == 16 && (u == 4 || u == 6 || u == 8)) ||
-                   (g == 8 && (u == 8 || u == 16)) || (g == 32 && u == 4) ||
+                   (g == 8 && (u == 8 || u == 16)) || (g == 32 && (u == 3 || u == 4)) ||
                    (g == 64 && u == 2);
   return geo && (block == 0 || block == 64 || block == 128 || block == 256 || block == 512 ||
                  block == 1024);
