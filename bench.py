@@ -631,8 +631,8 @@ def summary_of(result):
                                  ex.get("F1500", {}).get("parity") == "ok") else "MISMATCH"
     out = {"F1500": f15, "F9000": pick(ex.get("F9000")), "ZIPF": pick(ex.get("ZIPF"))}
     seg = ex.get("segment_TSO_64K_mss1460")
-    if isinstance(seg, dict) and "planned" in seg:
-        out["segment_planned_serial_frac"] = seg["planned"].get("frac_of_peak")
+    if isinstance(seg, dict) and "frac_of_peak" in seg:
+        out["segment_serial_frac"] = seg.get("frac_of_peak")
     hs = result.get("host_start")
     if isinstance(hs, dict) and "aggregate_GiBps" in hs:
         out["host_start_GiBps"] = hs["aggregate_GiBps"]
@@ -1817,12 +1817,12 @@ def frame_extras(torch, csum, dev, timer):
                                    solen[b * nseg:(b + 1) * nseg])
         ok = ok and bool((sfl == 0x0F).all().item()) and \
             int(sfirst[b * (nsf + 1) + nsf].item()) == nseg
-    ex["segment_TSO_64K_mss1460"] = rate_entry(
+    counted = rate_entry(
         moved, t, kernel="seg_prologue_small_kernel + segment_kernel<16,6> "
                          "(16-lane subgroup per output segment)",
-        workload="1024 super-frames of 64,294 B -> 45,056 segments of 1514 B per call",
+        entry="tulips_csum_segment_frames (segment counts computed on the device)",
         segments_per_s=round(nseg / t / 1e6, 2) * 1e6, pipeline=pipe_entry(moved, tp),
-        traffic=read_traffic("segment_TSO_64K_mss1460"),
+        traffic=read_traffic("segment_TSO_64K_mss1460_device_counted"),
         parity="ok" if ok else "MISMATCH")
     # the same calls with the caller's plan (tulips_csum_segment_frames_planned:
     # first[] from the host, as the reference's transport decides the TSO
@@ -1848,13 +1848,17 @@ def frame_extras(torch, csum, dev, timer):
     okp = plan_ok and bool(torch.equal(sout, ref_out)) and bool(torch.equal(solen, ref_len))
     tp = pipe_times(timer, fsegp, 32, poison=poisoner(sout, solen))
     okp = okp and bool(torch.equal(sout, ref_out)) and bool(torch.equal(solen, ref_len))
-    ex["segment_TSO_64K_mss1460"]["planned"] = rate_entry(
+    # the TSO path as the product runs it (the decorator's transmit side and
+    # tulips_csum_segment_frames_host plan on the host): the planned entry;
+    # the device-counted form beside it
+    ex["segment_TSO_64K_mss1460"] = rate_entry(
         moved, t, kernel="segment_planned_kernel<16,6> (frames found from the caller's "
                          "first[], headers parsed in the segment kernel, no prologue)",
-        entry="tulips_csum_segment_frames_planned",
-        traffic=read_traffic("segment_TSO_64K_mss1460_planned"),
+        entry="tulips_csum_segment_frames_planned (plan from tulips_csum_segment_plan_host)",
+        workload="1024 super-frames of 64,294 B -> 45,056 segments of 1514 B per call",
+        traffic=read_traffic("segment_TSO_64K_mss1460"),
         segments_per_s=round(nseg / t / 1e6, 2) * 1e6, pipeline=pipe_entry(moved, tp),
-        parity="ok" if okp else "MISMATCH")
+        parity="ok" if okp else "MISMATCH", device_counted=counted)
     del sa, sv, sout, ref_out, ref_len
 
     # Toeplitz RSS over 16M tuples (12 B in, 4 B out per tuple)

@@ -49,8 +49,8 @@ WORKLOADS = [
     # configs[3] as written: one 64-lane wave per segment
     ("csum_kernel<64, 4, true, tulips_amd::(anonymous namespace)::VarSegs>", None,
      "ZIPF_one_wave_per_segment"),
-    ("segment_planned_kernel<16, 6>", None, "segment_TSO_64K_mss1460_planned"),
-    ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
+    ("segment_planned_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
+    ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460_device_counted"),
     ("seg_prologue_small_kernel", None, "segment_TSO_64K_mss1460_prologue"),
     ("rss_kernel", None, "rss_toeplitz_16M"),
     ("stream_tiles_kernel", None, "F9000_read_same_bytes"),
@@ -64,7 +64,7 @@ ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673,
               "frames_generate_fields_F1514": 65536 * 1514 + 65536 * 4,
               "F9000_read_same_bytes": 65536 * 9000,
               "segment_TSO_64K_mss1460": 1024 * 64294 + 45056 * 1514,
-              "segment_TSO_64K_mss1460_planned": 1024 * 64294 + 45056 * 1514,
+              "segment_TSO_64K_mss1460_device_counted": 1024 * 64294 + 45056 * 1514,
               "rss_toeplitz_16M": (1 << 24) * 16}
 
 
