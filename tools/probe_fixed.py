@@ -40,8 +40,10 @@ def main():
         out = torch.empty(nb * N, dtype=torch.uint16, device=dev)
         res, ref = {}, None
         for rnd in range(int(os.environ.get("ROUNDS", "3"))):
-            for (g, u, blk), nt in [(gm, nt) for gm in geoms for nt in nts]:
-                t = csum.Tuning(group=g, unroll=u, nontemporal=nt, block=blk)
+            for gm, nt in [(gm, nt) for gm in geoms for nt in nts]:
+                g, u, blk = gm[:3]
+                cap = gm[3] if len(gm) > 3 else 0    # g:u:block[:max_blocks]
+                t = csum.Tuning(group=g, unroll=u, nontemporal=nt, block=blk, max_blocks=cap)
 
                 def fn(i, sh, t=t):
                     b = i % nb
@@ -56,12 +58,12 @@ def main():
                 o = out.cpu().numpy()
                 if ref is None:
                     ref = o
-                assert np.array_equal(o, ref), (g, u, blk, nt)
-                res.setdefault((g, u, blk, nt), []).append(
+                assert np.array_equal(o, ref), (g, u, blk, cap, nt)
+                res.setdefault((g, u, blk, cap, nt), []).append(
                     timer(fn, bench.SERIAL_LAUNCHES, replays=3))
-        for (g, u, blk, nt), ts in res.items():
+        for (g, u, blk, cap, nt), ts in res.items():
             tm = float(np.median(ts))
-            print(json.dumps({"L": L, "geom": f"g{g}u{u}b{blk}nt{nt}", "us": round(tm * 1e6, 2),
+            print(json.dumps({"L": L, "geom": f"g{g}u{u}b{blk}c{cap}nt{nt}", "us": round(tm * 1e6, 2),
                               "GBps": round(bb / tm / 1e9, 1)}), flush=True)
         del buf
 
