@@ -793,42 +793,61 @@ def host_start_leg(torch, dist, csum, cdev, arena, rank, world):
     nbytes = NBATCH * NSEG * SEG
     lib = checked_lib(csum)
     ptr = C.c_void_p()
-    lib.tulips_csum_host_alloc(nbytes, C.byref(ptr))
+    ctx = None
+    err = None
+    times = []
+    ok = False
+    # every rank takes part in every barrier and reduction below whatever
+    # fails locally (a failure becomes this rank's error and parity MISMATCH),
+    # so no rank is left waiting in a collective
     try:
+        lib.tulips_csum_host_alloc(nbytes, C.byref(ptr))
         host = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))
         torch.from_numpy(host).copy_(arena[:nbytes])     # the shard's bytes, D2H once
         torch.cuda.synchronize()
         offs = np.arange(NBATCH * NSEG, dtype=np.uint64) * np.uint64(SEG)
         lens = np.full(NBATCH * NSEG, SEG, dtype=np.uint16)
         out = np.empty(NBATCH * NSEG, dtype=np.uint16)
-        times = []
-        with csum.HostContext(torch.cuda.current_device()) as ctx:
-            ctx.batch(ptr.value, offs, lens, out=out)          # staging made
-            for _ in range(3):
+        ctx = csum.HostContext(torch.cuda.current_device())
+        ctx.batch(ptr.value, offs, lens, out=out)          # staging made
+    except Exception as e:  # noqa: BLE001 - reported, never hidden
+        err = f"{type(e).__name__}: {e}"
+    for _ in range(3):
+        if world > 1:
+            dist.barrier()
+        if err is None:
+            try:
                 out.fill(0xA5A5)
-                if world > 1:
-                    dist.barrier()
                 t0 = time.perf_counter()
                 ctx.batch(ptr.value, offs, lens, out=out)
                 times.append(time.perf_counter() - t0)
-        t_local = float(np.median(times))
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+    if err is None:
         gold = golden_digests().get("M8x1500", {}).get("shards", [])
         ok = rank < len(gold) and "batches" in gold[rank] and all(
             fnv1a_u16(out[b * NSEG:(b + 1) * NSEG]) == gold[rank]["batches"][b]
             for b in range(NBATCH))
-    finally:
+    if ctx is not None:
+        ctx.close()
+    if ptr.value:
         lib.tulips_csum_host_free(ptr)
+    t_local = float(np.median(times)) if times and err is None else float("inf")
     t_max = max_over_ranks(t_local, dist, cdev) if world > 1 else t_local
     t_min = -max_over_ranks(-t_local, dist, cdev) if world > 1 else t_local
-    ok = all_ranks_ok(ok, dist, cdev) if world > 1 else ok
-    return {"what": "each rank's M8x1500 shard from page-locked host memory near its GPU: "
-                    "tulips_csum_batch_host (H2D -> kernel -> D2H pipeline, one call per "
-                    "1.57 GB shard), median of 3, max over ranks",
-            "bytes_per_rank": nbytes, "ms_max": round(t_max * 1e3, 3),
-            "ms_min": round(t_min * 1e3, 3),
-            "per_gpu_GiBps": round(nbytes / t_max / GIB, 2),
-            "aggregate_GiBps": round(world * nbytes / t_max / GIB, 2),
-            "parity": "ok" if ok else "MISMATCH"}
+    ok = all_ranks_ok(ok and err is None, dist, cdev) if world > 1 else (ok and err is None)
+    res = {"what": "each rank's M8x1500 shard from page-locked host memory near its GPU: "
+                   "tulips_csum_batch_host (H2D -> kernel -> D2H pipeline, one call per "
+                   "1.57 GB shard), median of 3, max over ranks",
+           "bytes_per_rank": nbytes,
+           "parity": "ok" if ok else "MISMATCH"}
+    if err is not None or t_max == float("inf"):
+        res["error"] = err or "another rank failed"
+        return res
+    res.update({"ms_max": round(t_max * 1e3, 3), "ms_min": round(t_min * 1e3, 3),
+                "per_gpu_GiBps": round(nbytes / t_max / GIB, 2),
+                "aggregate_GiBps": round(world * nbytes / t_max / GIB, 2)})
+    return res
 
 
 def mctx_device_leg(torch, dist, csum, cdev, rank, world, args):
