@@ -633,6 +633,8 @@ def summary_of(result):
     seg = ex.get("segment_TSO_64K_mss1460")
     if isinstance(seg, dict) and "frac_of_peak" in seg:
         out["segment_serial_frac"] = seg.get("frac_of_peak")
+        out["segment_copy_same_bytes_frac"] = (seg.get("copy_same_bytes") or {}).get(
+            "frac_of_peak")
     hs = result.get("host_start")
     if isinstance(hs, dict) and "aggregate_GiBps" in hs:
         out["host_start_GiBps"] = hs["aggregate_GiBps"]
@@ -1878,7 +1880,31 @@ def frame_extras(torch, csum, dev, timer):
         traffic=read_traffic("segment_TSO_64K_mss1460"),
         segments_per_s=round(nseg / t / 1e6, 2) * 1e6, pipeline=pipe_entry(moved, tp),
         parity="ok" if okp else "MISMATCH", device_counted=counted)
-    del sa, sv, sout, ref_out, ref_len
+    # the segment kernel's loads and stores without its header work, over the
+    # same rotated source: slot k copies [frame + (k % 44) * 1460, + 1514) to
+    # its 1536 B slot (tulips_csum_stream_copy_slots); the ceiling the
+    # segmentation figure is held against. Parity: every slot's payload bytes
+    # equal the planned segmentation's
+    cout = torch.empty_like(sout)
+
+    def fcopy(i, st):
+        b = i % sb
+        lib.tulips_csum_stream_copy_slots(sa.data_ptr() + b * nsf * sslot, sslot, pay // mss,
+                                          mss, 54 + mss, nseg,
+                                          cout.data_ptr() + b * nseg * ostride, ostride, st)
+    t = timer(fcopy, 32, replays=3)
+    tp = pipe_times(timer, fcopy, 32)
+    okc = bool(torch.equal(cout.view(-1, ostride)[:, 54:54 + mss],
+                           sout.view(-1, ostride)[:, 54:54 + mss]))
+    ex["segment_TSO_64K_mss1460"]["copy_same_bytes"] = {
+        "what": "tulips_csum_stream_copy_slots: the segment kernel's loads and stores (one "
+                "16-lane subgroup per 1514 B slot, dword-aligned loads, funnel shift, "
+                "nontemporal stores), no header parse, patch or sums",
+        "avg_launch_us": round(t * 1e6, 2),
+        "frac_of_peak": round(moved / t / 1e9 / HBM_PEAK_GBS, 4),
+        "pipeline": pipe_entry(moved, tp),
+        "parity": "ok" if okc else "MISMATCH"}
+    del sa, sv, sout, cout, ref_out, ref_len
 
     # Toeplitz RSS over 16M tuples (12 B in, 4 B out per tuple)
     nt = 1 << 24

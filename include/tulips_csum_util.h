@@ -130,6 +130,19 @@ int tulips_csum_stream_read_tiles(const uint8_t* p, uint64_t tile_bytes, uint32_
 int tulips_csum_stream_read_slots(const uint8_t* p, uint64_t slot_bytes, uint32_t read_bytes,
                                   uint32_t nslots, uint32_t* sink, void* stream);
 
+/* The segmentation kernels' data movement without their header work: slot k
+ * copies the `bytes` source bytes at src + (k / per_group) * group_stride +
+ * (k % per_group) * step to out + k * out_stride (one 16-lane subgroup per
+ * slot, dword-aligned 16-byte loads clamped to the source's last 16-byte
+ * chunk, funnel shift, nontemporal 16-byte stores; the last chunk's bytes
+ * past `bytes` are written as 0). out 16-byte aligned, out_stride a multiple
+ * of 16 and >= bytes, bytes <= 65535. The ceiling the segmentation figures
+ * are compared against (bench.py extras.segment_TSO_64K_mss1460
+ * .copy_same_bytes). */
+int tulips_csum_stream_copy_slots(const uint8_t* src, uint64_t group_stride, uint32_t per_group,
+                                  uint32_t step, uint32_t bytes, uint32_t nslots, uint8_t* out,
+                                  uint64_t out_stride, void* stream);
+
 /* Latency of `reps` back-to-back receive validations of one burst of
  * host-resident frames, timed in C with a steady clock around each call
  * (no interpreter in the loop): path 0 = tulips_csum_validate_frames_host

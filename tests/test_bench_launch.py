@@ -100,13 +100,15 @@ def test_summary_of_picks_the_judged_figures():
                                 "read_same_bytes": {"frac_of_peak": 0.70},
                                 "parity": "MISMATCH"},
                        "segment_TSO_64K_mss1460": {"frac_of_peak": 0.69,
-                                                   "device_counted": {"frac_of_peak": 0.57}}}}
+                                                   "device_counted": {"frac_of_peak": 0.57},
+                                                   "copy_same_bytes": {"frac_of_peak": 0.78}}}}
     s = bench.summary_of(line)
     assert s["F1500"] == {"serial_frac": 0.77, "branches4_frac": 0.89,
                           "read_same_bytes_frac": 0.80, "parity": "ok"}
     assert s["F9000"]["serial_frac"] == 0.89 and s["F9000"]["read_same_bytes_frac"] == 0.88
     assert s["ZIPF"]["parity"] == "MISMATCH"
     assert s["segment_serial_frac"] == 0.69 and s["host_start_GiBps"] == 380.5
+    assert s["segment_copy_same_bytes_frac"] == 0.78
     assert len(json.dumps(s)) < 900      # fits the driver's stored tail
     # extras missing (N > 1, or the child failed): no crash, configs None
     s = bench.summary_of({"value": 1.0, "parity": "ok", "roofline": {"frac": 0.7},

@@ -187,6 +187,15 @@ def test_batch_validation_without_gpu():
     assert lib.tulips_csum_stream_read_slots(FAKE, 1000, 1514, 4, FAKE, None) == 1
     assert lib.tulips_csum_stream_read_slots(FAKE, 70000, 65536, 4, FAKE, None) == 1
     assert lib.tulips_csum_stream_read_slots(None, 2048, 1514, 0, None, None) == 0
+    cp = lib.tulips_csum_stream_copy_slots
+    assert cp(FAKE, 65536, 0, 1460, 1514, 4, FAKE, 1536, None) == 1       # per_group 0
+    assert cp(FAKE, 65536, 44, 1460, 0, 4, FAKE, 1536, None) == 1         # no bytes
+    assert cp(FAKE, 65536, 44, 1460, 70000, 4, FAKE, 70016, None) == 1    # > 65535
+    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE + 8, 1536, None) == 1  # misaligned out
+    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE, 1528, None) == 1      # stride % 16
+    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE, 1504, None) == 1      # stride < bytes
+    assert cp(None, 65536, 44, 1460, 1514, 4, FAKE, 1536, None) == 1
+    assert cp(None, 0, 0, 0, 0, 0, None, 0, None) == 0                    # nothing to do
 
 
 def test_python_binding_raises_typed_errors():

@@ -52,6 +52,7 @@ WORKLOADS = [
     ("segment_planned_kernel<16, 6>", None, "segment_TSO_64K_mss1460"),
     ("segment_kernel<16, 6>", None, "segment_TSO_64K_mss1460_device_counted"),
     ("seg_prologue_small_kernel", None, "segment_TSO_64K_mss1460_prologue"),
+    ("copy_slots_kernel<16, 6>", None, "segment_TSO_64K_mss1460_copy_same_bytes"),
     ("rss_kernel", None, "rss_toeplitz_16M"),
     ("stream_tiles_kernel", None, "F9000_read_same_bytes"),
 ]
@@ -65,6 +66,7 @@ ALGO_BYTES = {"F1500": 65536 * 1500, "F9000": 65536 * 9000, "ZIPF": 43772673,
               "F9000_read_same_bytes": 65536 * 9000,
               "segment_TSO_64K_mss1460": 1024 * 64294 + 45056 * 1514,
               "segment_TSO_64K_mss1460_device_counted": 1024 * 64294 + 45056 * 1514,
+              "segment_TSO_64K_mss1460_copy_same_bytes": 1024 * 64294 + 45056 * 1514,
               "rss_toeplitz_16M": (1 << 24) * 16}
 
 

@@ -8,8 +8,9 @@ separable here - use rocprofv3 for that. Serial (HIP events around a captured
 chain of 32 calls, median of 3 replays) and on 4 graph branches, ROUNDS
 alternations; the planned outputs are compared with the prologue form's byte
 for byte after every timed replay. Measurement only; prints JSON lines.
-Optional env LIB_B: a second build of the library whose planned entry is
-timed beside the in-tree one (A/B of planned-kernel variants)."""
+Optional env LIB_B: other builds of the library (comma-separated paths) whose
+planned entries are timed beside the in-tree one (A/B of planned-kernel
+variants)."""
 import ctypes as C
 import json
 import os
@@ -49,16 +50,17 @@ def main():
     soffs = torch.arange(nsf, dtype=torch.int64, device=dev) * sslot
     slens = torch.full((nsf,), sflen - 65536, dtype=torch.int16, device=dev)
     nseg, ost = nsf * 44, 1536
-    outs = {k: torch.empty(sb * nseg * ost, dtype=torch.uint8, device=dev) for k in "PQR"}
-    olen = {k: torch.zeros(sb * nseg, dtype=torch.int16, device=dev) for k in "PQR"}
+    libs = {"P": csum.lib}
+    for i, path in enumerate(filter(None, os.environ.get("LIB_B", "").split(","))):
+        libs[f"Q{i}"] = load(os.path.join(ROOT, path))
+    keys = list(libs) + ["R"]
+    outs = {k: torch.empty(sb * nseg * ost, dtype=torch.uint8, device=dev) for k in keys}
+    olen = {k: torch.zeros(sb * nseg, dtype=torch.int16, device=dev) for k in keys}
     sfirst = torch.empty(sb * (nsf + 1), dtype=torch.int32, device=dev)
     hdr = sv[:nsf, :64].cpu().numpy().reshape(-1)
     plan = csum.segment_plan(hdr, np.arange(nsf, dtype=np.uint64) * np.uint64(64),
                              np.full(nsf, sflen, dtype=np.uint16), mss)
     dplan = torch.from_numpy(plan.view(np.int32).copy()).to(dev)
-    libs = {"P": csum.lib}
-    if os.environ.get("LIB_B"):
-        libs["Q"] = load(os.path.join(ROOT, os.environ["LIB_B"]))
 
     def prologue(i, st):
         b = i % sb

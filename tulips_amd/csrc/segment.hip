@@ -758,6 +758,67 @@ segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
   }
 }
 
+// The segment kernels' data movement without their header work: slot k
+// copies source bytes [src + (k / per) * gstride + (k % per) * step, + bytes)
+// to out + k * ostride, one G-lane subgroup per slot, SU + 1 dword-aligned
+// 16-byte loads per lane per batch (clamped to the source's last 16-byte
+// chunk), funnel shift, nontemporal 16-byte stores: build_segment's loads and
+// stores with no header chunk, parse, patch or sums. The ceiling the
+// segmentation figures are held against (bench.py extras.segment_*).
+template<int G, int SU>
+__global__ __launch_bounds__(256) void
+copy_slots_kernel(uintptr_t src, uint64_t gstride, uint32_t per, uint32_t step, uint32_t bytes,
+                  uint32_t n, uint8_t* out, uint64_t ostride)
+{
+  const uint32_t t = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const uint32_t k = t / G;
+  if (k >= n) {
+    return; // (whole subgroups: their shuffles stay inside the subgroup)
+  }
+  const int lane = int(t % G), sub0 = int(threadIdx.x & 63) & ~(G - 1);
+  const uintptr_t xs = src + uint64_t(k / per) * gstride + uint64_t(k % per) * step;
+  const uintptr_t hi = (xs + bytes - 1) & ~uintptr_t(15);
+  const uintptr_t p0 = xs & ~uintptr_t(3);
+  const uint32_t r = uint32_t(xs & 3);
+  const uintptr_t dst = reinterpret_cast<uintptr_t>(out) + uint64_t(k) * ostride;
+  const int nchunks = int((bytes + 15) >> 4);
+  auto src_chunk = [&](int c, uint32_t& sel) {
+    const uintptr_t p = p0 + 16 * uintptr_t(c);
+    const uintptr_t q = p > hi ? hi : p;
+    sel = uint32_t(p - q) >> 2;
+    return u32x4(*reinterpret_cast<gdw4_ptr>(q));
+  };
+  for (int b0 = 0; b0 < nchunks; b0 += G * SU) {
+    u32x4 X[SU + 1];
+    uint32_t XS[SU + 1];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      X[u] = src_chunk(b0 + lane + G * u, XS[u]);
+    }
+    X[SU] = src_chunk(lane == 0 ? b0 + G * SU : b0 + lane + G * (SU - 1), XS[SU]);
+    realign(X[0], XS[0]);
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      realign(X[u + 1], XS[u + 1]);
+      const uint32_t d4 = next_dword<G>(X[u].x, X[u + 1].x, lane, sub0);
+      const int c = b0 + lane + G * u;
+      if (c >= nchunks) {
+        continue;
+      }
+      const u32x4 a = X[u];
+      u32x4 v;
+      v.x = __builtin_amdgcn_alignbyte(a.y, a.x, r);
+      v.y = __builtin_amdgcn_alignbyte(a.z, a.y, r);
+      v.z = __builtin_amdgcn_alignbyte(a.w, a.z, r);
+      v.w = __builtin_amdgcn_alignbyte(d4, a.w, r);
+      if (uint32_t(16 * c + 16) > bytes) {
+        v = keep_bytes(v, int(bytes) - 16 * c);
+      }
+      store_chunk(dst + 16 * uintptr_t(c), v);
+    }
+  }
+}
+
 // Workspace per (device, stream) (stream_state.h): the scan's block totals
 // (MAX_FRAMES / CB words), the run starts (one word per RUN output segments)
 // and the frame descriptors (16 bytes per input frame). Direct calls on one
@@ -1026,4 +1087,29 @@ tulips_csum_segment_plan_host(const uint8_t* base, const uint64_t* offsets,
   }
   first[n] = uint32_t(acc);
   return TULIPS_STATUS_OK;
+}
+
+extern "C" int
+tulips_csum_stream_copy_slots(const uint8_t* src, uint64_t group_stride, uint32_t per_group,
+                              uint32_t step, uint32_t bytes, uint32_t nslots, uint8_t* out,
+                              uint64_t out_stride, void* stream)
+{
+  using namespace tulips_amd;
+  if (nslots == 0) {
+    return TULIPS_STATUS_OK;
+  }
+  if (!src || !out || per_group == 0 || bytes == 0 || bytes > 0xffffu ||
+      (reinterpret_cast<uintptr_t>(out) & 15) || (out_stride & 15) || out_stride < bytes) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  constexpr int G = 16, SU = 6;
+  const uint64_t blocks = (uint64_t(nslots) * G + 255) / 256;
+  if (blocks > 0xffffffffull) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL((copy_slots_kernel<G, SU>), dim3(uint32_t(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), reinterpret_cast<uintptr_t>(src),
+                     group_stride, per_group, step, bytes, nslots, out, out_stride);
+  return hipGetLastError() == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
 }
