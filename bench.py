@@ -626,7 +626,10 @@ def summary_of(result):
                 "parity": e.get("parity")}
     f15 = pick(ex.get("F1500"), serial=result.get("roofline", {}).get("frac"))
     if f15 is not None:
+        # the plain contiguous read of the batch, and the kernel's own load pattern
         f15["read_same_bytes_frac"] = ex.get("stream_read_F1500_batch", {}).get("frac_of_peak")
+        f15["read_same_pattern_frac"] = (ex.get("F1500", {}).get("read_same_bytes") or {}).get(
+            "frac_of_peak")
         f15["parity"] = "ok" if (result.get("parity") == "ok" and
                                  ex.get("F1500", {}).get("parity") == "ok") else "MISMATCH"
     out = {"F1500": f15, "F9000": pick(ex.get("F9000")), "ZIPF": pick(ex.get("ZIPF"))}
@@ -1269,6 +1272,22 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
                    "pipeline": pipe_entry(batch_bytes, tp15),
                    "parity": "ok" if okf else "MISMATCH"}
     del o15
+
+    # the F1500 kernel's exact load pattern without its arithmetic (32-lane
+    # subgroup per 1500 B segment at stride 1500, 3 clamped loads per lane),
+    # over the same rotated batches: that kernel's own ceiling
+    def f15read(i, st):
+        b = i % NBATCH
+        lib.tulips_csum_stream_read_slots_geom(arena.data_ptr() + b * batch_bytes, SEG, SEG,
+                                               NSEG, 32, 3, sink.data_ptr(), st)
+    t = timer(f15read, 64)
+    tp = pipe_times(timer, f15read, 64)
+    ex["F1500"]["read_same_bytes"] = {
+        "what": "tulips_csum_stream_read_slots_geom(32, 3): the kernel's loads (one 32-lane "
+                "subgroup per 1500 B segment, 3 clamped loads per lane), no arithmetic",
+        "avg_launch_us": round(t * 1e6, 2),
+        "frac_of_peak": round(batch_bytes / t / 1e9 / HBM_PEAK_GBS, 4),
+        "pipeline": pipe_entry(batch_bytes, tp)}
 
     # F9000 (configs[2]): 4 distinct 590 MB batches (2.36 GB, 9x the 256 MB
     # Infinity Cache) rotated, so every launch streams from HBM; the 2-batch

@@ -130,6 +130,15 @@ int tulips_csum_stream_read_tiles(const uint8_t* p, uint64_t tile_bytes, uint32_
 int tulips_csum_stream_read_slots(const uint8_t* p, uint64_t slot_bytes, uint32_t read_bytes,
                                   uint32_t nslots, uint32_t* sink, void* stream);
 
+/* The same with the subgroup geometry named: group lanes per slot, unroll
+ * clamped loads per lane per pass; (16, 6) as above, or (32, 3), the F1500
+ * checksum kernel's (csum_kernel<32, 3>: slot_bytes = read_bytes = 1500 is
+ * that kernel's exact load pattern, bench.py extras.F1500.read_same_bytes).
+ * Other geometries: InvalidArgument. */
+int tulips_csum_stream_read_slots_geom(const uint8_t* p, uint64_t slot_bytes, uint32_t read_bytes,
+                                       uint32_t nslots, int group, int unroll, uint32_t* sink,
+                                       void* stream);
+
 /* The segmentation kernels' data movement without their header work: slot k
  * copies the `bytes` source bytes at src + (k / per_group) * group_stride +
  * (k % per_group) * step to out + k * out_stride (one 16-lane subgroup per

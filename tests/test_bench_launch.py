@@ -92,7 +92,7 @@ def test_summary_of_picks_the_judged_figures():
     line = {"value": 6000.0, "parity": "ok", "roofline": {"frac": 0.77},
             "host_start": {"aggregate_GiBps": 380.5},
             "extras": {"F1500": {"frac_of_peak": 0.76, "pipeline": {"frac_of_peak": 0.89},
-                                 "parity": "ok"},
+                                 "read_same_bytes": {"frac_of_peak": 0.79}, "parity": "ok"},
                        "stream_read_F1500_batch": {"frac_of_peak": 0.80},
                        "F9000": {"frac_of_peak": 0.89, "pipeline": {"frac_of_peak": 0.93},
                                  "read_same_bytes": {"frac_of_peak": 0.88}, "parity": "ok"},
@@ -104,7 +104,8 @@ def test_summary_of_picks_the_judged_figures():
                                                    "copy_same_bytes": {"frac_of_peak": 0.78}}}}
     s = bench.summary_of(line)
     assert s["F1500"] == {"serial_frac": 0.77, "branches4_frac": 0.89,
-                          "read_same_bytes_frac": 0.80, "parity": "ok"}
+                          "read_same_bytes_frac": 0.80, "read_same_pattern_frac": 0.79,
+                          "parity": "ok"}
     assert s["F9000"]["serial_frac"] == 0.89 and s["F9000"]["read_same_bytes_frac"] == 0.88
     assert s["ZIPF"]["parity"] == "MISMATCH"
     assert s["segment_serial_frac"] == 0.69 and s["host_start_GiBps"] == 380.5

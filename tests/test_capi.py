@@ -187,6 +187,11 @@ def test_batch_validation_without_gpu():
     assert lib.tulips_csum_stream_read_slots(FAKE, 1000, 1514, 4, FAKE, None) == 1
     assert lib.tulips_csum_stream_read_slots(FAKE, 70000, 65536, 4, FAKE, None) == 1
     assert lib.tulips_csum_stream_read_slots(None, 2048, 1514, 0, None, None) == 0
+    g = lib.tulips_csum_stream_read_slots_geom
+    assert g(FAKE, 1500, 1500, 4, 32, 4, FAKE, None) == 1                 # geometry
+    assert g(FAKE, 1500, 1500, 4, 64, 12, FAKE, None) == 1
+    assert g(FAKE, 1000, 1500, 4, 32, 3, FAKE, None) == 1                 # slot < read
+    assert g(None, 0, 0, 0, 32, 3, None, None) == 0                       # nothing to do
     cp = lib.tulips_csum_stream_copy_slots
     assert cp(FAKE, 65536, 0, 1460, 1514, 4, FAKE, 1536, None) == 1       # per_group 0
     assert cp(FAKE, 65536, 44, 1460, 0, 4, FAKE, 1536, None) == 1         # no bytes

@@ -440,3 +440,22 @@ def test_fixed_small_workgroups(length, group, unroll):
     bad = csum.Tuning(group=group, unroll=unroll, block=96)
     assert csum.lib.tulips_csum_batch_fixed_tuned(arena.data_ptr(), length, length, None, None,
                                                   None, want.data_ptr(), n, 0, bad, st) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group,unroll,stride,length", [(32, 3, 1500, 1500), (16, 6, 2048, 1514),
+                                                        (32, 3, 1501, 37)])
+def test_gpu_stream_read_slots_geom(group, unroll, stride, length):
+    """The load-pattern ceilings bench.py quotes run on any slot alignment and
+    read only inside the slots' 16-byte chunks (the buffer ends right after
+    the last slot's last chunk)."""
+    import torch
+    from tulips_amd import csum
+    n = 4097
+    nbytes = ((n - 1) * stride + length + 15) // 16 * 16
+    buf = torch.zeros(nbytes, dtype=torch.uint8, device="cuda:0")
+    sink = torch.zeros(4, dtype=torch.int32, device="cuda:0")
+    assert csum.lib.tulips_csum_stream_read_slots_geom(buf.data_ptr(), stride, length, n, group,
+                                                       unroll, sink.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert int(sink.sum().item()) == 0

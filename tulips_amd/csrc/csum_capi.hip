@@ -677,7 +677,21 @@ tulips_csum_stream_read_slots(const uint8_t* p, uint64_t slot_bytes, uint32_t re
                  slot_bytes < read_bytes)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
-  return status_of(launch_stream_slots(p, slot_bytes, read_bytes, nslots, sink,
+  return status_of(launch_stream_slots(p, slot_bytes, read_bytes, nslots, 16, 6, sink,
+                                       static_cast<hipStream_t>(stream)));
+}
+
+int
+tulips_csum_stream_read_slots_geom(const uint8_t* p, uint64_t slot_bytes, uint32_t read_bytes,
+                                   uint32_t nslots, int group, int unroll, uint32_t* sink,
+                                   void* stream)
+{
+  const bool geom = (group == 16 && unroll == 6) || (group == 32 && unroll == 3);
+  if (!geom || (nslots && (!p || !sink || read_bytes == 0 ||
+                           read_bytes > TULIPS_CSUM_MAX_SEGMENT || slot_bytes < read_bytes))) {
+    return TULIPS_STATUS_INVALID_ARGUMENT;
+  }
+  return status_of(launch_stream_slots(p, slot_bytes, read_bytes, nslots, group, unroll, sink,
                                        static_cast<hipStream_t>(stream)));
 }
 

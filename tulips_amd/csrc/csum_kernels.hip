@@ -587,17 +587,24 @@ stream_slots_kernel(uintptr_t base, uint64_t stride, uint32_t bytes, uint32_t n,
 } // namespace
 
 hipError_t
-launch_stream_slots(const uint8_t* p, uint64_t stride, uint32_t bytes, uint32_t n,
-                    uint32_t* sink, hipStream_t stream)
+launch_stream_slots(const uint8_t* p, uint64_t stride, uint32_t bytes, uint32_t n, int group,
+                    int unroll, uint32_t* sink, hipStream_t stream)
 {
   if (n == 0 || bytes == 0) {
     return hipSuccess;
   }
-  constexpr uint32_t G = 16, U = 6;
+  const uint32_t blocks = uint32_t((uint64_t(n) * uint32_t(group) + 255) / 256);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   (void)hipGetLastError();
-  hipLaunchKernelGGL((stream_slots_kernel<G, U>), dim3(uint32_t((uint64_t(n) * G + 255) / 256)),
-                     dim3(256), 0, stream, reinterpret_cast<uintptr_t>(p), stride, bytes, n,
-                     sink);
+  if (group == 16 && unroll == 6) {
+    hipLaunchKernelGGL((stream_slots_kernel<16, 6>), dim3(blocks), dim3(256), 0, stream, a,
+                       stride, bytes, n, sink);
+  } else if (group == 32 && unroll == 3) {
+    hipLaunchKernelGGL((stream_slots_kernel<32, 3>), dim3(blocks), dim3(256), 0, stream, a,
+                       stride, bytes, n, sink);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

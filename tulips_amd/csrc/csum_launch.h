@@ -97,7 +97,7 @@ hipError_t launch_zc_server(ZcMailbox* mb, const ZcArgs* oneshot, hipStream_t st
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                 uint64_t byte_off, hipStream_t stream);
 hipError_t launch_stream_slots(const uint8_t* p, uint64_t stride, uint32_t bytes, uint32_t n,
-                               uint32_t* sink, hipStream_t stream);
+                               int group, int unroll, uint32_t* sink, hipStream_t stream);
 hipError_t launch_stream_tiles(const uint8_t* p, uint64_t tile, uint32_t ntiles,
                                uint32_t* sink, hipStream_t stream);
 hipError_t launch_stream_read(const uint8_t* p, uint64_t nbytes,

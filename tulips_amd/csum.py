@@ -129,6 +129,8 @@ _SIGNATURES = {
     "tulips_csum_stream_read_tiles": (C.c_int, [_vp, C.c_uint64, C.c_uint32, _vp, _vp]),
     "tulips_csum_stream_read_slots": (C.c_int, [_vp, C.c_uint64, C.c_uint32, C.c_uint32, _vp,
                                                 _vp]),
+    "tulips_csum_stream_read_slots_geom": (C.c_int, [_vp, C.c_uint64, C.c_uint32, C.c_uint32,
+                                                     C.c_int, C.c_int, _vp, _vp]),
     "tulips_csum_stream_copy_slots": (C.c_int, [_vp, C.c_uint64, C.c_uint32, C.c_uint32,
                                                 C.c_uint32, C.c_uint32, _vp, C.c_uint64, _vp]),
     "tulips_rss_toeplitz_host": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16,
