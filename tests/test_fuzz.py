@@ -1,0 +1,169 @@
+"""Seeded, time-budgeted fuzz of the batch entry points against the oracle.
+
+Each case draws a batch shape at random - segment count (0 to 40,000,
+log-uniform), a length mix (empty, tiny, Zipf-like, uniform to 65,535, one
+fixed length), an arena with all-0x00 / all-0xFF stretches, a base alignment
+and gaps between segments - and runs it through every entry that accepts it:
+tulips_csum_batch (any layout: the offsets shuffled and overlapping),
+tulips_csum_batch_arena (in order, with gaps), tulips_csum_verify_arena
+(its count against the oracle's) and tulips_csum_batch_fixed (fixed stride),
+in a random mode (RAW / INET / TCP, with or without seeds, complemented or
+not). Expected values: oracle/csum_oracle.c (pinned to the reference by
+tests/test_oracle.py). Bar: bit-exact.
+
+TULIPS_FUZZ_SECONDS (default 8) bounds the run; TULIPS_FUZZ_SEED (default 1)
+picks the sequence. A failure names its case seed; TULIPS_FUZZ_CASE=<case
+seed> runs that case alone.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from oracle import FLAG_COMPLEMENT, MODE_INET, MODE_RAW, MODE_TCP  # noqa: E402
+
+from tulips_amd import csum  # noqa: E402
+
+DEV = "cuda:0"
+ARENA_MAX = 48 << 20   # bytes per case: the oracle finishes a case in well under a second
+
+
+def _d(a):
+    return torch.from_numpy(np.array(a, copy=True, order="C")).to(DEV)
+
+
+def _u16(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint16)
+
+
+def _lengths(rng, n):
+    kind = rng.integers(0, 6)
+    if kind == 0:      # Zipf-like, mostly short
+        lens = np.minimum(np.minimum(rng.zipf(1.3, n), 1000) * 40, 9000)
+    elif kind == 1:    # uniform to the maximum
+        lens = rng.integers(0, 65536, n)
+    elif kind == 2:    # tiny
+        lens = rng.integers(0, 80, n)
+    elif kind == 3:    # MTU-ish with jumbo outliers
+        lens = rng.integers(1400, 1515, n)
+        lens[rng.random(n) < 0.02] = 9000
+    elif kind == 4:    # one fixed length
+        lens = np.full(n, int(rng.choice([0, 1, 15, 16, 17, 1500, 1514, 9000, 65535])))
+    else:              # mixed, with runs of empty segments
+        lens = rng.integers(0, 3000, n)
+        lens[rng.random(n) < 0.2] = 0
+        if n > 64:
+            s = int(rng.integers(0, n - 64))
+            lens[s:s + 64] = 0
+    lens = np.asarray(lens, dtype=np.int64)
+    # keep the arena bounded
+    total = int(lens.sum())
+    if total > ARENA_MAX // 2:
+        lens = (lens * (ARENA_MAX // 2) // max(total, 1)).astype(np.int64)
+    return lens.astype(np.uint16)
+
+
+def _arena(rng, nbytes):
+    a = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    for _ in range(int(rng.integers(0, 4))):      # all-0x00 / all-0xFF stretches
+        s = int(rng.integers(0, max(nbytes - 1, 1)))
+        e = min(nbytes, s + int(rng.integers(1, 70000)))
+        a[s:e] = 0xFF if rng.random() < 0.5 else 0
+    return a
+
+
+def _mode(rng):
+    m = [MODE_RAW, MODE_INET, MODE_TCP][int(rng.integers(0, 3))]
+    if rng.random() < 0.3:
+        m |= FLAG_COMPLEMENT
+    return m
+
+
+def _case(oracle, seed):
+    rng = np.random.default_rng(seed)
+    n = int(np.exp(rng.uniform(0, np.log(40001)))) - 1
+    lens = _lengths(rng, n)
+    gaps = rng.integers(0, 40, n) * (rng.random(n) < 0.5)
+    base = int(rng.integers(0, 16))
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[:] = base + np.concatenate(([0], np.cumsum(lens.astype(np.int64) + gaps)[:-1]))
+    nbytes = int(offs[-1]) + int(lens[-1]) + 64 if n else 64
+    arena = _arena(rng, nbytes)
+    mode = _mode(rng)
+    seeds = rng.integers(0, 65536, n, dtype=np.uint16) if rng.random() < 0.5 else None
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    if (mode & 0xff) == MODE_TCP:
+        seeds = None
+    exp = oracle.batch(arena, offs, lens, seeds=seeds, src=src, dst=dst, mode=mode, nthreads=8)
+    da, dl = _d(arena), _d(lens.view(np.int16))
+    ds = _d(seeds.view(np.int16)) if seeds is not None else None
+    dsrc, ddst = _d(src.view(np.int32)), _d(dst.view(np.int32))
+    what = f"case seed {seed}: n={n} mode={mode:#x} base={base}"
+    # in order, with gaps
+    do = _d(offs.view(np.int64))
+    got = csum.batch_arena(da, do, dl, arena_bytes=nbytes, seeds=ds, src=dsrc, dst=ddst,
+                           mode=mode)
+    np.testing.assert_array_equal(_u16(got), exp, err_msg=f"batch_arena {what}")
+    # any layout: shuffled, and some segments re-pointed to overlap others
+    perm = rng.permutation(n)
+    offs2, lens2 = offs[perm].copy(), lens[perm].copy()
+    if n > 1:
+        k = rng.integers(0, n, max(1, n // 20))
+        src_k = rng.integers(0, n, len(k))
+        offs2[k], lens2[k] = offs2[src_k], lens2[src_k]
+    exp2 = oracle.batch(arena, offs2, lens2, seeds=None if seeds is None else seeds[perm],
+                        src=src[perm], dst=dst[perm], mode=mode, nthreads=8)
+    got2 = csum.batch(da, _d(offs2.view(np.int64)), _d(lens2.view(np.int16)),
+                      seeds=None if seeds is None else _d(seeds[perm].view(np.int16)),
+                      src=_d(src[perm].view(np.int32)), dst=_d(dst[perm].view(np.int32)),
+                      mode=mode)
+    np.testing.assert_array_equal(_u16(got2), exp2, err_msg=f"batch {what}")
+    # verify counts (INET / TCP without the complement flag)
+    vmode = mode & 0xff
+    if vmode in (MODE_INET, MODE_TCP) and seeds is None:
+        bad = csum.verify_arena(da, do, dl, arena_bytes=nbytes, src=dsrc, dst=ddst, mode=vmode)
+        torch.cuda.synchronize()
+        want = int(np.count_nonzero(oracle.batch(arena, offs, lens, src=src, dst=dst,
+                                                 mode=vmode, nthreads=8) != 0xFFFF))
+        assert int(bad.item()) == want, f"verify_arena {what}"
+    # fixed stride over the same arena
+    if n:
+        L = int(lens[0])
+        stride = L + int(rng.integers(0, 48))
+        nf = max(0, min(n, (nbytes - base - L) // max(stride, 1) + 1)) if stride else 0
+        if nf:
+            offs3 = (base + np.arange(nf, dtype=np.uint64) * np.uint64(stride))
+            lens3 = np.full(nf, L, dtype=np.uint16)
+            exp3 = oracle.batch(arena, offs3, lens3, mode=mode, nthreads=8,
+                                src=src[:nf], dst=dst[:nf])
+            got3 = csum.batch_fixed(da, stride, L, nf, src=dsrc[:nf], dst=ddst[:nf],
+                                    mode=mode, base_offset=base)
+            np.testing.assert_array_equal(_u16(got3), exp3, err_msg=f"batch_fixed {what} "
+                                                                    f"L={L} stride={stride}")
+
+
+def test_fuzz_batch_entries_vs_oracle(oracle):
+    if os.environ.get("TULIPS_FUZZ_CASE"):
+        _case(oracle, int(os.environ["TULIPS_FUZZ_CASE"]))
+        return
+    budget = float(os.environ.get("TULIPS_FUZZ_SECONDS", "8"))
+    seed0 = int(os.environ.get("TULIPS_FUZZ_SEED", "1"))
+    t0 = time.monotonic()
+    done = 0
+    last = t0
+    while done == 0 or time.monotonic() - t0 < budget:
+        _case(oracle, seed0 * 1_000_003 + done)
+        done += 1
+        if time.monotonic() - last > 20:      # progress for long runs
+            last = time.monotonic()
+            print(f"fuzz: {done} cases, {last - t0:.0f} s", flush=True)
+    print(f"fuzz: {done} cases in {time.monotonic() - t0:.1f} s", flush=True)
+    assert done >= 1
