@@ -167,3 +167,120 @@ def test_fuzz_batch_entries_vs_oracle(oracle):
             print(f"fuzz: {done} cases, {last - t0:.0f} s", flush=True)
     print(f"fuzz: {done} cases in {time.monotonic() - t0:.1f} s", flush=True)
     assert done >= 1
+
+
+# ------------------------------------------------ frames and segmentation ----
+def _frame(oracle, rng, payload, doff):
+    """Ethernet/IPv4/TCP frame, checksums generated by the oracle."""
+    from test_segment import super_frame
+    return super_frame(oracle, rng, payload, doff=doff)
+
+
+def _frame_set(oracle, rng, n, max_payload):
+    frames = []
+    for _ in range(n):
+        kind = rng.random()
+        if kind < 0.6:                                   # well formed, any size
+            pay = int(rng.integers(0, max_payload + 1)) if rng.random() < 0.8 else \
+                int(rng.choice([0, 1, 1459, 1460, 1461, max_payload]))
+            f = bytearray(_frame(oracle, rng, pay, int(rng.integers(5, 16))))
+        elif kind < 0.8:                                 # corrupted header or payload bytes
+            f = bytearray(_frame(oracle, rng, int(rng.integers(0, 3000)), 5))
+            for _ in range(int(rng.integers(1, 4))):
+                at = int(rng.integers(0, min(len(f), 64) if rng.random() < 0.7 else len(f)))
+                f[at] ^= int(rng.integers(1, 256))
+        elif kind < 0.9:                                 # truncated (declared > present)
+            f = bytearray(_frame(oracle, rng, int(rng.integers(10, 3000)), 5))
+            f = f[:int(rng.integers(14, len(f)))]
+        else:                                            # runts and non-IPv4 frames
+            f = bytearray(rng.integers(0, 256, int(rng.integers(0, 80)), dtype=np.uint8).tobytes())
+        frames.append(bytes(f))
+    from test_frames import pack
+    return pack(frames, rng, gap=24, lead=int(rng.integers(0, 16)))
+
+
+def _frames_case(oracle, seed):
+    from test_frames import fields_of
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 1500))
+    arena, offs, lens = _frame_set(oracle, rng, n, 9000 if rng.random() < 0.3 else 1460)
+    what = f"frames case seed {seed}: n={n}"
+    a, o, l = _d(arena), _d(offs.view(np.int64)), _d(lens.view(np.int16))
+    # validation: flags and counters
+    exp = oracle.validate_frames(arena, offs, lens)
+    cnt = torch.zeros(4, dtype=torch.int32, device=DEV)
+    fl = csum.validate_frames(a, o, l, counters=cnt)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(fl.cpu().numpy(), exp, err_msg=f"validate {what}")
+    from test_frames import counters_of
+    np.testing.assert_array_equal(cnt.cpu().numpy().astype(np.uint32), counters_of(exp),
+                                  err_msg=f"counters {what}")
+    # generation: compact fields, then in place
+    exp_arena, exp_flags = oracle.generate_frames(arena, offs, lens)
+    fields, ffl = csum.generate_fields(a, o, l)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ffl.cpu().numpy(), exp_flags, err_msg=f"fields flags {what}")
+    np.testing.assert_array_equal(fields.cpu().numpy().view(np.uint32),
+                                  fields_of(exp_arena, offs, lens, exp_flags),
+                                  err_msg=f"fields {what}")
+    gfl = csum.generate_frames(a, o, l)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(gfl.cpu().numpy(), exp_flags, err_msg=f"generate {what}")
+    got = a.cpu().numpy()
+    assert np.array_equal(got, exp_arena), (what, np.nonzero(got != exp_arena)[0][:8])
+
+
+def _segment_case(oracle, seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 200))
+    arena, offs, lens = _frame_set(oracle, rng, n, int(rng.choice([1460, 9000, 30000])))
+    mss = int(rng.choice([int(rng.integers(1, 65536)), int(rng.integers(16, 1461)), 536,
+                          1460, 8960]))
+    if mss < 16 and int(lens.astype(np.int64).sum()) > 200000:
+        mss = 16                                       # keep the output bounded
+    stride = 16 * ((94 + min(mss, 9000) + 15) // 16) + 16 * int(rng.integers(0, 3))
+    what = f"segment case seed {seed}: n={n} mss={mss} stride={stride}"
+    e_first, e_out, e_lens = oracle.segment_frames(arena, offs, lens, mss, stride)
+    total = int(e_first[-1])
+    a, o, l = _d(arena), _d(offs.view(np.int64)), _d(lens.view(np.int16))
+    keep = np.arange(stride)[None, :] < e_lens.astype(np.int64)[:, None]
+    want = e_out.reshape(total, stride)[keep]
+    # the device-counted form
+    out, ol, first = csum.segment_frames(a, o, l, mss, stride=stride)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(first.cpu().numpy().view(np.uint32), e_first,
+                                  err_msg=f"first {what}")
+    got_l = ol.cpu().numpy().view(np.uint16)[:total]
+    np.testing.assert_array_equal(got_l, e_lens, err_msg=f"lengths {what}")
+    got = out.cpu().numpy()[:total * stride].reshape(total, stride)[keep]
+    assert np.array_equal(got, want), f"bytes {what}"
+    # the planned form, plan from the host
+    plan = csum.segment_plan(arena, offs, lens, mss)
+    np.testing.assert_array_equal(plan, e_first, err_msg=f"plan {what}")
+    out2, ol2 = csum.segment_frames_planned(a, o, l, mss, _d(plan.view(np.int32)), stride=stride)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ol2.cpu().numpy().view(np.uint16)[:total], e_lens,
+                                  err_msg=f"planned lengths {what}")
+    got2 = out2.cpu().numpy()[:total * stride].reshape(total, stride)[keep]
+    assert np.array_equal(got2, want), f"planned bytes {what}"
+
+
+def test_fuzz_frames_and_segmentation_vs_oracle(oracle):
+    if os.environ.get("TULIPS_FUZZ_CASE"):
+        s = int(os.environ["TULIPS_FUZZ_CASE"])
+        _frames_case(oracle, s)
+        _segment_case(oracle, s)
+        return
+    budget = float(os.environ.get("TULIPS_FUZZ_SECONDS", "8"))
+    seed0 = int(os.environ.get("TULIPS_FUZZ_SEED", "1"))
+    t0 = last = time.monotonic()
+    done = 0
+    while done == 0 or time.monotonic() - t0 < budget:
+        s = seed0 * 1_000_033 + done
+        _frames_case(oracle, s)
+        _segment_case(oracle, s)
+        done += 1
+        if time.monotonic() - last > 20:
+            last = time.monotonic()
+            print(f"fuzz frames: {done} cases, {last - t0:.0f} s", flush=True)
+    print(f"fuzz frames: {done} cases in {time.monotonic() - t0:.1f} s", flush=True)
