@@ -284,3 +284,44 @@ def test_fuzz_frames_and_segmentation_vs_oracle(oracle):
             last = time.monotonic()
             print(f"fuzz frames: {done} cases, {last - t0:.0f} s", flush=True)
     print(f"fuzz frames: {done} cases in {time.monotonic() - t0:.1f} s", flush=True)
+
+
+# --------------------------------------------------------------- Toeplitz ----
+def _rss_case(oracle, seed):
+    rng = np.random.default_rng(seed)
+    n = int(np.exp(rng.uniform(0, np.log(200001))))
+    key = rng.integers(0, 256, int(rng.integers(4, 61)), dtype=np.uint8).tobytes()
+    init = int(rng.integers(0, 2**32)) if rng.random() < 0.3 else 0
+    sa = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    da = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    sp = rng.integers(0, 65536, n, dtype=np.uint32).astype(np.uint16)
+    dp = rng.integers(0, 65536, n, dtype=np.uint32).astype(np.uint16)
+    # arrays at a random element offset: the 4-tuples-per-thread path needs
+    # 16-byte aligned addresses, the one-tuple path takes any
+    sh = int(rng.integers(0, 4))
+
+    def dev(x, dt):
+        t = _d(np.concatenate([np.zeros(sh, x.dtype), x]).view(dt))
+        return t[sh:]
+    out = csum.rss_batch(dev(sa, np.int32), dev(da, np.int32), dev(sp, np.int16),
+                         dev(dp, np.int16), key, init)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    for k in rng.integers(0, n, min(n, 64)):
+        k = int(k)
+        want = oracle.toeplitz(int(sa[k]), int(da[k]), int(sp[k]), int(dp[k]), key, init)
+        assert int(got[k]) == want, f"rss case seed {seed}: n={n} tuple {k} key {len(key)} B"
+
+
+def test_fuzz_toeplitz_vs_oracle(oracle):
+    if os.environ.get("TULIPS_FUZZ_CASE"):
+        _rss_case(oracle, int(os.environ["TULIPS_FUZZ_CASE"]))
+        return
+    budget = min(float(os.environ.get("TULIPS_FUZZ_SECONDS", "8")), 60.0) / 2
+    seed0 = int(os.environ.get("TULIPS_FUZZ_SEED", "1"))
+    t0 = time.monotonic()
+    done = 0
+    while done == 0 or time.monotonic() - t0 < budget:
+        _rss_case(oracle, seed0 * 1_000_037 + done)
+        done += 1
+    print(f"fuzz toeplitz: {done} cases in {time.monotonic() - t0:.1f} s", flush=True)
