@@ -325,3 +325,68 @@ def test_fuzz_toeplitz_vs_oracle(oracle):
         _rss_case(oracle, seed0 * 1_000_037 + done)
         done += 1
     print(f"fuzz toeplitz: {done} cases in {time.monotonic() - t0:.1f} s", flush=True)
+
+
+# ---------------------------------------------------- host-memory context ----
+def _host_case(oracle, ctxs, seed):
+    """Host-resident batches through the staging pipeline (chunk sizes from
+    the minimum up, so segments straddle chunk boundaries in every way):
+    checksums, frame validation (staged and zero-copy) and in-place
+    generation against the oracle."""
+    rng = np.random.default_rng(seed)
+    ctx = ctxs[int(rng.integers(0, len(ctxs)))]
+    n = int(np.exp(rng.uniform(0, np.log(20001)))) - 1
+    lens = _lengths(rng, n)
+    if int(lens.astype(np.int64).sum()) > (8 << 20):
+        lens = (lens.astype(np.int64) * (8 << 20) // int(lens.astype(np.int64).sum())
+                ).astype(np.uint16)
+    gaps = rng.integers(0, 40, n) * (rng.random(n) < 0.5)
+    base = int(rng.integers(0, 16))
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[:] = base + np.concatenate(([0], np.cumsum(lens.astype(np.int64) + gaps)[:-1]))
+    if n and rng.random() < 0.5:          # any order (the host path packs what it stages)
+        perm = rng.permutation(n)
+        offs, lens = offs[perm], lens[perm]
+    nbytes = (int(offs.max()) + 65600) if n else 64
+    arena = _arena(rng, nbytes)
+    mode = _mode(rng)
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(arena, offs, lens, src=src, dst=dst, mode=mode, nthreads=8)
+    got = ctx.batch(arena, offs, lens, src=src, dst=dst, mode=mode)
+    np.testing.assert_array_equal(got, exp, err_msg=f"host batch case seed {seed}: n={n}")
+    # frames
+    nf = int(rng.integers(1, 600))
+    farena, foffs, flens = _frame_set(oracle, rng, nf, 9000 if rng.random() < 0.3 else 1460)
+    fexp = oracle.validate_frames(farena, foffs, flens)
+    for low in (False, True):
+        fl = ctx.validate_frames(farena, foffs, flens, low_latency=low)
+        np.testing.assert_array_equal(fl, fexp, err_msg=f"host validate ({low}) case seed {seed}")
+    g = np.array(farena, copy=True)
+    e_arena, e_flags = oracle.generate_frames(farena, foffs, flens)
+    gfl = ctx.generate_frames(g, foffs, flens)
+    np.testing.assert_array_equal(gfl, e_flags, err_msg=f"host generate flags case seed {seed}")
+    assert np.array_equal(g, e_arena), f"host generate bytes case seed {seed}"
+
+
+def test_fuzz_host_context_vs_oracle(oracle):
+    ctxs = [csum.HostContext(0, c) for c in (0, 65536 + 16, 1 << 20)]
+    try:
+        if os.environ.get("TULIPS_FUZZ_CASE"):
+            _host_case(oracle, ctxs, int(os.environ["TULIPS_FUZZ_CASE"]))
+            return
+        budget = float(os.environ.get("TULIPS_FUZZ_SECONDS", "8"))
+        seed0 = int(os.environ.get("TULIPS_FUZZ_SEED", "1"))
+        t0 = last = time.monotonic()
+        done = 0
+        while done == 0 or time.monotonic() - t0 < budget:
+            _host_case(oracle, ctxs, seed0 * 1_000_039 + done)
+            done += 1
+            if time.monotonic() - last > 20:
+                last = time.monotonic()
+                print(f"fuzz host: {done} cases, {last - t0:.0f} s", flush=True)
+        print(f"fuzz host: {done} cases in {time.monotonic() - t0:.1f} s", flush=True)
+    finally:
+        for c in ctxs:
+            c.close()
