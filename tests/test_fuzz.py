@@ -390,3 +390,86 @@ def test_fuzz_host_context_vs_oracle(oracle):
     finally:
         for c in ctxs:
             c.close()
+
+
+# ------------------------------------------------ multi-device context -------
+def _mctx_case(oracle, mctxs, seed):
+    """The multi-device context over 1..5 logical devices (all GPU 0 here,
+    peer and staged modes): host batches, device-resident arena and
+    fixed-stride batches spread over the devices, host and device-resident
+    flow-affine validation, against the oracle (device_of against the
+    reference-pinned host hash mod the table)."""
+    rng = np.random.default_rng(seed)
+    m = mctxs[int(rng.integers(0, len(mctxs)))]
+    n = int(np.exp(rng.uniform(0, np.log(30001)))) - 1
+    lens = _lengths(rng, n)
+    gaps = rng.integers(0, 40, n) * (rng.random(n) < 0.5)
+    base = int(rng.integers(0, 16))
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[:] = base + np.concatenate(([0], np.cumsum(lens.astype(np.int64) + gaps)[:-1]))
+    nbytes = int(offs[-1]) + int(lens[-1]) + 64 if n else 64
+    arena = _arena(rng, nbytes)
+    mode = _mode(rng)
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    what = f"mctx case seed {seed}: ndev={m.ndev} n={n}"
+    exp = oracle.batch(arena, offs, lens, src=src, dst=dst, mode=mode, nthreads=8)
+    np.testing.assert_array_equal(m.batch(arena, offs, lens, src=src, dst=dst, mode=mode), exp,
+                                  err_msg=f"host {what}")
+    if n:
+        da, do, dl = _d(arena), _d(offs.view(np.int64)), _d(lens.view(np.int16))
+        dsrc, ddst = _d(src.view(np.int32)), _d(dst.view(np.int32))
+        got = m.batch_arena_device(da, do, dl, arena_bytes=nbytes, src=dsrc, dst=ddst, mode=mode)
+        np.testing.assert_array_equal(_u16(got), exp, err_msg=f"arena device {what}")
+        L = int(lens[0])
+        stride = max(L + int(rng.integers(0, 48)), 1)
+        nf = max(0, min(n, (nbytes - base - L) // stride + 1))
+        if nf:
+            offs3 = base + np.arange(nf, dtype=np.uint64) * np.uint64(stride)
+            exp3 = oracle.batch(arena, offs3, np.full(nf, L, np.uint16), src=src[:nf],
+                                dst=dst[:nf], mode=mode, nthreads=8)
+            got3 = m.batch_fixed_device(da, stride, L, nf, src=dsrc[:nf], dst=ddst[:nf],
+                                        mode=mode, base_offset=base)
+            np.testing.assert_array_equal(_u16(got3), exp3, err_msg=f"fixed device {what}")
+    # flow-affine validation
+    nf = int(rng.integers(1, 500))
+    farena, foffs, flens = _frame_set(oracle, rng, nf, 1460)
+    key = rng.integers(0, 256, 40, dtype=np.uint8).tobytes()
+    table = rng.integers(0, m.ndev, int(rng.integers(1, 129)), dtype=np.uint16)
+    fexp = oracle.validate_frames(farena, foffs, flens)
+    fl, devof = m.validate_frames_rss(farena, foffs, flens, key, table)
+    np.testing.assert_array_equal(fl, fexp, err_msg=f"rss host flags {what}")
+    fa, fo, fln = _d(farena), _d(foffs.view(np.int64)), _d(flens.view(np.int16))
+    dfl, ddev = m.validate_frames_rss_device(fa, fo, fln, key, table)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dfl.cpu().numpy(), fexp, err_msg=f"rss device flags {what}")
+    np.testing.assert_array_equal(ddev.cpu().numpy().view(np.uint16), devof,
+                                  err_msg=f"rss device_of {what}")
+
+
+def test_fuzz_multi_device_context_vs_oracle(oracle):
+    mctxs = []
+    try:
+        for nd in (1, 2, 3, 5):
+            m = csum.MultiContext([0] * nd)
+            if nd == 3:
+                m.set_peer_mode(True)   # staged through page-locked host memory
+            mctxs.append(m)
+        if os.environ.get("TULIPS_FUZZ_CASE"):
+            _mctx_case(oracle, mctxs, int(os.environ["TULIPS_FUZZ_CASE"]))
+            return
+        budget = float(os.environ.get("TULIPS_FUZZ_SECONDS", "8"))
+        seed0 = int(os.environ.get("TULIPS_FUZZ_SEED", "1"))
+        t0 = last = time.monotonic()
+        done = 0
+        while done == 0 or time.monotonic() - t0 < budget:
+            _mctx_case(oracle, mctxs, seed0 * 1_000_081 + done)
+            done += 1
+            if time.monotonic() - last > 20:
+                last = time.monotonic()
+                print(f"fuzz mctx: {done} cases, {last - t0:.0f} s", flush=True)
+        print(f"fuzz mctx: {done} cases in {time.monotonic() - t0:.1f} s", flush=True)
+    finally:
+        for m in mctxs:
+            m.close()
