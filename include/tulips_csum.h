@@ -327,9 +327,7 @@ int tulips_rss_toeplitz_batch(const uint32_t* saddr, const uint32_t* daddr,
  * overwrites it with this call's counts { IPv4 frames, bad IP checksums, TCP
  * frames, TCP frames without L4_CSUM_OK } (zeros for n == 0). At least one of
  * flags / counters is required for n > 0. Counting uses the per-stream state
- * below, made on the stream's first counting call; made inside a stream
- * capture, that call returns InvalidArgument (count once on the stream before
- * capturing).
+ * below (a call captured in a graph gets counter shards the graph owns).
  */
 int tulips_csum_validate_frames(const uint8_t* base, const uint64_t* offsets,
                                 const uint16_t* lengths, uint32_t n,
@@ -531,8 +529,8 @@ int tulips_csum_segment_frames_host(tulips_csum_ctx* ctx, const uint8_t* in_base
  * from its first launch to its last, so host threads sharing a stream (e.g.
  * the NULL stream) never interleave their launch sequences. A counting call
  * captured in a HIP graph gets counter shards of its own, owned by the graph
- * (up to 16 per stream; count once on the stream before capturing); a
- * captured segmentation call, a workspace of its own.
+ * (no warm-up call needed); a captured segmentation call, a workspace of its
+ * own.
  *
  * tulips_csum_release_stream waits for `stream` and frees everything the
  * library holds for it, including shards and workspaces owned by graphs

@@ -189,6 +189,38 @@ def test_captured_counting_call_owns_its_shards():
 
 
 @pytest.mark.gpu
+def test_captured_counting_without_warmup_and_past_the_spares():
+    """A counting call captured on a stream that never counted directly, and
+    more captures on one stream than the spare shards made with the direct
+    ones: each capture gets zeroed shards of its own (made in relaxed capture
+    mode), and every graph's replays count exactly."""
+    import torch
+    from tulips_amd import csum
+    fx = frames_fixture()
+    fa, fo, fl = _dev(fx["arena"], fx["offsets"].astype(np.int64), fx["lengths"].view(np.int16))
+    fexp = counters_of(fx["expect"])
+    cap, other = torch.cuda.Stream(), torch.cuda.Stream()
+    graphs = []
+    for k in range(20):                    # > SPARE_SHARDS (16)
+        cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            csum.validate_frames(fa, fo, fl, counters=cnt, want_flags=False)
+        graphs.append((g, cnt))
+    for rep in range(2):
+        for g, cnt in graphs:
+            cnt.fill_(-1)
+            torch.cuda.synchronize()
+            with torch.cuda.stream(other):
+                g.replay()
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32), fexp)
+    del graphs
+    torch.cuda.synchronize()
+    csum.release_stream(cap.cuda_stream)
+
+
+@pytest.mark.gpu
 def test_release_stream_keeps_memory_flat(oracle):
     import torch
     from tulips_amd import csum

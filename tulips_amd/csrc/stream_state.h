@@ -9,12 +9,12 @@
 //    their launches queued as whole sequences, never interleaved.
 //  * The device is the stream's own (hipStreamGetDevice), not the calling
 //    thread's current device; state is allocated on that device.
-//  * A counting call captured in a HIP graph gets shards of its own (taken
-//    from a spare set made with the stream's direct shards), owned by the
-//    graph from then on, so replays never share shards with direct calls on
-//    the capture stream. A capture cannot allocate: count once on the stream
-//    before capturing (spares are made then), at most SPARE_SHARDS captured
-//    counting calls per stream until tulips_csum_release_stream.
+//  * A counting call captured in a HIP graph gets shards of its own, owned by
+//    the graph from then on, so replays never share shards with direct calls
+//    on the capture stream: a spare from the set made with the stream's
+//    direct shards, or, when none is left (or no direct counting call came
+//    first), shards made in relaxed capture mode and zeroed on a private
+//    stream.
 //  * Segmentation calls captured in a graph run on a workspace made for that
 //    capture and owned by the graph (no warm-up needed, nothing a later
 //    direct call does can free it under the graph).
@@ -100,8 +100,9 @@ hipError_t stream_state(hipStream_t stream, std::shared_ptr<StreamState>* out);
 bool stream_capturing(hipStream_t stream);
 
 // Counter shards for one counting call on `s` (caller holds s.call):
-// the stream's direct shards, or, inside a capture, a spare set the graph
-// keeps. hipErrorStreamCaptureUnsupported when a capture finds no spare.
+// the stream's direct shards, or, inside a capture, a zeroed set the graph
+// keeps (a spare, or made then). hipErrorStreamCaptureUnsupported when a
+// capture's set cannot be made.
 hipError_t call_shards(StreamState& s, bool capturing, uint32_t** out);
 
 // The split-form span words for one call on `s` (caller holds s.call): at

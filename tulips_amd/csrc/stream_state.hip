@@ -20,6 +20,7 @@ std::mutex g_mutex;
 std::map<std::pair<int, hipStream_t>, std::shared_ptr<StreamState>> g_states;
 
 constexpr size_t SHARD_BYTES = sizeof(uint32_t) * CNT_LINE * CNT_SHARDS;
+static_assert(SHARD_BYTES % 8 == 0, "shards are made as 64-bit words");
 
 hipError_t
 stream_device(hipStream_t stream, int* dev)
@@ -123,13 +124,27 @@ stream_capturing(hipStream_t stream)
   return cs != hipStreamCaptureStatusNone;
 }
 
+hipError_t zeroed_words(int device, uint64_t words, bool capturing, int count,
+                        hipStream_t stream, std::vector<uint64_t*>* out);
+
 hipError_t
 call_shards(StreamState& s, bool capturing, uint32_t** out)
 {
-  if (!s.shards) {
-    if (capturing) {
+  if (capturing && (!s.shards || s.spare.empty())) {
+    // a capture on a stream with no spare left (or none made yet: no direct
+    // counting call before it): shards of its own, made in relaxed capture
+    // mode and zeroed by a kernel node of the graph, owned by the graph
+    std::vector<uint64_t*> made;
+    const hipError_t e = zeroed_words(s.device, SHARD_BYTES / 8, true, 1, s.stream, &made);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
       return hipErrorStreamCaptureUnsupported;
     }
+    *out = reinterpret_cast<uint32_t*>(made[0]);
+    s.graph_owned.push_back(*out);
+    return hipSuccess;
+  }
+  if (!s.shards) {
     // direct shards plus the spares captured calls will take, one
     // allocation each, zeroed in stream order before any kernel uses them
     std::vector<uint32_t*> made;
@@ -152,54 +167,76 @@ call_shards(StreamState& s, bool capturing, uint32_t** out)
     *out = s.shards;
     return hipSuccess;
   }
-  if (s.spare.empty()) {
-    return hipErrorStreamCaptureUnsupported;
-  }
   *out = s.spare.back();
   s.spare.pop_back();
   s.graph_owned.push_back(*out);
   return hipSuccess;
 }
 
-// `count` arrays of zeroed words on `device` (not stream-ordered: used only
-// before any launch can read them). Inside a capture the thread's capture
-// mode is relaxed for the allocations, so hipMalloc is allowed, and the
-// zeroing runs on a private stream that is not capturing.
-hipError_t
-zeroed_words(int device, uint64_t words, bool capturing, int count, std::vector<uint64_t*>* out)
+// Zeroes words [0, n) of p (a kernel: inside a capture it is a kernel node
+// of the graph, which a captured hipMemsetAsync on an array allocated in the
+// capture did not reliably become).
+__global__ __launch_bounds__(256) void
+zero_words_kernel(uint64_t* __restrict__ p, uint64_t n)
 {
-  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-  if (capturing) {
-    (void)hipThreadExchangeStreamCaptureMode(&mode);
+  for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += uint64_t(gridDim.x) * 256) {
+    p[i] = 0;
   }
+}
+
+hipError_t
+launch_zero_words(uint64_t* p, uint64_t n, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  const uint64_t want = (n + 255) / 256;
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(zero_words_kernel, dim3(uint32_t(want < 1024 ? want : 1024)), dim3(256), 0,
+                     stream, p, n);
+  return hipGetLastError();
+}
+
+// `count` arrays of zeroed words on `device`, zeroed in `stream`'s order:
+// outside a capture the caller synchronises `stream` before anything else
+// can read them; inside a capture (the thread's capture mode relaxed for the
+// allocations, so hipMalloc is allowed) the zeroing is a kernel node of the
+// graph on the capturing stream, run before the captured kernels at every
+// replay. No stream is created or destroyed while a capture is in progress:
+// doing that (a private zeroing stream, as before) corrupted the HIP
+// runtime's graph state, and a later hipGraphLaunch crashed on it (the r04
+// SIGSEGV; tests/test_fuzz.py::test_fuzz_captured_graphs).
+hipError_t
+zeroed_words(int device, uint64_t words, bool capturing, int count, hipStream_t stream,
+             std::vector<uint64_t*>* out)
+{
   std::vector<void*> made;
   hipError_t e = hipSuccess;
-  for (int k = 0; k < count && e == hipSuccess; ++k) {
-    void* p = nullptr;
-    if ((e = device_malloc(device, &p, sizeof(uint64_t) * words)) == hipSuccess) {
-      made.push_back(p);
+  {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    if (capturing) {
+      (void)hipThreadExchangeStreamCaptureMode(&mode);
     }
-  }
-  int prev = 0;
-  (void)hipGetDevice(&prev);
-  if (e == hipSuccess && (e = hipSetDevice(device)) == hipSuccess) {
-    hipStream_t z = nullptr;
-    if ((e = hipStreamCreateWithFlags(&z, hipStreamNonBlocking)) == hipSuccess) {
-      for (void* p : made) {
-        if (e == hipSuccess) {
-          e = hipMemsetAsync(p, 0, sizeof(uint64_t) * words, z);
-        }
+    for (int k = 0; k < count && e == hipSuccess; ++k) {
+      void* p = nullptr;
+      if ((e = device_malloc(device, &p, sizeof(uint64_t) * words)) == hipSuccess) {
+        made.push_back(p);
       }
-      const hipError_t e2 = hipStreamSynchronize(z);
-      e = e != hipSuccess ? e : e2;
-      (void)hipStreamDestroy(z);
     }
-    (void)hipSetDevice(prev);
+    if (capturing) {
+      (void)hipThreadExchangeStreamCaptureMode(&mode);
+    }
   }
-  if (capturing) {
-    (void)hipThreadExchangeStreamCaptureMode(&mode);
+  for (void* p : made) {
+    if (e == hipSuccess) {
+      e = launch_zero_words(static_cast<uint64_t*>(p), words, stream);
+    }
   }
   if (e != hipSuccess) {
+    if (!capturing) {
+      (void)hipStreamSynchronize(stream);
+    }
     free_on(device, made);
     return e;
   }
@@ -219,7 +256,7 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64
       // direct words plus spares for captures, all zeroed before use
       const uint64_t want = need < 4096 ? 4096 : need;
       std::vector<uint64_t*> made;
-      hipError_t e = zeroed_words(s.device, want, false, 1 + SPARE_SHARDS, &made);
+      hipError_t e = zeroed_words(s.device, want, false, 1 + SPARE_SHARDS, s.stream, &made);
       if (e == hipSuccess) {
         e = hipStreamSynchronize(s.stream); // the old arrays are idle
       }
@@ -272,7 +309,7 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64
   } else {
     size = need < 4096 ? 4096 : need;
     std::vector<uint64_t*> made;
-    if (zeroed_words(s.device, size, true, 1, &made) != hipSuccess) {
+    if (zeroed_words(s.device, size, true, 1, s.stream, &made) != hipSuccess) {
       (void)hipGetLastError();
       return hipErrorStreamCaptureUnsupported;
     }
