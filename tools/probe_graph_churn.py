@@ -7,7 +7,9 @@ them, random drops. If this crashes in hipGraphLaunch as the library's fuzz
 does, the fault is the runtime's, not the library's. Variants (env):
 NOEMPTY=1 never forks a side stream that gets no work; SAME=1 replays on the
 current stream instead of a fresh pool stream; NODROP=1 never destroys a
-graph while others live (at most 8 are made). Prints progress; a crash ends
+graph while others live (at most 8 are made); MAXLIVE=k keeps at most k
+graphs (a new capture drops one); KEEPALL=1 never destroys a graph and
+keeps capturing. Prints progress; a crash ends
 the process (exit 139)."""
 import os
 import time
@@ -43,7 +45,7 @@ while time.monotonic() - t0 < budget:
             for sd in side:
                 main.wait_stream(sd)
         graphs.append((g, outs))
-        if len(graphs) > 8:
+        if not os.environ.get("KEEPALL") and len(graphs) > int(os.environ.get("MAXLIVE", "8")):
             graphs.pop(int(rng.integers(0, len(graphs))))
     elif op < 0.75:
         g, outs = graphs[int(rng.integers(0, len(graphs)))]
@@ -63,7 +65,7 @@ while time.monotonic() - t0 < budget:
         with torch.cuda.stream(s):
             o.add_(xs[0])
         torch.cuda.synchronize()
-    elif not os.environ.get("NODROP"):
+    elif not os.environ.get("NODROP") and not os.environ.get("KEEPALL"):
         graphs.pop(int(rng.integers(0, len(graphs))))
     steps += 1
     if time.monotonic() - last > 10:
