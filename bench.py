@@ -217,6 +217,11 @@ class Timer:
         # the capture stream and the branch streams, made once and reused by
         # every call (not drawn again from torch's recycled pool per call)
         self._streams = []
+        # every graph this timer captured, kept alive until the process ends:
+        # the HIP runtime torch bundles can crash in hipGraphLaunch after a
+        # multi-branch graph was destroyed (DESIGN.md §5 "The r04 SIGSEGV",
+        # tools/probe_graph_churn.py), and no launch follows the teardown
+        self._kept = []
 
     def streams(self, k):
         while len(self._streams) < k:
@@ -252,6 +257,7 @@ class Timer:
                 for sd in side:
                     main.wait_stream(sd)
             g.replay()                      # warm replay
+            self._kept.append(g)
         t.cuda.synchronize()
         if poison is not None:
             poison()
