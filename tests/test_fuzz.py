@@ -476,6 +476,9 @@ def test_fuzz_multi_device_context_vs_oracle(oracle):
 
 
 # ------------------------------------------------------ captured graphs ------
+_KEPT_GRAPHS = []
+
+
 class _Job:
     """One library call with its inputs on the device, its expected result,
     and output buffers made per use (a graph keeps the ones it captured)."""
@@ -587,9 +590,7 @@ def test_fuzz_captured_graphs(oracle):
     # crash, with torch kernels alone too (tools/probe_graph_churn.py;
     # DESIGN.md §5). TULIPS_FUZZ_GRAPH_DESTROY=1 destroys them (that crash).
     destroy = bool(os.environ.get("TULIPS_FUZZ_GRAPH_DESTROY"))
-    if not (destroy or os.environ.get("TULIPS_FUZZ_GRAPHS")):
-        pytest.skip("opt-in: TULIPS_FUZZ_GRAPHS=1")
-    kept = []
+    kept = _KEPT_GRAPHS    # (alive to the end of the process: later tests launch graphs)
     budget = float(os.environ.get("TULIPS_FUZZ_SECONDS", "8"))
     seed = int(os.environ.get("TULIPS_FUZZ_CASE") or os.environ.get("TULIPS_FUZZ_SEED", "1"))
     rng = np.random.default_rng(seed * 1_000_099)
@@ -661,4 +662,6 @@ def test_fuzz_captured_graphs(oracle):
             last = time.monotonic()
             print(f"fuzz graphs: {steps} steps, {last - t0:.0f} s", flush=True)
     torch.cuda.synchronize()
+    if not destroy:
+        kept.extend(g for g, _ in graphs)
     print(f"fuzz graphs: {steps} steps in {time.monotonic() - t0:.1f} s", flush=True)
