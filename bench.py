@@ -167,21 +167,34 @@ def gate(stream):
     """Queue the untimed start delay (tulips_csum_gpu_sleep) on `stream`."""
     if START_DELAY_US > 0:
         from tulips_amd import csum
-        rc = csum.lib.tulips_csum_gpu_sleep(START_DELAY_US, stream.cuda_stream)
+        rc = _bench().lib.tulips_csum_gpu_sleep(START_DELAY_US, stream.cuda_stream)
         if rc:
             raise csum.CsumError(rc, "tulips_csum_gpu_sleep")
+
+
+def _bench():
+    """The measurement library (benchlib/, include/tulips_csum_bench.h): the
+    device data fill, the ceiling kernels, the start-delay sleep."""
+    import benchlib
+    return benchlib
 
 
 class CheckedLib:
     """csum.lib with every status-returning call checked: a non-zero status
     raises CsumError at the call, which also ends a graph capture in progress
-    (torch.cuda.graph's exit), so no capture can silently miss a launch."""
+    (torch.cuda.graph's exit), so no capture can silently miss a launch.
+    Names the product does not export (the ceiling kernels) resolve in the
+    measurement library."""
 
     def __init__(self, csum):
         self._csum = csum
 
     def __getattr__(self, name):
-        f, err = getattr(self._csum.lib, name), self._csum.CsumError
+        try:
+            f = getattr(self._csum.lib, name)
+        except AttributeError:
+            f = getattr(_bench().lib, name)
+        err = self._csum.CsumError
 
         def call(*a):
             rc = f(*a)
@@ -335,7 +348,7 @@ def main():
     from tulips_amd.shard import (all_ranks_ok, gather_results, gather_strings,
                                   max_over_ranks, shard_for)
     # a native crash names its frames before faulthandler prints Python's
-    checked_lib(csum).tulips_csum_debug_crash_backtrace(1)
+    _bench().crash_backtrace()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # control-plane reductions live on the GPU under RCCL, on the CPU under gloo
@@ -355,7 +368,7 @@ def main():
     shard = shard_for(rank, world)
     batch_bytes = NSEG * SEG
     arena = torch.empty(shard.nbytes + 256, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(arena, shard.nbytes, seed=DATA_SEED, byte_off=shard.byte_offset)
+    _bench().fill_splitmix(arena, shard.nbytes, seed=DATA_SEED, byte_off=shard.byte_offset)
     outs = torch.empty(NBATCH * NSEG, dtype=torch.uint16, device=dev)
     base = arena.data_ptr()
     optr = outs.data_ptr()
@@ -677,12 +690,12 @@ def extras_child():
     import torch
     from tulips_amd import csum
     from tulips_amd.shard import shard_for
-    checked_lib(csum).tulips_csum_debug_crash_backtrace(1)
+    _bench().crash_backtrace()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     shard = shard_for(0, 1)
     arena = torch.empty(shard.nbytes + 256, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(arena, shard.nbytes, seed=DATA_SEED, byte_off=shard.byte_offset)
+    _bench().fill_splitmix(arena, shard.nbytes, seed=DATA_SEED, byte_off=shard.byte_offset)
     torch.cuda.synchronize()
     ex = extras(torch, csum, dev, torch.cuda.current_stream(), arena, NSEG * SEG)
     print(json.dumps({"extras": ex}), flush=True)
@@ -882,7 +895,7 @@ def mctx_device_leg(torch, dist, csum, cdev, rank, world, args):
             d0 = torch.device("cuda", 0)
             with torch.cuda.device(d0):
                 arena = torch.empty(n * SEG + 64, dtype=torch.uint8, device=d0)
-                csum.fill_splitmix(arena, n * SEG, seed=DATA_SEED)
+                _bench().fill_splitmix(arena, n * SEG, seed=DATA_SEED)
                 out = torch.empty(n, dtype=torch.uint16, device=d0)
                 st = torch.cuda.current_stream(d0)
                 with csum.MultiContext(devs, chunk_bytes=1 << 20) as m:
@@ -938,7 +951,7 @@ def single_process_kernel_only(torch, csum, devs, rotations=4):
         dv = torch.device("cuda", d)
         with torch.cuda.device(dv):
             a = torch.empty(SHARD_SEGMENTS * SEG + 256, dtype=torch.uint8, device=dv)
-            csum.fill_splitmix(a, SHARD_SEGMENTS * SEG, seed=DATA_SEED,
+            _bench().fill_splitmix(a, SHARD_SEGMENTS * SEG, seed=DATA_SEED,
                                byte_off=k * SHARD_SEGMENTS * SEG)
             o = torch.empty(SHARD_SEGMENTS, dtype=torch.uint16, device=dv)
             st = torch.cuda.Stream(device=dv)
@@ -1121,7 +1134,7 @@ def zipf_sharded_leg(torch, dist, csum, dev, cdev, stream, rank, world):
     if len(ll) > 1:
         np.cumsum(ll[:-1], dtype=np.uint64, out=offs[1:])
     az = torch.empty(bs.nbytes + 256, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(az, bs.nbytes, byte_off=bs.byte_offset)
+    _bench().fill_splitmix(az, bs.nbytes, byte_off=bs.byte_offset)
     doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
     dlens = torch.from_numpy(ll.view(np.int16).copy()).to(dev)
     out = torch.empty(max(1, len(ll)), dtype=torch.uint16, device=dev)
@@ -1303,7 +1316,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     L9, NB9 = 9000, 4
     b9 = NSEG * L9
     a9 = torch.empty(NB9 * b9 + 256, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(a9, NB9 * b9)
+    _bench().fill_splitmix(a9, NB9 * b9)
     o9 = torch.empty(NB9 * NSEG, dtype=torch.uint16, device=dev)
     fixed = lib.tulips_csum_batch_fixed
     p9 = poisoner(o9)
@@ -1380,7 +1393,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
         ncp = 4
         cb = NSEG * S
         ac = torch.empty(ncp * cb + 256, dtype=torch.uint8, device=dev)
-        csum.fill_splitmix(ac, cb)
+        _bench().fill_splitmix(ac, cb)
         for c in range(1, ncp):
             ac[c * cb:(c + 1) * cb].copy_(ac[:cb])
         oc = torch.empty(ncp * NSEG, dtype=torch.uint16, device=dev)
@@ -1417,7 +1430,7 @@ def extras(torch, csum, dev, stream, arena, batch_bytes):
     zb = int(lens.astype(np.int64).sum())
     nz = 24
     az = torch.empty(nz * zb + 256, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(az, nz * zb)
+    _bench().fill_splitmix(az, nz * zb)
     doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
     dlens = torch.from_numpy(lens).to(dev)
     oz = torch.empty(nz * NSEG, dtype=torch.uint16, device=dev)
@@ -1630,7 +1643,7 @@ def burst_latency(torch, csum):
                                          ("cpu_product", 2, False), ("decorator", 3, False)):
                 ctx.set_lowlat(resident)
                 reps = 2000 if nf <= 64 else 300
-                rc = csum.lib.tulips_csum_time_validate(
+                rc = _bench().lib.tulips_csum_time_validate(
                     ctx._h, path, pinned.data_ptr(), offs.ctypes.data, lens.ctypes.data, nf,
                     reps, flags.ctypes.data, out)
                 if rc:
@@ -1657,7 +1670,7 @@ def burst_latency(torch, csum):
             for name, path in (("zero_copy", 1), ("cpu_product", 2), ("decorator", 3)):
                 ctx.set_lowlat(False)
                 reps = int(min(nb, 2000))
-                rc = csum.lib.tulips_csum_time_validate_ring(
+                rc = _bench().lib.tulips_csum_time_validate_ring(
                     ctx._h, path, ring.data_ptr(), len(ar), nb, offs.ctypes.data,
                     lens.ctypes.data, nf, reps, flags.ctypes.data, out)
                 ent[name] = ({"error": rc} if rc else
@@ -1737,7 +1750,7 @@ def frame_extras(torch, csum, dev, timer):
     # 1.07 GB in all so the rotation streams from HBM.
     nf, slot, flen, nb = NSEG, 2048, SEG + 14, 8
     ar = torch.empty(nb * nf * slot, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(ar, seed=0xF4A3E5)
+    _bench().fill_splitmix(ar, seed=0xF4A3E5)
     v = ar.view(nb * nf, slot)
     for off, val in ((12, 0x08), (13, 0), (14, 0x45), (15, 0), (16, SEG >> 8),
                      (17, SEG & 0xFF), (20, 0x40), (21, 0), (23, 6), (46, 0x50)):
@@ -1830,7 +1843,7 @@ def frame_extras(torch, csum, dev, timer):
     sslot = 65536
     sb = 4
     sa = torch.empty(sb * nsf * sslot, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(sa, seed=0x7505)
+    _bench().fill_splitmix(sa, seed=0x7505)
     sv = sa.view(sb * nsf, sslot)
     tot = sflen - 14
     for off, val_ in ((12, 0x08), (13, 0), (14, 0x45), (15, 0), (16, tot >> 8),

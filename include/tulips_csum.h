@@ -276,6 +276,11 @@ int tulips_csum_mctx_validate_frames_rss_device(tulips_csum_mctx* ctx, const uin
                                                 void* stream);
 /* The shard bounds (ndevices + 1 entries) of the context's last call. */
 int tulips_csum_mctx_shard_bounds(const tulips_csum_mctx* ctx, uint32_t* bounds);
+/* How the device-resident calls move a piece to a device other than the
+ * source: 0 = over xGMI (peer DMA) where hipDeviceCanAccessPeer allows it,
+ * else staged through page-locked host memory (the default); 1 = always
+ * staged through page-locked host memory. */
+int tulips_csum_mctx_set_peer_mode(tulips_csum_mctx* ctx, int mode);
 
 /* ---- Toeplitz RSS hash -------------------------------- */
 /*
@@ -390,10 +395,10 @@ int tulips_csum_generate_fields(const uint8_t* base, const uint64_t* offsets,
  * The library keeps a device workspace per (device, stream), made or grown
  * on a call that needs more room; calls on one stream run in order, calls
  * on different streams may overlap. The calls a stream capture records on a
- * stream share a workspace made for that capture and owned by the graph
- * (freed by tulips_csum_release_stream), so no warm-up call is needed, later
- * direct calls never free it under the graph, and a replay may overlap
- * direct calls on the capture stream.
+ * stream share a workspace made for that capture and owned by the graph (see
+ * "per-stream state" below), so no warm-up call is needed, later direct
+ * calls never free it under the graph, and a replay may overlap direct calls
+ * on the capture stream.
  */
 int tulips_csum_segment_frames(const uint8_t* in_base,
                                const uint64_t* in_offsets,
@@ -521,23 +526,119 @@ int tulips_csum_segment_frames_host(tulips_csum_ctx* ctx, const uint8_t* in_base
                                     uint64_t out_stride, uint32_t out_capacity,
                                     uint16_t* out_lengths, uint32_t* out_first);
 
+/* ---- explicit kernel geometry -------------------------------------------- */
+/*
+ * The entry points above pick their kernel geometry themselves
+ * (tulips_csum_default_tuning). These forms take it from the caller, for
+ * geometry sweeps and the parity tests of every shipped geometry; results are
+ * identical whatever the geometry.
+ */
+/* Kernel families (tulips_csum_tuning.kind). Kinds 2 and 4 (hybrid,
+   workgroup-balanced) and the other span forms are measured variants kept
+   outside the library (tools/variants/); the library rejects them. */
+#define TULIPS_CSUM_KIND_DEFAULT 0
+#define TULIPS_CSUM_KIND_SUBGROUP 1 /* `group` lanes (16/32/64) per segment,
+                                       `unroll` chunks per lane in flight
+                                       (16/32: 2/4/8; 32: 3; 64: 4/8/9/10/12) */
+#define TULIPS_CSUM_KIND_PACKED 3   /* variable only: one wave per `group`
+                                       segments (8/16), their chunks packed
+                                       end to end, `unroll` 64-chunk windows
+                                       per batch (2/4), double-buffered
+                                       (`sps` 2) */
+#define TULIPS_CSUM_KIND_SPAN 5     /* in-order arenas only
+                                       (tulips_csum_batch_arena): a workgroup
+                                       per 4 KiB * `unroll` (4..8) of arena
+                                       bytes; a segment crossing ranges is
+                                       summed in parts that meet in a
+                                       per-range word of the stream's state.
+                                       `group` 0 (or 7: the same form);
+                                       `group` 9 (unroll 6..8): the
+                                       tail-shaped cut, the last `sps` %
+                                       (0 = 12) of the arena in ranges of
+                                       unroll / 2 rows (measured variant);
+                                       `group` 10 (unroll 6..8): the uniform
+                                       cut with each quarter of the ranges at
+                                       instruction priority 3..0 (measured
+                                       variant) */
+
+/* Explicit kernel geometry. Zero fields pick the library default. */
+typedef struct tulips_csum_tuning
+{
+  int32_t kind;        /* TULIPS_CSUM_KIND_* */
+  int32_t group;       /* see kind */
+  int32_t unroll;      /* see kind */
+  int32_t nontemporal; /* bit 0: nt loads, bit 1: nt result stores; -1 = default */
+  uint32_t max_blocks; /* grid cap; 0 = default */
+  int32_t block;       /* threads per workgroup: 256, 512 or 1024 (fixed-length
+                          batches and frames also 64 or 128); 0 = default */
+  int32_t sps;         /* PACKED: 2 = double-buffered windows (the only
+                          form; 0 = default) */
+} tulips_csum_tuning;
+
+/* The geometry tulips_csum_batch_fixed / tulips_csum_batch would pick. */
+int tulips_csum_default_tuning(uint32_t fixed_length, int variable,
+                               tulips_csum_tuning* out);
+
+int tulips_csum_batch_fixed_tuned(const uint8_t* base, uint64_t stride,
+                                  uint32_t length, const uint16_t* seeds,
+                                  const uint32_t* src, const uint32_t* dst,
+                                  uint16_t* out, uint32_t n, uint32_t mode,
+                                  const tulips_csum_tuning* tuning,
+                                  void* stream);
+
+int tulips_csum_batch_tuned(const uint8_t* base, const uint64_t* offsets,
+                            const uint16_t* lengths, const uint16_t* seeds,
+                            const uint32_t* src, const uint32_t* dst,
+                            uint16_t* out, uint32_t n, uint32_t mode,
+                            const tulips_csum_tuning* tuning, void* stream);
+
+int tulips_csum_batch_arena_tuned(const uint8_t* base, uint64_t arena_bytes,
+                                  const uint64_t* offsets, const uint16_t* lengths,
+                                  const uint16_t* seeds, const uint32_t* src,
+                                  const uint32_t* dst, uint16_t* out, uint32_t n,
+                                  uint32_t mode, const tulips_csum_tuning* tuning,
+                                  void* stream);
+
+/* Frame kernels (include/tulips_csum.h) with an explicit geometry: op 0 =
+ * tulips_csum_validate_frames, op 1 = tulips_csum_generate_frames (counters
+ * ignored), op 2 = tulips_csum_generate_fields (`counters` is the n-entry
+ * fields array). Uses tuning->group (lanes per frame, 0 = 16), unroll
+ * (chunks in flight per lane, 0 = 6; supported pairs 16x4, 16x6, 16x8, 8x8,
+ * 8x16, 32x4, 64x2), nontemporal (bit 0: nt loads, -1 = on), max_blocks and
+ * block (64, 128, 256, 512 or 1024 threads; 0 = 256); sps 2 = two frames per subgroup in flight, 3 = a software pipeline
+ * (the next frame's loads issued before this one is summed, ~4 frames per
+ * subgroup) (validation at 16 x 6 only; otherwise ignored); kind is ignored. */
+int tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
+                             const uint16_t* lengths, uint32_t n,
+                             uint8_t* flags, uint32_t* counters,
+                             const tulips_csum_tuning* tuning, void* stream);
+
 /* ---- per-stream state ---------------------------------------------------- */
 /*
  * Counting calls (tulips_csum_verify, tulips_csum_validate_frames with
- * counters) and tulips_csum_segment_frames keep a small device workspace per
- * (device, stream), on the stream's own device. A call holds the stream's lock
- * from its first launch to its last, so host threads sharing a stream (e.g.
- * the NULL stream) never interleave their launch sequences. A counting call
- * captured in a HIP graph gets counter shards of its own, owned by the graph
- * (no warm-up call needed); a captured segmentation call, a workspace of its
- * own.
+ * counters), the arena calls (tulips_csum_batch_arena, _verify_arena) and
+ * tulips_csum_segment_frames keep a small device workspace per (device,
+ * stream), on the stream's own device. A call holds the stream's lock from
+ * its first launch to its last, so host threads sharing a stream (e.g. the
+ * NULL stream) never interleave their launch sequences.
  *
- * tulips_csum_release_stream waits for `stream` and frees everything the
- * library holds for it, including shards and workspaces owned by graphs
- * captured on it
- * (destroy those graphs first). Call it before hipStreamDestroy; it must not
- * race calls on the same stream. Later calls on the stream start afresh.
- * tulips_csum_ctx_destroy releases the context's own streams.
+ * A call captured in a HIP graph (stream capture) runs on arrays made for
+ * that capture, so no warm-up call is needed and replays never share arrays
+ * with direct calls or with other graphs. The graph owns them, as the
+ * reference's callers own their buffers (src/transport/list/Device.cpp:
+ * 60-62): they are attached to the graph as a HIP user object
+ * (hipGraphRetainUserObject), every executable instantiated from it holds a
+ * reference, and once the graph and all its executables are destroyed the
+ * arrays are freed by the library's next uncaptured call on any stream (or by
+ * tulips_csum_release_stream). Graphs may be destroyed in any order and at
+ * any time after their last replay completes.
+ *
+ * tulips_csum_release_stream waits for `stream` and frees the arrays the
+ * library holds for that stream's direct calls, plus the arrays of graphs
+ * destroyed so far. Call it before hipStreamDestroy; it must not race calls
+ * on the same stream. Later calls on the stream start afresh; graphs
+ * captured on it stay valid. tulips_csum_ctx_destroy releases the context's
+ * own streams.
  */
 int tulips_csum_release_stream(void* stream);
 

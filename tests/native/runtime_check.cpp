@@ -1,0 +1,620 @@
+// runtime_check.cpp — the product library driven through its C ABI from a
+// plain C++ process: no torch, no Python, linked against the ROCm runtime an
+// integrator links (/opt/rocm, libamdhip64.so.7 by the library's RUNPATH).
+// Test infrastructure (tests/test_native_runtime.py runs it on the GPU box).
+//
+//   runtime_check runtime
+//       which libamdhip64 the process mapped (dl_iterate_phdr) and the HIP
+//       runtime/driver versions, as one JSON line.
+//   runtime_check zipf-lengths
+//       (no GPU) the FNV-1a-64 digest and total of the §8c Zipf lengths.
+//   runtime_check parity NAME=FNV ...
+//       the SURVEY.md §8c golden batches F1500, F1500-tcp, F9000, F9000-tcp,
+//       ZIPF, ZIPF-tcp (and ZIPF_LENGTHS, the Zipf length sequence itself):
+//       SplitMix64 arena made on the host, copied to HBM, checksummed by
+//       tulips_csum_batch_fixed / tulips_csum_batch_arena / tulips_csum_batch,
+//       FNV-1a-64 of the outputs compared with the expected digests (the
+//       driving test passes tests/golden/digests.json's). Semantics:
+//       /root/reference/src/stack/Utils.cpp:14-42 and
+//       src/stack/tcpv4/Processor.cpp:337-357.
+//   runtime_check user-object
+//       the HIP user-object contract the library's graph ownership relies on
+//       (stream_state.h): a user object moved to a capture's graph survives
+//       the graph's destruction while an executable instantiated from it
+//       lives, and its destructor runs once the last of them is gone.
+//   runtime_check graph-cycles N
+//       N single-stream cycles of capture (counting verify, arena batch,
+//       segmentation), instantiate, destroy the template, replay twice,
+//       destroy the executable: every replay's outputs equal the direct
+//       calls', and device memory (hipMemGetInfo, after 5 warm-up cycles)
+//       ends within 1 MiB of where it started (also reported half-way).
+// Exit status 0 = all checks passed; every result is printed as JSON.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <link.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/tulips_csum.h"
+
+namespace {
+
+#define HIP_OK(x)                                                                    \
+  do {                                                                               \
+    const hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(3);                                                                       \
+    }                                                                                \
+  } while (0)
+
+#define CS_OK(x)                                                                     \
+  do {                                                                               \
+    const int rc_ = (x);                                                             \
+    if (rc_ != TULIPS_STATUS_OK) {                                                   \
+      fprintf(stderr, "%s:%d %s: status %d (%s)\n", __FILE__, __LINE__, #x, rc_,     \
+              tulips_csum_last_error());                                             \
+      exit(4);                                                                       \
+    }                                                                                \
+  } while (0)
+
+// ---- SURVEY.md §8c golden spec ----------------------------------------------
+constexpr uint64_t ARENA_SEED = 0x54554C495053ull;
+constexpr uint64_t ZIPF_SEED = 0x5A495046ull;
+constexpr uint32_t ZIPF_RMAX = 8937;
+constexpr uint32_t NSEG = 65536;
+
+uint64_t
+splitmix_next(uint64_t& s)
+{
+  s += 0x9E3779B97F4A7C15ull;
+  uint64_t z = s;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// the arena byte stream: 8 little-endian bytes per draw, continuous
+void
+splitmix_fill(uint8_t* dst, uint64_t nbytes)
+{
+  uint64_t s = ARENA_SEED;
+  uint64_t i = 0;
+  for (; i + 8 <= nbytes; i += 8) {
+    const uint64_t z = splitmix_next(s);
+    memcpy(dst + i, &z, 8);
+  }
+  if (i < nbytes) {
+    const uint64_t z = splitmix_next(s);
+    memcpy(dst + i, &z, nbytes - i);
+  }
+}
+
+// Zipf lengths: u = (next >> 11) * 2^-53, r = first index with
+// C[r] >= u * C[rmax], C[r] = sum_{k<=r} k^-1.1 summed in order; L = 63 + r
+std::vector<uint16_t>
+zipf_lengths(uint32_t n)
+{
+  std::vector<double> c(ZIPF_RMAX);
+  double acc = 0;
+  for (uint32_t k = 1; k <= ZIPF_RMAX; ++k) {
+    acc += std::pow(double(k), -1.1);
+    c[k - 1] = acc;
+  }
+  std::vector<uint16_t> out(n);
+  uint64_t s = ZIPF_SEED;
+  for (uint32_t i = 0; i < n; ++i) {
+    const double u = double(splitmix_next(s) >> 11) * 0x1p-53;
+    const double t = u * c.back();
+    const uint32_t r = uint32_t(std::lower_bound(c.begin(), c.end(), t) - c.begin()) + 1;
+    out[i] = uint16_t(63 + r);
+  }
+  return out;
+}
+
+uint64_t
+fnv1a_u16(const std::vector<uint16_t>& v)
+{
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint16_t x : v) {
+    h = (h ^ (x & 0xff)) * 0x100000001b3ull;
+    h = (h ^ (x >> 8)) * 0x100000001b3ull;
+  }
+  return h;
+}
+
+uint32_t
+ip4(uint8_t a, uint8_t b, uint8_t c, uint8_t d)
+{
+  return uint32_t(a) | uint32_t(b) << 8 | uint32_t(c) << 16 | uint32_t(d) << 24;
+}
+
+template<class T>
+T*
+to_device(const std::vector<T>& v)
+{
+  void* p = nullptr;
+  HIP_OK(hipMalloc(&p, std::max<size_t>(1, v.size()) * sizeof(T)));
+  if (!v.empty()) {
+    HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  }
+  return static_cast<T*>(p);
+}
+
+template<class T>
+std::vector<T>
+to_host(const T* p, size_t n)
+{
+  std::vector<T> v(n);
+  HIP_OK(hipMemcpy(v.data(), p, n * sizeof(T), hipMemcpyDeviceToHost));
+  return v;
+}
+
+std::string
+hex64(uint64_t v)
+{
+  char b[17];
+  snprintf(b, sizeof(b), "%016llx", static_cast<unsigned long long>(v));
+  return b;
+}
+
+// ---- runtime --------------------------------------------------------------------
+int
+find_hip(struct dl_phdr_info* info, size_t, void* data)
+{
+  if (info->dlpi_name && strstr(info->dlpi_name, "libamdhip64")) {
+    static_cast<std::vector<std::string>*>(data)->push_back(info->dlpi_name);
+  }
+  return 0;
+}
+
+std::string
+runtime_json()
+{
+  std::vector<std::string> libs;
+  dl_iterate_phdr(find_hip, &libs);
+  int rt = 0, drv = 0;
+  (void)hipRuntimeGetVersion(&rt);
+  (void)hipDriverGetVersion(&drv);
+  std::string s = "{\"hip_runtime_libs\": [";
+  for (size_t i = 0; i < libs.size(); ++i) {
+    s += (i ? ", \"" : "\"") + libs[i] + "\"";
+  }
+  s += "], \"hip_runtime_version\": " + std::to_string(rt) +
+       ", \"hip_driver_version\": " + std::to_string(drv) + ", \"library\": \"" +
+       tulips_csum_version() + "\"}";
+  return s;
+}
+
+// ---- parity ---------------------------------------------------------------------
+int
+cmd_parity(int argc, char** argv)
+{
+  std::map<std::string, std::string> want;
+  for (int i = 0; i < argc; ++i) {
+    const char* eq = strchr(argv[i], '=');
+    if (!eq) {
+      fprintf(stderr, "expected NAME=FNV, got %s\n", argv[i]);
+      return 2;
+    }
+    want[std::string(argv[i], size_t(eq - argv[i]))] = eq + 1;
+  }
+  const std::vector<uint16_t> zl = zipf_lengths(NSEG);
+  uint64_t ztotal = 0;
+  std::vector<uint64_t> zoffs(NSEG);
+  for (uint32_t i = 0; i < NSEG; ++i) {
+    zoffs[i] = ztotal;
+    ztotal += zl[i];
+  }
+  // one arena for all batches: the largest is F9000 (NSEG * 9000 bytes)
+  const uint64_t nbytes = uint64_t(NSEG) * 9000;
+  std::vector<uint8_t> host(nbytes + 64, 0);
+  splitmix_fill(host.data(), nbytes);
+  uint8_t* arena = to_device(host);
+  host.clear();
+  host.shrink_to_fit();
+  uint16_t* out = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&out), NSEG * 2));
+  uint32_t* src = to_device(std::vector<uint32_t>(NSEG, ip4(10, 1, 0, 1)));
+  uint32_t* dst = to_device(std::vector<uint32_t>(NSEG, ip4(10, 1, 0, 2)));
+  uint64_t* d_zoffs = to_device(zoffs);
+  uint16_t* d_zlens = to_device(zl);
+  hipStream_t st = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+
+  std::map<std::string, std::string> got;
+  auto digest = [&]() {
+    HIP_OK(hipStreamSynchronize(st));
+    return hex64(fnv1a_u16(to_host(out, NSEG)));
+  };
+  got["ZIPF_LENGTHS"] = hex64(fnv1a_u16(zl));
+  for (uint32_t L : { 1500u, 9000u }) {
+    const std::string name = "F" + std::to_string(L);
+    CS_OK(tulips_csum_batch_fixed(arena, L, L, nullptr, nullptr, nullptr, out, NSEG,
+                                  TULIPS_CSUM_RAW, st));
+    got[name] = digest();
+    CS_OK(tulips_csum_batch_fixed(arena, L, L, nullptr, src, dst, out, NSEG, TULIPS_CSUM_TCP,
+                                  st));
+    got[name + "-tcp"] = digest();
+  }
+  CS_OK(tulips_csum_batch_arena(arena, ztotal, d_zoffs, d_zlens, nullptr, nullptr, nullptr, out,
+                                NSEG, TULIPS_CSUM_RAW, st));
+  got["ZIPF"] = digest();
+  CS_OK(tulips_csum_batch_arena(arena, ztotal, d_zoffs, d_zlens, nullptr, src, dst, out, NSEG,
+                                TULIPS_CSUM_TCP, st));
+  got["ZIPF-tcp"] = digest();
+  // the any-layout entry point over the same Zipf segments
+  CS_OK(tulips_csum_batch(arena, d_zoffs, d_zlens, nullptr, nullptr, nullptr, out, NSEG,
+                          TULIPS_CSUM_RAW, st));
+  got["ZIPF-any"] = digest();
+  if (want.count("ZIPF")) {
+    want["ZIPF-any"] = want["ZIPF"];
+  }
+
+  int bad = 0;
+  std::string s = "{\"parity\": {";
+  bool first = true;
+  for (auto& kv : got) {
+    const auto w = want.find(kv.first);
+    const bool ok = w != want.end() && w->second == kv.second;
+    bad += ok ? 0 : 1;
+    s += std::string(first ? "" : ", ") + "\"" + kv.first + "\": {\"fnv1a64\": \"" + kv.second +
+         "\", \"expect\": \"" + (w == want.end() ? "" : w->second) + "\", \"ok\": " +
+         (ok ? "true" : "false") + "}";
+    first = false;
+  }
+  s += "}, \"runtime\": " + runtime_json() + "}";
+  printf("%s\n", s.c_str());
+  HIP_OK(hipStreamDestroy(st));
+  (void)hipFree(arena);
+  (void)hipFree(out);
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  (void)hipFree(d_zoffs);
+  (void)hipFree(d_zlens);
+  return bad ? 1 : 0;
+}
+
+// ---- user objects ---------------------------------------------------------------
+std::atomic<int> g_fired{ 0 };
+std::atomic<bool> g_same_thread{ false };
+std::thread::id g_main;
+
+void
+on_destroy(void*)
+{
+  g_same_thread = std::this_thread::get_id() == g_main;
+  g_fired.fetch_add(1);
+}
+
+int
+fired_after_settle()
+{
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  return g_fired.load();
+}
+
+int
+cmd_user_object()
+{
+  g_main = std::this_thread::get_id();
+  hipStream_t s = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  void* d = nullptr;
+  HIP_OK(hipMalloc(&d, 4096));
+  struct Order
+  {
+    const char* name;
+    bool exec_first;
+  };
+  std::string js = "{\"user_object\": [";
+  int bad = 0;
+  for (const Order o : { Order{ "template_destroyed_first", false },
+                         Order{ "exec_destroyed_first", true } }) {
+    g_fired = 0;
+    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    HIP_OK(hipMemsetAsync(d, 1, 4096, s));
+    hipStreamCaptureStatus cs;
+    unsigned long long id = 0;
+    hipGraph_t cg = nullptr;
+    HIP_OK(hipStreamGetCaptureInfo_v2(s, &cs, &id, &cg, nullptr, nullptr));
+    hipUserObject_t obj = nullptr;
+    HIP_OK(hipUserObjectCreate(&obj, nullptr, on_destroy, 1, hipUserObjectNoDestructorSync));
+    HIP_OK(hipGraphRetainUserObject(cg, obj, 1, hipGraphUserObjectMove));
+    HIP_OK(hipMemsetAsync(d, 2, 4096, s));
+    hipGraph_t g = nullptr;
+    HIP_OK(hipStreamEndCapture(s, &g));
+    const bool same_graph = g == cg;
+    hipGraphExec_t x = nullptr;
+    HIP_OK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+    int after_first = 0, after_launch = 0, after_second = 0;
+    if (o.exec_first) {
+      HIP_OK(hipGraphLaunch(x, s));
+      HIP_OK(hipStreamSynchronize(s));
+      after_launch = fired_after_settle();
+      HIP_OK(hipGraphExecDestroy(x));
+      after_first = fired_after_settle();
+      HIP_OK(hipGraphDestroy(g));
+      after_second = fired_after_settle();
+    } else {
+      HIP_OK(hipGraphDestroy(g));
+      after_first = fired_after_settle();
+      HIP_OK(hipGraphLaunch(x, s));
+      HIP_OK(hipStreamSynchronize(s));
+      after_launch = fired_after_settle();
+      HIP_OK(hipGraphExecDestroy(x));
+      after_second = fired_after_settle();
+    }
+    const bool ok = same_graph && after_first == 0 && after_launch == 0 && after_second == 1;
+    bad += ok ? 0 : 1;
+    char b[400];
+    snprintf(b, sizeof(b),
+             "%s{\"order\": \"%s\", \"capture_graph_is_result\": %s, \"fired_after_first_destroy\": "
+             "%d, \"fired_after_launch\": %d, \"fired_after_last_destroy\": %d, "
+             "\"destructor_on_calling_thread\": %s, \"ok\": %s}",
+             o.exec_first ? ", " : "", o.name, same_graph ? "true" : "false", after_first,
+             after_launch, after_second, g_same_thread ? "true" : "false", ok ? "true" : "false");
+    js += b;
+  }
+  js += "], \"runtime\": " + runtime_json() + "}";
+  printf("%s\n", js.c_str());
+  (void)hipFree(d);
+  HIP_OK(hipStreamDestroy(s));
+  return bad ? 1 : 0;
+}
+
+// ---- graph cycles ---------------------------------------------------------------
+struct Rng
+{
+  uint64_t s;
+  uint32_t next() { return uint32_t(splitmix_next(s) >> 32); }
+};
+
+void
+put16(uint8_t* p, uint16_t v)
+{
+  p[0] = uint8_t(v >> 8);
+  p[1] = uint8_t(v);
+}
+
+// an Ethernet / option-less IPv4 / TCP frame with `payload` bytes
+std::vector<uint8_t>
+tcp_frame(Rng& r, uint32_t payload)
+{
+  std::vector<uint8_t> f(14 + 20 + 20 + payload);
+  for (auto& b : f) {
+    b = uint8_t(r.next());
+  }
+  put16(&f[12], 0x0800);
+  uint8_t* ip = &f[14];
+  ip[0] = 0x45;
+  ip[1] = 0;
+  put16(ip + 2, uint16_t(40 + payload));
+  put16(ip + 6, 0x4000); // DF
+  ip[8] = 64;
+  ip[9] = 6;
+  uint8_t* tcp = ip + 20;
+  tcp[12] = 5 << 4;
+  tcp[13] = 0x18; // PSH | ACK
+  return f;
+}
+
+int
+cmd_graph_cycles(uint32_t cycles)
+{
+  Rng r{ 0x6c69666574696d65ull };
+  // counting + arena batch: 4,096 segments of 40-9000 bytes, packed in order
+  const uint32_t n = 4096;
+  std::vector<uint16_t> lens(n);
+  std::vector<uint64_t> offs(n);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    lens[i] = uint16_t(40 + r.next() % 8960);
+    offs[i] = total;
+    total += lens[i];
+  }
+  std::vector<uint8_t> bytes(total + 64);
+  for (auto& b : bytes) {
+    b = uint8_t(r.next());
+  }
+  uint8_t* d_arena = to_device(bytes);
+  uint64_t* d_offs = to_device(offs);
+  uint16_t* d_lens = to_device(lens);
+  uint32_t* src = to_device(std::vector<uint32_t>(n, ip4(10, 1, 0, 1)));
+  uint32_t* dst = to_device(std::vector<uint32_t>(n, ip4(10, 1, 0, 2)));
+  // segmentation: 24 super-frames of 1-60 KB payload, 2 KiB-aligned in
+  std::vector<uint8_t> frames;
+  std::vector<uint64_t> foffs;
+  std::vector<uint16_t> flens;
+  for (int k = 0; k < 24; ++k) {
+    const std::vector<uint8_t> f = tcp_frame(r, 1000 + r.next() % 59000);
+    foffs.push_back(frames.size());
+    flens.push_back(uint16_t(f.size()));
+    frames.insert(frames.end(), f.begin(), f.end());
+    frames.resize((frames.size() + 2047) & ~size_t(2047));
+  }
+  const uint32_t nf = uint32_t(foffs.size()), mss = 1460, ostride = 2048, cap = 1024;
+  uint8_t* d_frames = to_device(frames);
+  uint64_t* d_foffs = to_device(foffs);
+  uint16_t* d_flens = to_device(flens);
+
+  struct Outs
+  {
+    uint16_t* csum;
+    uint32_t* bad;
+    uint16_t* arena;
+    uint8_t* seg;
+    uint16_t* seg_lens;
+    uint32_t* first;
+  };
+  auto make_outs = [&]() {
+    Outs o{};
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.csum), n * 2));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.bad), 4));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.arena), n * 2));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.seg), size_t(cap) * ostride));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.seg_lens), cap * 2));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.first), (nf + 1) * 4));
+    return o;
+  };
+  auto clear = [&](const Outs& o, hipStream_t s) {
+    HIP_OK(hipMemsetAsync(o.csum, 0xA5, n * 2, s));
+    HIP_OK(hipMemsetAsync(o.bad, 0xA5, 4, s));
+    HIP_OK(hipMemsetAsync(o.arena, 0xA5, n * 2, s));
+    HIP_OK(hipMemsetAsync(o.seg, 0xA5, size_t(cap) * ostride, s));
+    HIP_OK(hipMemsetAsync(o.seg_lens, 0xA5, cap * 2, s));
+    HIP_OK(hipMemsetAsync(o.first, 0xA5, (nf + 1) * 4, s));
+  };
+  auto calls = [&](const Outs& o, hipStream_t s) {
+    CS_OK(tulips_csum_verify(d_arena, d_offs, d_lens, src, dst, o.csum, o.bad, n,
+                             TULIPS_CSUM_TCP, s));
+    CS_OK(tulips_csum_batch_arena(d_arena, total, d_offs, d_lens, nullptr, nullptr, nullptr,
+                                  o.arena, n, TULIPS_CSUM_INET, s));
+    CS_OK(tulips_csum_segment_frames(d_frames, d_foffs, d_flens, nf, mss, o.seg, ostride, cap,
+                                     o.seg_lens, o.first, s));
+  };
+  struct Snap
+  {
+    std::vector<uint16_t> csum, arena, seg_lens;
+    std::vector<uint32_t> bad, first;
+    std::vector<uint8_t> seg;
+    bool operator==(const Snap& b) const
+    {
+      return csum == b.csum && arena == b.arena && seg_lens == b.seg_lens && bad == b.bad &&
+             first == b.first && seg == b.seg;
+    }
+  };
+  auto snap = [&](const Outs& o) {
+    Snap x;
+    x.csum = to_host(o.csum, n);
+    x.bad = to_host(o.bad, 1);
+    x.arena = to_host(o.arena, n);
+    x.first = to_host(o.first, nf + 1);
+    x.seg_lens = to_host(o.seg_lens, cap);
+    x.seg = to_host(o.seg, size_t(cap) * ostride);
+    return x;
+  };
+
+  hipStream_t s = nullptr, other = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&other, hipStreamNonBlocking));
+  const Outs direct = make_outs(), replay = make_outs();
+  clear(direct, s);
+  calls(direct, s);
+  HIP_OK(hipStreamSynchronize(s));
+  const Snap want = snap(direct);
+  const uint32_t segs = want.first[nf];
+  uint32_t mismatches = 0;
+  auto cycle = [&](uint32_t c, bool check_all) {
+    hipGraph_t g = nullptr;
+    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    calls(replay, s);
+    HIP_OK(hipStreamEndCapture(s, &g));
+    hipGraphExec_t x = nullptr;
+    HIP_OK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+    HIP_OK(hipGraphDestroy(g)); // as torch.cuda.CUDAGraph does
+    for (int rep = 0; rep < 2; ++rep) {
+      hipStream_t on = rep ? other : s;
+      clear(replay, on);
+      HIP_OK(hipGraphLaunch(x, on));
+      HIP_OK(hipStreamSynchronize(on));
+      // a direct call on the capture stream between replays
+      if (rep == 0) {
+        calls(direct, s);
+      }
+      if (check_all || c % 25 == 0) {
+        mismatches += snap(replay) == want ? 0 : 1;
+      } else {
+        mismatches += to_host(replay.bad, 1) == want.bad && to_host(replay.arena, n) == want.arena
+                        ? 0
+                        : 1;
+      }
+    }
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipGraphExecDestroy(x));
+  };
+  // the library's next uncaptured call frees what the destroyed graphs held
+  auto free_now = [&]() {
+    calls(direct, s);
+    HIP_OK(hipDeviceSynchronize());
+    size_t f = 0, t = 0;
+    HIP_OK(hipMemGetInfo(&f, &t));
+    return f;
+  };
+  // warm-up: the runtime's own first-use pools (graph instantiation, kernel
+  // arguments) are made here, before the measured cycles
+  for (uint32_t c = 0; c < 5; ++c) {
+    cycle(c, true);
+  }
+  const size_t free0 = free_now();
+  size_t free_half = 0;
+  for (uint32_t c = 0; c < cycles; ++c) {
+    cycle(c, c + 1 == cycles);
+    if (c + 1 == cycles / 2) {
+      free_half = free_now();
+    }
+  }
+  const size_t free1 = free_now();
+  mismatches += snap(direct) == want ? 0 : 1;
+  const long long grew = (long long)free0 - (long long)free1;
+  const bool ok = mismatches == 0 && grew < (1ll << 20);
+  printf("{\"graph_cycles\": %u, \"segments\": %u, \"mismatches\": %u, \"free_before\": %zu, "
+         "\"free_half\": %zu, \"free_after\": %zu, \"device_memory_growth\": %lld, "
+         "\"ok\": %s, \"runtime\": %s}\n",
+         cycles, segs, mismatches, free0, free_half, free1, grew, ok ? "true" : "false",
+         runtime_json().c_str());
+  CS_OK(tulips_csum_release_stream(s));
+  CS_OK(tulips_csum_release_stream(other));
+  HIP_OK(hipStreamDestroy(s));
+  HIP_OK(hipStreamDestroy(other));
+  return ok ? 0 : 1;
+}
+
+} // namespace
+
+int
+main(int argc, char** argv)
+{
+  if (argc < 2) {
+    fprintf(stderr, "usage: %s runtime | parity NAME=FNV... | user-object | graph-cycles N\n",
+            argv[0]);
+    return 2;
+  }
+  const std::string cmd = argv[1];
+  if (cmd == "runtime") {
+    printf("%s\n", runtime_json().c_str());
+    return 0;
+  }
+  if (cmd == "zipf-lengths") { // no GPU: the §8c length sequence's digest and total
+    const std::vector<uint16_t> zl = zipf_lengths(NSEG);
+    uint64_t total = 0;
+    for (uint16_t l : zl) {
+      total += l;
+    }
+    printf("{\"fnv1a64\": \"%s\", \"total\": %llu}\n", hex64(fnv1a_u16(zl)).c_str(),
+           static_cast<unsigned long long>(total));
+    return 0;
+  }
+  if (cmd == "parity") {
+    return cmd_parity(argc - 2, argv + 2);
+  }
+  if (cmd == "user-object") {
+    return cmd_user_object();
+  }
+  if (cmd == "graph-cycles" && argc == 3) {
+    return cmd_graph_cycles(uint32_t(strtoul(argv[2], nullptr, 10)));
+  }
+  fprintf(stderr, "unknown command %s\n", cmd.c_str());
+  return 2;
+}

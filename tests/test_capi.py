@@ -13,16 +13,26 @@ from tulips_amd import csum
 from oracle import ip4
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("tulips_csum.h", "tulips_csum_util.h")]
+PRODUCT_H = os.path.join(ROOT, "include", "tulips_csum.h")
+BENCH_H = os.path.join(ROOT, "include", "tulips_csum_bench.h")
 
 
-def declared_functions():
-    names = []
-    for h in HEADERS:
-        text = open(h).read()
-        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-        names += re.findall(r"\b(tulips_csum_\w+)\s*\(", text)
-    return sorted(set(names))
+def declared_functions(header=PRODUCT_H):
+    text = open(header).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tulips_(?:csum|rss)_\w+)\s*\(", text)))
+
+
+def exported(path):
+    """Defined dynamic symbols of a shared library (binutils nm -D)."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm")
+    if nm is None:
+        pytest.skip("nm not installed")
+    out = subprocess.run([nm, "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return sorted(line.split()[-1] for line in out.splitlines() if line.strip())
 
 
 def test_library_exports_every_declared_symbol():
@@ -31,6 +41,21 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(csum.lib, n), f"{n} declared in include/ but not exported"
         assert n in csum._SIGNATURES, f"{n} has no ctypes signature"
+
+
+def test_product_exports_exactly_the_header_and_reference_symbols():
+    """The product .so exports include/tulips_csum.h and the reference's own
+    C++ symbols (include/tulips/stack/Utils.h:10-11 & co.), nothing else:
+    no measurement entry points, internal C++ or HIP registration symbols
+    (tulips_amd/csrc/libtulips_csum.map)."""
+    assert exported(csum.LIB_PATH) == sorted(declared_functions() + list(csum.CXX_SYMBOLS))
+
+
+def test_bench_library_exports_exactly_its_header():
+    import benchlib
+    got = exported(benchlib.LIB_PATH)
+    assert got == declared_functions(BENCH_H)
+    assert not set(got) & set(exported(csum.LIB_PATH))
 
 
 def test_reference_cxx_symbols_exported():
@@ -181,26 +206,6 @@ def test_batch_validation_without_gpu():
     assert lib.tulips_csum_ctx_create(0, 0, None) == 1
     assert lib.tulips_csum_ctx_destroy(None) == 1
     assert lib.tulips_csum_batch_host(None, FAKE, FAKE, FAKE, None, None, None, FAKE, 4, 0) == 1
-    assert lib.tulips_csum_stream_read(FAKE + 1, 16, FAKE, 0, None) == 1
-    assert lib.tulips_csum_stream_read_tiles(FAKE, 0, 4, FAKE, None) == 1
-    assert lib.tulips_csum_stream_read_slots(FAKE, 2048, 0, 4, FAKE, None) == 1
-    assert lib.tulips_csum_stream_read_slots(FAKE, 1000, 1514, 4, FAKE, None) == 1
-    assert lib.tulips_csum_stream_read_slots(FAKE, 70000, 65536, 4, FAKE, None) == 1
-    assert lib.tulips_csum_stream_read_slots(None, 2048, 1514, 0, None, None) == 0
-    g = lib.tulips_csum_stream_read_slots_geom
-    assert g(FAKE, 1500, 1500, 4, 32, 4, FAKE, None) == 1                 # geometry
-    assert g(FAKE, 1500, 1500, 4, 64, 12, FAKE, None) == 1
-    assert g(FAKE, 1000, 1500, 4, 32, 3, FAKE, None) == 1                 # slot < read
-    assert g(None, 0, 0, 0, 32, 3, None, None) == 0                       # nothing to do
-    cp = lib.tulips_csum_stream_copy_slots
-    assert cp(FAKE, 65536, 0, 1460, 1514, 4, FAKE, 1536, None) == 1       # per_group 0
-    assert cp(FAKE, 65536, 44, 1460, 0, 4, FAKE, 1536, None) == 1         # no bytes
-    assert cp(FAKE, 65536, 44, 1460, 70000, 4, FAKE, 70016, None) == 1    # > 65535
-    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE + 8, 1536, None) == 1  # misaligned out
-    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE, 1528, None) == 1      # stride % 16
-    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE, 1504, None) == 1      # stride < bytes
-    assert cp(None, 65536, 44, 1460, 1514, 4, FAKE, 1536, None) == 1
-    assert cp(None, 0, 0, 0, 0, 0, None, 0, None) == 0                    # nothing to do
 
 
 def test_python_binding_raises_typed_errors():
@@ -253,16 +258,16 @@ def test_missing_library_fails_loudly(tmp_path):
 
 
 def test_crash_backtrace_names_native_frames(tmp_path):
-    """tulips_csum_debug_crash_backtrace (bench.py installs it): a SIGSEGV in
+    """tulips_csum_debug_crash_backtrace (benchlib; bench.py installs it): a SIGSEGV in
     native code prints the native call stack, then Python's faulthandler (the
     handler installed before) prints the interpreter's, and the process still
     dies of the signal."""
     import subprocess
     import sys
     prog = ("import faulthandler, sys, ctypes; faulthandler.enable(); "
-            f"sys.path.insert(0, {ROOT!r}); from tulips_amd import csum; "
-            "assert csum.lib.tulips_csum_debug_crash_backtrace(1) == 0; "
-            "assert csum.lib.tulips_csum_debug_crash_backtrace(2) == 1; "
+            f"sys.path.insert(0, {ROOT!r}); import benchlib; "
+            "assert benchlib.lib.tulips_csum_debug_crash_backtrace(1) == 0; "
+            "assert benchlib.lib.tulips_csum_debug_crash_backtrace(2) == 1; "
             "ctypes.string_at(16)")
     r = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True,
                        timeout=300, cwd=tmp_path)
@@ -316,3 +321,30 @@ def test_no_kernel_spills_to_scratch(tmp_path):
                 spilling.append((name.group(1) if name else "?", size))
     assert kernels >= 100, kernels
     assert not spilling, spilling
+
+
+def test_bench_library_rejects_bad_arguments():
+    """The measurement library's ceiling kernels (include/tulips_csum_bench.h)
+    validate their arguments before any launch (no GPU call is made)."""
+    import benchlib
+    lib = benchlib.lib
+    assert lib.tulips_csum_stream_read(FAKE + 1, 16, FAKE, 0, None) == 1
+    assert lib.tulips_csum_stream_read_tiles(FAKE, 0, 4, FAKE, None) == 1
+    assert lib.tulips_csum_stream_read_slots(FAKE, 2048, 0, 4, FAKE, None) == 1
+    assert lib.tulips_csum_stream_read_slots(FAKE, 1000, 1514, 4, FAKE, None) == 1
+    assert lib.tulips_csum_stream_read_slots(FAKE, 70000, 65536, 4, FAKE, None) == 1
+    assert lib.tulips_csum_stream_read_slots(None, 2048, 1514, 0, None, None) == 0
+    g = lib.tulips_csum_stream_read_slots_geom
+    assert g(FAKE, 1500, 1500, 4, 32, 4, FAKE, None) == 1                 # geometry
+    assert g(FAKE, 1500, 1500, 4, 64, 12, FAKE, None) == 1
+    assert g(FAKE, 1000, 1500, 4, 32, 3, FAKE, None) == 1                 # slot < read
+    assert g(None, 0, 0, 0, 32, 3, None, None) == 0                       # nothing to do
+    cp = lib.tulips_csum_stream_copy_slots
+    assert cp(FAKE, 65536, 0, 1460, 1514, 4, FAKE, 1536, None) == 1       # per_group 0
+    assert cp(FAKE, 65536, 44, 1460, 0, 4, FAKE, 1536, None) == 1         # no bytes
+    assert cp(FAKE, 65536, 44, 1460, 70000, 4, FAKE, 70016, None) == 1    # > 65535
+    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE + 8, 1536, None) == 1  # misaligned out
+    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE, 1528, None) == 1      # stride % 16
+    assert cp(FAKE, 65536, 44, 1460, 1514, 4, FAKE, 1504, None) == 1      # stride < bytes
+    assert cp(None, 65536, 44, 1460, 1514, 4, FAKE, 1536, None) == 1
+    assert cp(None, 0, 0, 0, 0, 0, None, 0, None) == 0                    # nothing to do

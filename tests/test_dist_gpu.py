@@ -43,6 +43,7 @@ def _worker(rank, world, port, q):
     import torch.distributed as dist
     import bench
     from tulips_amd import csum
+    import benchlib
     from tulips_amd.shard import (all_ranks_ok, byte_shard_for, gather_results,
                                   gather_strings, shard_for)
 
@@ -57,7 +58,7 @@ def _worker(rank, world, port, q):
         # M8x1500 shard <rank>, as bench.py lays it out
         sh = shard_for(rank, world)
         arena = torch.empty(sh.nbytes + 256, dtype=torch.uint8, device=dev)
-        csum.fill_splitmix(arena, sh.nbytes, seed=bench.DATA_SEED, byte_off=sh.byte_offset)
+        benchlib.fill_splitmix(arena, sh.nbytes, seed=bench.DATA_SEED, byte_off=sh.byte_offset)
         outs = torch.empty(NBATCH * NSEG, dtype=torch.uint16, device=dev)
         for b in range(NBATCH):
             rc = lib.tulips_csum_batch_fixed(arena.data_ptr() + sh.batch_offset(b), SEG, SEG,
@@ -85,7 +86,7 @@ def _worker(rank, world, port, q):
         if len(ll) > 1:
             np.cumsum(ll[:-1], dtype=np.uint64, out=offs[1:])
         az = torch.empty(bs.nbytes + 256, dtype=torch.uint8, device=dev)
-        csum.fill_splitmix(az, bs.nbytes, byte_off=bs.byte_offset)
+        benchlib.fill_splitmix(az, bs.nbytes, byte_off=bs.byte_offset)
         doffs = torch.from_numpy(offs.view(np.int64)).to(dev)
         dlens = torch.from_numpy(ll.view(np.int16).copy()).to(dev)
         zo = torch.empty(max(1, len(ll)), dtype=torch.uint16, device=dev)

@@ -598,7 +598,8 @@ def test_fuzz_captured_graphs(oracle):
     if os.environ.get("TULIPS_FUZZ_KINDS"):              # (bisection: some kinds only)
         jobs = [j for j in jobs if j.kind in os.environ["TULIPS_FUZZ_KINDS"].split(",")]
     torch.cuda.synchronize()
-    csum.lib.tulips_csum_debug_crash_backtrace(1)      # a native crash names its frames
+    import benchlib
+    benchlib.crash_backtrace()                          # a native crash names its frames
     trace = os.environ.get("TULIPS_FUZZ_TRACE")
     graphs = []       # (graph, [(job, outs)])
     t0 = last = time.monotonic()

@@ -17,6 +17,7 @@ from oracle import (MODE_INET, MODE_RAW, MODE_TCP, FLAG_COMPLEMENT,  # noqa: E40
 
 import tulips_amd  # noqa: E402
 from tulips_amd import csum  # noqa: E402
+import benchlib  # noqa: E402
 
 DEV = "cuda:0"
 
@@ -116,7 +117,7 @@ def test_kat_through_device_batch(golden, oracle):
 # -- SURVEY.md §8c batches: digests at full size -------------------------------
 def _fill(nbytes, byte_off=0):
     buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=DEV)
-    csum.fill_splitmix(buf, nbytes, byte_off=byte_off)
+    benchlib.fill_splitmix(buf, nbytes, byte_off=byte_off)
     return buf
 
 
@@ -125,7 +126,7 @@ def test_device_fill_matches_spec(oracle):
     np.testing.assert_array_equal(h(buf)[: 1 << 20], oracle.splitmix_bytes(1 << 20))
     for off in (1, 3, 8, 12345):
         buf = torch.zeros(4096, dtype=torch.uint8, device=DEV)
-        csum.fill_splitmix(buf[5:], 1000, byte_off=off)
+        benchlib.fill_splitmix(buf[5:], 1000, byte_off=off)
         got = h(buf)
         np.testing.assert_array_equal(got[5:1005], oracle.splitmix_bytes(1000, byte_off=off))
         assert not got[:5].any() and not got[1005:].any()
@@ -182,7 +183,7 @@ def test_m8_all_shards(golden, oracle):
     arena = torch.empty(shard_n * L + 64, dtype=torch.uint8, device=DEV)
     outs = []
     for r in range(8):
-        csum.fill_splitmix(arena, shard_n * L, byte_off=r * shard_n * L)
+        benchlib.fill_splitmix(arena, shard_n * L, byte_off=r * shard_n * L)
         out = tulips_amd.batch_fixed(arena, L, L, shard_n)
         assert fnv(oracle, out) == b["shards"][r]["fnv1a64"], r
         outs.append(u16(out))
@@ -424,7 +425,7 @@ def test_fixed_small_workgroups(length, group, unroll):
     default launch's, odd counts and a capped grid included."""
     n = 4099
     arena = torch.empty(n * length + 64, dtype=torch.uint8, device=DEV)
-    csum.fill_splitmix(arena, n * length, seed=0x5EED + length)
+    benchlib.fill_splitmix(arena, n * length, seed=0x5EED + length)
     st = torch.cuda.current_stream().cuda_stream
     want = torch.empty(n, dtype=torch.int16, device=DEV)   # u16 results, viewed signed
     assert csum.lib.tulips_csum_batch_fixed(arena.data_ptr(), length, length, None, None, None,
@@ -455,7 +456,8 @@ def test_gpu_stream_read_slots_geom(group, unroll, stride, length):
     nbytes = ((n - 1) * stride + length + 15) // 16 * 16
     buf = torch.zeros(nbytes, dtype=torch.uint8, device="cuda:0")
     sink = torch.zeros(4, dtype=torch.int32, device="cuda:0")
-    assert csum.lib.tulips_csum_stream_read_slots_geom(buf.data_ptr(), stride, length, n, group,
-                                                       unroll, sink.data_ptr(), None) == 0
+    assert benchlib.lib.tulips_csum_stream_read_slots_geom(buf.data_ptr(), stride, length, n,
+                                                           group, unroll, sink.data_ptr(),
+                                                           None) == 0
     torch.cuda.synchronize()
     assert int(sink.sum().item()) == 0

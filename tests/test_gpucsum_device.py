@@ -106,7 +106,7 @@ def run_cpu_below(fx, burst, cpu_below, n=None):
     f = lib.gpucsum_run_cpu_below
     f.restype = C.c_int
     f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint16,
-                  C.c_uint32, C.c_void_p, C.c_void_p]
+                  C.c_int64, C.c_void_p, C.c_void_p]   # int64_t cpu_below (gpucsum_harness.cpp)
     n = len(fx["offsets"]) if n is None else n
     arena = np.ascontiguousarray(fx["arena"])
     offs = np.ascontiguousarray(fx["offsets"][:n])

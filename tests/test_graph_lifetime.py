@@ -1,0 +1,172 @@
+"""Graph-captured calls: the library's arrays live exactly as long as the graph
+(tulips_amd/csrc/stream_state.h, include/tulips_csum.h "per-stream state").
+
+The reference's callers own their buffers for the call only
+(/root/reference/src/transport/list/Device.cpp:60-62). A captured call needs
+arrays that outlive the call (counter shards, the arena calls' span words,
+the segmentation workspace), so the library attaches them to the capture's
+graph as a HIP user object: destroying the graph and its executables frees
+them (at the library's next uncaptured call). Here, on the runtime torch
+bundles:
+
+* the runtime honours that contract: a user object moved to a capture's graph
+  survives torch's CUDAGraph capture_end (which destroys the template after
+  instantiating it) and every replay, and is destroyed with the executable;
+* 500 single-stream graphs of counting, arena and segmentation calls are
+  captured, replayed (checked against the oracle every time) and destroyed,
+  and device memory returns to within 1 MiB of where it started.
+
+tests/test_native_runtime.py runs the same two checks from a plain C++
+process on the ROCm runtime an integrator links.
+"""
+import ctypes as C
+import gc
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from test_frames import _dev
+from test_segment import pack as seg_pack, super_frame
+from test_stream_state import _hip
+
+MODE_INET, MODE_TCP = 1, 2
+
+
+@pytest.mark.gpu
+def test_user_object_lives_with_the_executable():
+    import torch
+    hip = _hip()
+    destroy_fn = C.CFUNCTYPE(None, C.c_void_p)
+    fired = []
+    cb = destroy_fn(lambda p: fired.append(threading.get_ident()))
+    hip.hipStreamGetCaptureInfo_v2.argtypes = [C.c_void_p, C.POINTER(C.c_int),
+                                               C.POINTER(C.c_ulonglong), C.POINTER(C.c_void_p),
+                                               C.c_void_p, C.c_void_p]
+    hip.hipUserObjectCreate.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, destroy_fn,
+                                        C.c_uint, C.c_uint]
+    hip.hipGraphRetainUserObject.argtypes = [C.c_void_p, C.c_void_p, C.c_uint, C.c_uint]
+    x = torch.zeros(1024, device="cuda:0")
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        x.add_(1)
+        status, cid, graph = C.c_int(), C.c_ulonglong(), C.c_void_p()
+        assert hip.hipStreamGetCaptureInfo_v2(s.cuda_stream, C.byref(status), C.byref(cid),
+                                              C.byref(graph), None, None) == 0
+        assert status.value == 1 and graph.value          # hipStreamCaptureStatusActive
+        obj = C.c_void_p()
+        assert hip.hipUserObjectCreate(C.byref(obj), None, cb, 1, 1) == 0  # NoDestructorSync
+        assert hip.hipGraphRetainUserObject(graph, obj, 1, 1) == 0         # moved to the graph
+        x.add_(1)
+    time.sleep(0.05)
+    assert fired == [], "destroyed with the template: executables do not hold user objects"
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    time.sleep(0.05)
+    assert fired == []
+    assert float(x[0]) == 6.0                              # 3 replays of 2 adds
+    del g
+    gc.collect()
+    time.sleep(0.05)
+    assert len(fired) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_500_captured_graphs_leave_memory_flat(oracle):
+    """500 capture/replay/destroy cycles on one stream, every replay checked
+    against the oracle (verify count and results, arena batch, segmentation),
+    then one direct call; hipMemGetInfo ends within 1 MiB of its start."""
+    import torch
+    from tulips_amd import csum
+    rng = np.random.default_rng(500)
+    n = 4096
+    lens = rng.integers(40, 9000, n).astype(np.uint16)
+    offs = np.zeros(n, np.uint64)
+    np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+    total = int(lens.astype(np.int64).sum())
+    buf = rng.integers(0, 256, total + 16, dtype=np.uint8)
+    src = np.full(n, 0x0100010A, np.uint32)
+    dst = np.full(n, 0x0200010A, np.uint32)
+    exp_tcp = oracle.batch(buf, offs, lens, src=src, dst=dst, mode=MODE_TCP, nthreads=8)
+    exp_inet = oracle.batch(buf, offs, lens, mode=MODE_INET, nthreads=8)
+    exp_bad = int(np.count_nonzero(exp_tcp != 0xFFFF))
+    a, o, l, ds, dd = _dev(buf, offs.astype(np.int64), lens.view(np.int16), src.view(np.int32),
+                           dst.view(np.int32))
+    frames = [super_frame(oracle, rng, int(p)) for p in rng.integers(1000, 60000, 24)]
+    farena, foffs, flens = seg_pack(frames, rng)
+    mss, stride = 1460, 2048
+    efirst, eout, elens = oracle.segment_frames(farena, foffs, flens, mss, stride)
+    nseg = int(efirst[-1])
+    fa, fo, fl = _dev(farena, foffs.astype(np.int64), flens.view(np.int16))
+    e_first = torch.from_numpy(efirst.view(np.int32)).to("cuda:0")
+    e_out = torch.from_numpy(eout).to("cuda:0")
+    e_lens = torch.from_numpy(elens.view(np.int16)).to("cuda:0")
+    e_tcp = torch.from_numpy(exp_tcp.view(np.int16)).to("cuda:0")
+    e_inet = torch.from_numpy(exp_inet.view(np.int16)).to("cuda:0")
+    out_tcp = torch.empty(n, dtype=torch.int16, device="cuda:0")
+    bad = torch.empty(1, dtype=torch.int32, device="cuda:0")
+    out_inet = torch.empty(n, dtype=torch.int16, device="cuda:0")
+    seg_out = torch.empty(nseg * stride, dtype=torch.uint8, device="cuda:0")
+    seg_lens = torch.empty(nseg, dtype=torch.int16, device="cuda:0")
+    seg_first = torch.empty(len(frames) + 1, dtype=torch.int32, device="cuda:0")
+    outs = (out_tcp, bad, out_inet, seg_out, seg_lens, seg_first)
+    cap = torch.cuda.Stream()
+
+    def calls(st):
+        assert csum.lib.tulips_csum_verify(a.data_ptr(), o.data_ptr(), l.data_ptr(),
+                                           ds.data_ptr(), dd.data_ptr(), out_tcp.data_ptr(),
+                                           bad.data_ptr(), n, MODE_TCP, st) == 0
+        assert csum.lib.tulips_csum_batch_arena(a.data_ptr(), total, o.data_ptr(),
+                                                l.data_ptr(), None, None, None,
+                                                out_inet.data_ptr(), n, MODE_INET, st) == 0
+        assert csum.lib.tulips_csum_segment_frames(fa.data_ptr(), fo.data_ptr(), fl.data_ptr(),
+                                                   len(frames), mss, seg_out.data_ptr(), stride,
+                                                   nseg, seg_lens.data_ptr(),
+                                                   seg_first.data_ptr(), st) == 0
+
+    def poison():
+        for t in outs:
+            t.fill_(-91)
+
+    def exact():
+        # each segment's bytes only (the slot's tail past its length is not written)
+        got = seg_out.view(nseg, stride)
+        want = e_out.view(nseg, stride)
+        keep = (torch.arange(stride, device="cuda:0")[None, :] <
+                e_lens.to(torch.int64)[:, None])
+        return (torch.equal(out_tcp, e_tcp) and int(bad.item()) == exp_bad and
+                torch.equal(out_inet, e_inet) and torch.equal(seg_first, e_first) and
+                torch.equal(seg_lens, e_lens) and torch.equal(got[keep], want[keep]))
+
+    calls(cap.cuda_stream)                  # the stream's direct arrays exist before the start
+    torch.cuda.synchronize()
+    assert exact()
+    gc.collect()
+    free0, _ = torch.cuda.mem_get_info()
+    bad_replays = []
+    for cycle in range(500):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            calls(cap.cuda_stream)
+        for rep in range(2):
+            poison()
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            if not exact():
+                bad_replays.append((cycle, rep))
+        del g
+    calls(cap.cuda_stream)                  # reclaims what the destroyed graphs held
+    torch.cuda.synchronize()
+    gc.collect()
+    free1, _ = torch.cuda.mem_get_info()
+    assert not bad_replays, bad_replays[:10]
+    assert exact()
+    # without graph ownership each capture would keep ~1.7 MB (shards, span
+    # words, workspace): ~850 MB over 500 graphs
+    assert free0 - free1 < (1 << 20), (free0, free1)
+    csum.release_stream(cap.cuda_stream)

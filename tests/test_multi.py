@@ -84,12 +84,13 @@ def test_mctx_m8_two_shards_match_reference_digests():
     reference's shard digest."""
     import torch
     from tulips_amd import csum
+    import benchlib
     gold = golden()["M8x1500"]["shards"]
     nseg, seg = 1 << 20, 1500
     host = np.empty(2 * nseg * seg + 64, dtype=np.uint8)
     dev = torch.empty(nseg * seg + 64, dtype=torch.uint8, device="cuda:0")
     for s in range(2):
-        csum.fill_splitmix(dev, nseg * seg, byte_off=s * nseg * seg)
+        benchlib.fill_splitmix(dev, nseg * seg, byte_off=s * nseg * seg)
         host[s * nseg * seg:(s + 1) * nseg * seg] = dev[:nseg * seg].cpu().numpy()
     del dev
     offs = np.arange(2 * nseg, dtype=np.uint64) * np.uint64(seg)
@@ -145,13 +146,14 @@ def test_mctx_device_arena_zipf_digests(oracle, ndev):
     results home): ZIPF and ZIPF-tcp digests, byte-balanced bounds."""
     import torch
     from tulips_amd import csum
+    import benchlib
     from oracle import ip4
     g = golden()
     lens = oracle.zipf_lengths(65536)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     total = int(lens.astype(np.int64).sum())
     arena = torch.empty(total + 64, dtype=torch.uint8, device="cuda:0")
-    csum.fill_splitmix(arena, total)
+    benchlib.fill_splitmix(arena, total)
     do, dl = _dev(offs.view(np.int64)), _dev(lens)
     src = _dev(np.full(65536, ip4(10, 1, 0, 1), np.uint32))
     dst = _dev(np.full(65536, ip4(10, 1, 0, 2), np.uint32))
@@ -209,12 +211,13 @@ def test_mctx_device_fixed_m8_from_gpu0(oracle):
     boundaries. Then F1500-tcp through 3 logical devices."""
     import torch
     from tulips_amd import csum
+    import benchlib
     from oracle import ip4
     g = golden()
     gold = g["M8x1500"]
     n, seg = 8 << 20, 1500
     arena = torch.empty(n * seg + 64, dtype=torch.uint8, device="cuda:0")
-    csum.fill_splitmix(arena, n * seg)
+    benchlib.fill_splitmix(arena, n * seg)
     with csum.MultiContext([0] * 8) as m:
         out = m.batch_fixed_device(arena, seg, seg, n)
         torch.cuda.synchronize()
@@ -229,7 +232,7 @@ def test_mctx_device_fixed_m8_from_gpu0(oracle):
     bt = g["F1500-tcp"]
     nt = bt["n"]
     arena = torch.empty(nt * 1500 + 64, dtype=torch.uint8, device="cuda:0")
-    csum.fill_splitmix(arena, nt * 1500)
+    benchlib.fill_splitmix(arena, nt * 1500)
     src = _dev(np.full(nt, ip4(10, 1, 0, 1), np.uint32))
     dst = _dev(np.full(nt, ip4(10, 1, 0, 2), np.uint32))
     with csum.MultiContext([0] * 3) as m:
@@ -247,18 +250,19 @@ def test_mctx_device_staged_copies(oracle):
     back to peer copies (slots reused both ways)."""
     import torch
     from tulips_amd import csum
+    import benchlib
     from oracle import ip4
     g = golden()
     n = 65536
     arena = torch.empty(n * 1500 + 64, dtype=torch.uint8, device="cuda:0")
-    csum.fill_splitmix(arena, n * 1500)
+    benchlib.fill_splitmix(arena, n * 1500)
     src = _dev(np.full(n, ip4(10, 1, 0, 1), np.uint32))
     dst = _dev(np.full(n, ip4(10, 1, 0, 2), np.uint32))
     lens = oracle.zipf_lengths(n)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     ztot = int(lens.astype(np.int64).sum())
     za = torch.empty(ztot + 64, dtype=torch.uint8, device="cuda:0")
-    csum.fill_splitmix(za, ztot)
+    benchlib.fill_splitmix(za, ztot)
     do, dl = _dev(offs.view(np.int64)), _dev(lens)
 
     def dig(t):
@@ -285,13 +289,14 @@ def test_mctx_device_every_visible_gpu(oracle):
     otherwise): F1500 digest from GPU 0 over every device, both forms."""
     import torch
     from tulips_amd import csum
+    import benchlib
     nd = torch.cuda.device_count()
     if nd < 2:
         pytest.skip("one GPU visible")
     g = golden()
     n = 65536
     arena = torch.empty(n * 1500 + 64, dtype=torch.uint8, device="cuda:0")
-    csum.fill_splitmix(arena, n * 1500)
+    benchlib.fill_splitmix(arena, n * 1500)
     with csum.MultiContext(list(range(nd))) as m:
         for staged in (False, True):
             m.set_peer_mode(staged)

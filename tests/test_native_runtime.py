@@ -1,0 +1,66 @@
+"""The hot path on the runtime an integrator gets: tests/native/runtime_check
+(a plain C++ process, no torch, the library's NEEDED libamdhip64.so.7
+resolved through its RUNPATH to /opt/rocm) drives the C ABI and compares the
+SURVEY.md §8c golden digests (tests/golden/digests.json, made by the
+reference's own compiled sources) bit-exactly, checks the HIP user-object
+contract the graph ownership relies on, and runs 500 capture/replay/destroy
+cycles with device memory flat. Every pytest GPU run otherwise uses the HIP
+runtime torch bundles (tests/test_graph_lifetime.py covers that one).
+Semantics: /root/reference/src/stack/Utils.cpp:14-42,
+src/stack/tcpv4/Processor.cpp:337-357."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "native", "_build", "runtime_check")
+BATCHES = ("F1500", "F1500-tcp", "F9000", "F9000-tcp", "ZIPF", "ZIPF-tcp")
+
+
+def _run(*args, timeout=300):
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} is missing: `make native` (or __graft_entry__.build())")
+    p = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=timeout)
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    res = json.loads(lines[-1]) if lines else None
+    return p.returncode, res, p.stderr
+
+
+def test_zipf_lengths_match_the_spec(golden):
+    """CPU: the checker's own §8c Zipf generator reproduces the golden lengths."""
+    rc, res, err = _run("zipf-lengths")
+    assert rc == 0, err
+    z = golden.digests()["zipf_lengths"]
+    assert res["total"] == z["total"]
+    assert res["fnv1a64"] == z["fnv1a64"]
+
+
+@pytest.mark.gpu
+def test_native_parity_on_integrator_runtime(golden):
+    b = golden.digests()["batches"]
+    z = golden.digests()["zipf_lengths"]["fnv1a64"]
+    want = [f"{k}={b[k]['fnv1a64']}" for k in BATCHES] + [f"ZIPF_LENGTHS={z}"]
+    rc, res, err = _run("parity", *want)
+    print(json.dumps(res, indent=1))
+    assert res is not None, err
+    libs = res["runtime"]["hip_runtime_libs"]
+    assert libs and all("torch" not in p for p in libs), libs
+    bad = {k: v for k, v in res["parity"].items() if not v["ok"]}
+    assert rc == 0 and not bad, (bad, err)
+
+
+@pytest.mark.gpu
+def test_native_user_object_contract():
+    rc, res, err = _run("user-object")
+    print(json.dumps(res, indent=1))
+    assert rc == 0, (res, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_native_500_graph_cycles():
+    rc, res, err = _run("graph-cycles", "500", timeout=540)
+    print(json.dumps(res, indent=1))
+    assert rc == 0, (res, err)

@@ -67,13 +67,14 @@ def in_order(rng, lens, max_gap=0, gap_p=0.0):
 
 @pytest.mark.parametrize("name", ["ZIPF", "ZIPF-tcp"])
 def test_zipf_digest(golden, oracle, name):
+    import benchlib
     b = golden.digests()["batches"][name]
     n = b["n"]
     lens = oracle.zipf_lengths(n)
     offs = packed_offsets(lens)
     total = int(lens.astype(np.int64).sum())
     arena = torch.empty(total + 64, dtype=torch.uint8, device=DEV)
-    csum.fill_splitmix(arena, total)
+    benchlib.fill_splitmix(arena, total)
     kw = {}
     if b["mode"] == "tcp":
         kw = dict(src=d(np.full(n, ip4(10, 1, 0, 1), np.uint32)),

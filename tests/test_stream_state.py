@@ -5,9 +5,10 @@
   finalize are queued as one sequence under the stream's lock;
 * two host threads segmenting on the same stream each get their own output
   (the prologue and the segment kernel share the stream's workspace);
-* a counting call captured in a HIP graph owns its shards, so replaying the
-  graph on another stream while direct counting calls run on the capture
-  stream keeps both totals right;
+* a counting call captured in a HIP graph runs on shards of the graph's
+  (stream_state.h; their lifetime: tests/test_graph_lifetime.py), so
+  replaying the graph on another stream while direct counting calls run on
+  the capture stream keeps both totals right;
 * tulips_csum_release_stream frees what a stream holds: 100 streams created,
   used (verify, counted validation, segmentation), released and destroyed
   leave device memory flat;
@@ -159,7 +160,7 @@ def test_captured_counting_call_owns_its_shards():
     hexp = counters_of(fx["expect"][:half])
     cap = torch.cuda.Stream()
     g_cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
-    with torch.cuda.stream(cap):  # warm: makes the stream's shards and spares
+    with torch.cuda.stream(cap):  # the stream's direct shards exist before the capture
         csum.validate_frames(fa, fo, fl, counters=g_cnt, want_flags=False)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
@@ -189,11 +190,11 @@ def test_captured_counting_call_owns_its_shards():
 
 
 @pytest.mark.gpu
-def test_captured_counting_without_warmup_and_past_the_spares():
-    """A counting call captured on a stream that never counted directly, and
-    more captures on one stream than the spare shards made with the direct
-    ones: each capture gets zeroed shards of its own (made in relaxed capture
-    mode), and every graph's replays count exactly."""
+def test_captured_counting_without_warmup_many_graphs():
+    """Counting calls captured on a stream that never counted directly, 20
+    graphs on one stream: each capture gets zeroed shards of its own (made in
+    relaxed capture mode, zeroed by a kernel node of its graph), and every
+    graph's replays count exactly."""
     import torch
     from tulips_amd import csum
     fx = frames_fixture()
@@ -201,7 +202,7 @@ def test_captured_counting_without_warmup_and_past_the_spares():
     fexp = counters_of(fx["expect"])
     cap, other = torch.cuda.Stream(), torch.cuda.Stream()
     graphs = []
-    for k in range(20):                    # > SPARE_SHARDS (16)
+    for k in range(20):
         cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=cap):
@@ -269,8 +270,8 @@ def test_release_stream_keeps_memory_flat(oracle):
         cycle()
     torch.cuda.synchronize()
     free1, _ = torch.cuda.mem_get_info()
-    # unreleased, each stream would keep ~1.9 MB (17 shard sets, the scan
-    # totals, run map and descriptors, 17 span word arrays): 190 MB over 100
+    # unreleased, each stream would keep ~1.3 MB (its shards, the scan
+    # totals, run map and descriptors, its span words): 130 MB over 100
     # streams
     assert free0 - free1 < 8 << 20, (free0 - free1)
     np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),

@@ -1,5 +1,5 @@
-// csum_capi.hip — the C ABI of include/tulips_csum.h and
-// include/tulips_csum_util.h, plus the host scalar drop-ins that keep the
+// csum_capi.hip — the C ABI of include/tulips_csum.h (batches, tuning
+// forms, status strings), plus the host scalar drop-ins that keep the
 // reference's C++ symbols (tulips::stack::utils::checksum & co.).
 #include <execinfo.h>
 #include <hip/hip_runtime.h>
@@ -16,7 +16,6 @@
 #include <vector>
 
 #include "../../include/tulips_csum.h"
-#include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
 #include "stream_state.h"
@@ -405,7 +404,7 @@ batch_var(const uint8_t* base, const uint64_t* offsets, const uint16_t* lengths,
 
 // In-order arena batches (KIND_SPAN, csum_kernels.hip): the tuning's kind
 // must be DEFAULT or SPAN; unroll = chunks per lane (4 KiB of arena per
-// workgroup each), group 0 (or 7, the same form; include/tulips_csum_util.h).
+// workgroup each), group 0 (or 7, the same form; include/tulips_csum.h).
 int
 batch_arena(const uint8_t* base, uint64_t arena, const uint64_t* offsets,
             const uint16_t* lengths, const uint16_t* seeds, const uint32_t* src,
@@ -610,91 +609,6 @@ tulips_csum_batch_tuned(const uint8_t* base, const uint64_t* offsets,
                    mode, tuning, stream);
 }
 
-namespace {
-
-// One wave that returns after `ticks` of the 100 MHz realtime counter.
-__global__ __launch_bounds__(64) void
-gpu_sleep_kernel(uint64_t ticks)
-{
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
-    __builtin_amdgcn_s_sleep(8);
-  }
-}
-
-} // namespace
-
-int
-tulips_csum_gpu_sleep(uint32_t us, void* stream)
-{
-  if (us > 1000000u) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  (void)hipGetLastError();
-  hipLaunchKernelGGL(gpu_sleep_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
-                     uint64_t(us) * 100u);
-  return status_of(hipGetLastError());
-}
-
-int
-tulips_csum_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
-                          uint64_t byte_off, void* stream)
-{
-  if (nbytes && !dst) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  return status_of(launch_fill_splitmix(dst, nbytes, seed, byte_off,
-                                        static_cast<hipStream_t>(stream)));
-}
-
-int
-tulips_csum_stream_read(const uint8_t* p, uint64_t nbytes, uint32_t* sink,
-                        uint32_t max_blocks, void* stream)
-{
-  if ((nbytes && (!p || !sink)) || (reinterpret_cast<uintptr_t>(p) & 15)) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  return status_of(launch_stream_read(p, nbytes, sink, max_blocks,
-                                      static_cast<hipStream_t>(stream)));
-}
-
-int
-tulips_csum_stream_read_tiles(const uint8_t* p, uint64_t tile_bytes, uint32_t ntiles,
-                              uint32_t* sink, void* stream)
-{
-  if (ntiles && (!p || !sink || tile_bytes == 0 || tile_bytes > TULIPS_CSUM_MAX_SEGMENT)) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  return status_of(
-    launch_stream_tiles(p, tile_bytes, ntiles, sink, static_cast<hipStream_t>(stream)));
-}
-
-int
-tulips_csum_stream_read_slots(const uint8_t* p, uint64_t slot_bytes, uint32_t read_bytes,
-                              uint32_t nslots, uint32_t* sink, void* stream)
-{
-  if (nslots && (!p || !sink || read_bytes == 0 || read_bytes > TULIPS_CSUM_MAX_SEGMENT ||
-                 slot_bytes < read_bytes)) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  return status_of(launch_stream_slots(p, slot_bytes, read_bytes, nslots, 16, 6, sink,
-                                       static_cast<hipStream_t>(stream)));
-}
-
-int
-tulips_csum_stream_read_slots_geom(const uint8_t* p, uint64_t slot_bytes, uint32_t read_bytes,
-                                   uint32_t nslots, int group, int unroll, uint32_t* sink,
-                                   void* stream)
-{
-  const bool geom = (group == 16 && unroll == 6) || (group == 32 && unroll == 3);
-  if (!geom || (nslots && (!p || !sink || read_bytes == 0 ||
-                           read_bytes > TULIPS_CSUM_MAX_SEGMENT || slot_bytes < read_bytes))) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  return status_of(launch_stream_slots(p, slot_bytes, read_bytes, nslots, group, unroll, sink,
-                                       static_cast<hipStream_t>(stream)));
-}
-
 const char*
 tulips_csum_status_string(int status)
 {
@@ -728,90 +642,3 @@ tulips_csum_version(void)
 
 } // extern "C"
 
-// ---------------------------------------------------------------------------
-// tulips_csum_debug_crash_backtrace: native stack on a fatal signal.
-// ---------------------------------------------------------------------------
-namespace {
-
-constexpr int CRASH_SIGNALS[] = { SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT };
-struct sigaction g_crash_prev[sizeof(CRASH_SIGNALS) / sizeof(int)];
-bool g_crash_on = false;
-
-// async-signal-safe: write(2) of a decimal / hex number
-void
-crash_write(const char* s)
-{
-  (void)!write(2, s, strlen(s));
-}
-
-void
-crash_hex(uintptr_t v)
-{
-  char b[19] = "0x";
-  for (int i = 0; i < 16; ++i) {
-    const unsigned d = unsigned(v >> (60 - 4 * i)) & 15u;
-    b[2 + i] = char(d < 10 ? '0' + d : 'a' + d - 10);
-  }
-  b[18] = 0;
-  crash_write(b);
-}
-
-void
-crash_handler(int sig, siginfo_t* si, void* uc)
-{
-  crash_write("\ntulips_csum: fatal signal ");
-  char num[4] = { char('0' + (sig / 10) % 10), char('0' + sig % 10), 0, 0 };
-  crash_write(num);
-  crash_write(" (");
-  crash_write(sig == SIGSEGV ? "SIGSEGV" : sig == SIGBUS ? "SIGBUS" : sig == SIGILL ? "SIGILL"
-              : sig == SIGFPE ? "SIGFPE" : "SIGABRT");
-  crash_write(") at address ");
-  crash_hex(si ? reinterpret_cast<uintptr_t>(si->si_addr) : 0);
-  crash_write("; native stack:\n");
-  void* frames[64];
-  const int n = backtrace(frames, 64);
-  backtrace_symbols_fd(frames, n, 2);
-  // the earlier handler takes it from here: restored, then the signal is
-  // delivered again (a faulting instruction re-executes on return; abort()
-  // raises SIGABRT a second time once its handler returns)
-  for (size_t k = 0; k < sizeof(CRASH_SIGNALS) / sizeof(int); ++k) {
-    if (CRASH_SIGNALS[k] == sig) {
-      (void)sigaction(sig, &g_crash_prev[k], nullptr);
-    }
-  }
-  if (si && si->si_code <= 0) {
-    (void)raise(sig); // sent by kill/raise: nothing re-executes
-  }
-  (void)uc;
-}
-
-} // namespace
-
-extern "C" int
-tulips_csum_debug_crash_backtrace(int enable)
-{
-  if (enable != 0 && enable != 1) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  if (enable && !g_crash_on) {
-    void* warm[2];
-    (void)backtrace(warm, 2); // loads the unwinder now, not inside the handler
-    struct sigaction sa;
-    memset(&sa, 0, sizeof(sa));
-    sa.sa_sigaction = crash_handler;
-    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
-    sigemptyset(&sa.sa_mask);
-    for (size_t k = 0; k < sizeof(CRASH_SIGNALS) / sizeof(int); ++k) {
-      if (sigaction(CRASH_SIGNALS[k], &sa, &g_crash_prev[k]) != 0) {
-        return TULIPS_STATUS_HARDWARE_ERROR;
-      }
-    }
-    g_crash_on = true;
-  } else if (!enable && g_crash_on) {
-    for (size_t k = 0; k < sizeof(CRASH_SIGNALS) / sizeof(int); ++k) {
-      (void)sigaction(CRASH_SIGNALS[k], &g_crash_prev[k], nullptr);
-    }
-    g_crash_on = false;
-  }
-  return TULIPS_STATUS_OK;
-}

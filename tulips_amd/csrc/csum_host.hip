@@ -31,7 +31,6 @@
 #include <vector>
 
 #include "../../include/tulips_csum.h"
-#include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
 #include "zc_mailbox.h"
@@ -1047,16 +1046,6 @@ tulips_csum_ctx_set_lowlat(tulips_csum_ctx* ctx, int resident)
 }
 
 extern "C" int
-tulips_csum_ctx_debug_set_seq(tulips_csum_ctx* ctx, uint64_t seq)
-{
-  if (!ctx) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  ctx->zc.seq = seq;
-  return TULIPS_STATUS_OK;
-}
-
-extern "C" int
 tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,
                                const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
                                uint8_t* flags, uint32_t* counters)
@@ -1085,68 +1074,6 @@ tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,
     rc = tulips_csum_validate_frames_host(ctx, base, offsets, lengths, n, flags, counters);
   }
   return rc;
-}
-
-extern "C" int
-tulips_csum_time_validate(tulips_csum_ctx* ctx, int path, const uint8_t* base,
-                          const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
-                          uint32_t reps, uint8_t* flags, double* out)
-{
-  return tulips_csum_time_validate_ring(ctx, path, base, 0, 1, offsets, lengths, n, reps,
-                                        flags, out);
-}
-
-extern "C" int
-tulips_csum_time_validate_ring(tulips_csum_ctx* ctx, int path, const uint8_t* ring,
-                               uint64_t burst_stride, uint32_t nbursts,
-                               const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
-                               uint32_t reps, uint8_t* flags, double* out)
-{
-  if (!ctx || !out || reps == 0 || path < 0 || path > 3 || nbursts == 0) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  std::vector<double> t(reps), g;
-  for (uint32_t r = 0; r < reps; ++r) {
-    const uint8_t* base = ring + uint64_t(r % nbursts) * burst_stride;
-    const auto t0 = std::chrono::steady_clock::now();
-    int use = path;
-    if (use == 3) { // the decorator's default choice, made inside the timed call
-      uint64_t bytes = 0;
-      for (uint32_t k = 0; k < n; ++k) {
-        bytes += lengths[k];
-      }
-      use = tulips_csum_burst_prefers_cpu(n, bytes) ? 2 : 1;
-    }
-    const int rc =
-      use == 2   ? tulips_csum_validate_frames_cpu(base, offsets, lengths, n, flags, nullptr)
-      : use == 1 ? tulips_csum_validate_frames_zc(ctx, base, offsets, lengths, n, flags, nullptr)
-                  : tulips_csum_validate_frames_host(ctx, base, offsets, lengths, n, flags,
-                                                     nullptr);
-    t[r] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
-             .count();
-    if (rc != TULIPS_STATUS_OK) {
-      return rc;
-    }
-    if (use == 1 && ctx->zc.mb) {
-      g.push_back(double(ctx->zc.mb->t_done - ctx->zc.mb->t_req) / 100.0); // 100 MHz
-    }
-  }
-  std::vector<double> s = t;
-  std::sort(s.begin(), s.end());
-  double mean = 0;
-  for (double x : t) {
-    mean += x / reps;
-  }
-  out[0] = s[reps / 2];
-  out[1] = s[std::min<size_t>(reps - 1, size_t(double(reps) * 0.99))];
-  out[2] = s[0];
-  out[3] = mean;
-  out[4] = 0;
-  if (!g.empty()) {
-    std::sort(g.begin(), g.end());
-    out[4] = g[g.size() / 2];
-  }
-  return TULIPS_STATUS_OK;
 }
 
 namespace {

@@ -54,7 +54,7 @@ bool span_geometry_ok(int unroll, int group);
 constexpr int SPAN_DEFAULT_UNROLL = 7;
 // In-order arena (KIND_SPAN): segments lie in order in [base, base + arena);
 // a.unroll = chunks per lane (4 KiB of arena per workgroup each), a.group the
-// form (include/tulips_csum_util.h).
+// form (include/tulips_csum.h).
 hipError_t launch_span(const uint8_t* base, uint64_t arena, const uint64_t* offs,
                        const uint16_t* lens, const LaunchArgs& a,
                        hipStream_t stream);
@@ -94,14 +94,5 @@ struct ZcMailbox;
 struct ZcArgs;
 hipError_t launch_zc_server(ZcMailbox* mb, const ZcArgs* oneshot, hipStream_t stream);
 
-hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed,
-                                uint64_t byte_off, hipStream_t stream);
-hipError_t launch_stream_slots(const uint8_t* p, uint64_t stride, uint32_t bytes, uint32_t n,
-                               int group, int unroll, uint32_t* sink, hipStream_t stream);
-hipError_t launch_stream_tiles(const uint8_t* p, uint64_t tile, uint32_t ntiles,
-                               uint32_t* sink, hipStream_t stream);
-hipError_t launch_stream_read(const uint8_t* p, uint64_t nbytes,
-                              uint32_t* sink, uint32_t max_blocks,
-                              hipStream_t stream);
 
 }

@@ -29,7 +29,6 @@
 #include <mutex>
 
 #include "../../include/tulips_csum.h"
-#include "../../include/tulips_csum_util.h"
 #include "csum_common.h"
 #include "csum_launch.h"
 #include "frame_common.h"

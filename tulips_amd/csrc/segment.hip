@@ -41,6 +41,7 @@
 #include "../../include/tulips_csum.h"
 #include "csum_common.h"
 #include "frame_common.h"
+#include "seg_device.h"
 #include "stream_state.h"
 
 namespace tulips_amd {
@@ -48,7 +49,6 @@ namespace {
 
 using namespace frame;
 
-typedef __attribute__((address_space(1))) u32x4* gchunk_wptr;
 
 constexpr uint32_t TCP_FIN = 0x01, TCP_PSH = 0x08, TCP_CWR = 0x80;
 constexpr uint32_t MAX_FRAMES = 1u << 24; // 65536 count blocks of 256
@@ -177,16 +177,6 @@ load_chunk(uintptr_t q)
   return *reinterpret_cast<gchunk_ptr>(q);
 }
 
-// Output chunks are written once and read next by the NIC, not by this GPU:
-// nontemporal stores stream them out instead of leaving ~68 MB per call dirty
-// in L2 for the kernel boundary to write back (per call 41.0 -> 31.5 us in
-// bench.py's serial chain, 30.0 -> 23.4 us on 4 branches; the kernel's own
-// duration is unchanged).
-__device__ __forceinline__ void
-store_chunk(uintptr_t a, u32x4 v)
-{
-  __builtin_nontemporal_store(v, reinterpret_cast<gchunk_wptr>(a));
-}
 
 // Bytes x .. x+15 of a source: two consecutive aligned chunks a, b and the
 // offset m = x & 15 (assemble funnel-shifts them with v_alignbyte). Bytes
@@ -231,16 +221,6 @@ merge_bytes(u32x4 a, u32x4 b, int k)
   return v;
 }
 
-__device__ __forceinline__ u32x4
-keep_bytes(u32x4 a, int k)
-{
-  u32x4 v;
-  v.x = a.x & byte_mask(0, k, 0);
-  v.y = a.y & byte_mask(0, k, 4);
-  v.z = a.z & byte_mask(0, k, 8);
-  v.w = a.w & byte_mask(0, k, 12);
-  return v;
-}
 
 // One input frame as a segment builder sees it: its prologue descriptor.
 struct SegFrame
@@ -282,39 +262,7 @@ next_chunk(const u32x4& cur, const u32x4& nxt, int lane, int sub0)
   return r;
 }
 
-// The dword after each lane's chunk: lane l + 1's first dword, the next batch
-// slot's for the subgroup's last lane (lane 0 hands it nxt).
-template<int G>
-__device__ __forceinline__ uint32_t
-next_dword(uint32_t cur, uint32_t nxt, int lane, int sub0)
-{
-  const uint32_t give = lane == 0 ? nxt : cur;
-  if constexpr (G == 16) {
-    // a 16-lane subgroup is one DPP row: row_ror:15 hands lane l the value of
-    // lane (l + 1) mod 16 in one VALU move
-    return uint32_t(__builtin_amdgcn_update_dpp(0, int(give), 0x12F, 0xF, 0xF, false));
-  } else {
-    return __shfl(give, sub0 + ((lane + 1) & (G - 1)), 64);
-  }
-}
 
-typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-typedef const __attribute__((address_space(1))) u32x4_a4* gdw4_ptr;
-
-// A payload chunk whose dwords start past the frame's last aligned chunk is
-// loaded from that chunk instead (reads never leave the 16-byte chunks the
-// frame touches), sel dwords early: move its dwords down. Dwords that would
-// come from beyond that chunk lie past the frame and are never used.
-__device__ __forceinline__ void
-realign(u32x4& d, uint32_t sel)
-{
-  if (sel != 0) {
-    const u32x4 e = d;
-    d.x = sel == 1 ? e.y : (sel == 2 ? e.z : e.w);
-    d.y = sel == 1 ? e.z : e.w;
-    d.z = e.w;
-  }
-}
 
 // Build, checksum and store segment k of frame F as output frame j, on one
 // G-lane subgroup (lane = index in the subgroup, sub0 = its first lane in the
@@ -758,66 +706,6 @@ segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
   }
 }
 
-// The segment kernels' data movement without their header work: slot k
-// copies source bytes [src + (k / per) * gstride + (k % per) * step, + bytes)
-// to out + k * ostride, one G-lane subgroup per slot, SU + 1 dword-aligned
-// 16-byte loads per lane per batch (clamped to the source's last 16-byte
-// chunk), funnel shift, nontemporal 16-byte stores: build_segment's loads and
-// stores with no header chunk, parse, patch or sums. The ceiling the
-// segmentation figures are held against (bench.py extras.segment_*).
-template<int G, int SU>
-__global__ __launch_bounds__(256) void
-copy_slots_kernel(uintptr_t src, uint64_t gstride, uint32_t per, uint32_t step, uint32_t bytes,
-                  uint32_t n, uint8_t* out, uint64_t ostride)
-{
-  const uint32_t t = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  const uint32_t k = t / G;
-  if (k >= n) {
-    return; // (whole subgroups: their shuffles stay inside the subgroup)
-  }
-  const int lane = int(t % G), sub0 = int(threadIdx.x & 63) & ~(G - 1);
-  const uintptr_t xs = src + uint64_t(k / per) * gstride + uint64_t(k % per) * step;
-  const uintptr_t hi = (xs + bytes - 1) & ~uintptr_t(15);
-  const uintptr_t p0 = xs & ~uintptr_t(3);
-  const uint32_t r = uint32_t(xs & 3);
-  const uintptr_t dst = reinterpret_cast<uintptr_t>(out) + uint64_t(k) * ostride;
-  const int nchunks = int((bytes + 15) >> 4);
-  auto src_chunk = [&](int c, uint32_t& sel) {
-    const uintptr_t p = p0 + 16 * uintptr_t(c);
-    const uintptr_t q = p > hi ? hi : p;
-    sel = uint32_t(p - q) >> 2;
-    return u32x4(*reinterpret_cast<gdw4_ptr>(q));
-  };
-  for (int b0 = 0; b0 < nchunks; b0 += G * SU) {
-    u32x4 X[SU + 1];
-    uint32_t XS[SU + 1];
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      X[u] = src_chunk(b0 + lane + G * u, XS[u]);
-    }
-    X[SU] = src_chunk(lane == 0 ? b0 + G * SU : b0 + lane + G * (SU - 1), XS[SU]);
-    realign(X[0], XS[0]);
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      realign(X[u + 1], XS[u + 1]);
-      const uint32_t d4 = next_dword<G>(X[u].x, X[u + 1].x, lane, sub0);
-      const int c = b0 + lane + G * u;
-      if (c >= nchunks) {
-        continue;
-      }
-      const u32x4 a = X[u];
-      u32x4 v;
-      v.x = __builtin_amdgcn_alignbyte(a.y, a.x, r);
-      v.y = __builtin_amdgcn_alignbyte(a.z, a.y, r);
-      v.z = __builtin_amdgcn_alignbyte(a.w, a.z, r);
-      v.w = __builtin_amdgcn_alignbyte(d4, a.w, r);
-      if (uint32_t(16 * c + 16) > bytes) {
-        v = keep_bytes(v, int(bytes) - 16 * c);
-      }
-      store_chunk(dst + 16 * uintptr_t(c), v);
-    }
-  }
-}
 
 // Workspace per (device, stream) (stream_state.h): the scan's block totals
 // (MAX_FRAMES / CB words), the run starts (one word per RUN output segments)
@@ -865,30 +753,24 @@ workspace(StreamState& s, bool capturing, uint32_t capacity, uint32_t n,
   const uint64_t need_desc = capacity ? uint64_t(n) : 0;
   StreamState::SegWs* w = nullptr;
   if (capturing) {
-    unsigned long long id = 0;
-    if (!capture_id(s.stream, &id)) {
+    StreamState::Capture* c = nullptr;
+    if (capture_record(s, &c) != hipSuccess) {
       return hipErrorStreamCaptureUnsupported;
     }
-    // only the capture in progress can add calls to its workspace
-    for (auto it = s.seg_capture.begin(); it != s.seg_capture.end();) {
-      it = it->first == id ? std::next(it) : s.seg_capture.erase(it);
-    }
-    auto it = s.seg_capture.find(id);
-    if (it == s.seg_capture.end() || it->second.nruns < need_runs ||
-        it->second.ndesc < need_desc) {
+    if (!c->seg.blocks || c->seg.nruns < need_runs || c->seg.ndesc < need_desc) {
       // a fresh one sized for this call (the graph keeps it; an earlier one
       // of this capture stays with the calls recorded on it)
       StreamState::SegWs fresh;
       std::vector<void*> made;
       const hipError_t e = ws_alloc(s.device, true, need_runs ? need_runs : 1,
                                     need_desc ? need_desc : 1, &fresh, &made);
-      s.seg_owned.insert(s.seg_owned.end(), made.begin(), made.end());
+      capture_keep(s, made);
       if (e != hipSuccess) {
         return e;
       }
-      it = s.seg_capture.insert_or_assign(id, fresh).first;
+      c->seg = fresh;
     }
-    w = &it->second;
+    w = &c->seg;
   } else {
     w = &s.seg;
     if (!w->blocks || need_runs > w->nruns || need_desc > w->ndesc) {
@@ -1089,27 +971,3 @@ tulips_csum_segment_plan_host(const uint8_t* base, const uint64_t* offsets,
   return TULIPS_STATUS_OK;
 }
 
-extern "C" int
-tulips_csum_stream_copy_slots(const uint8_t* src, uint64_t group_stride, uint32_t per_group,
-                              uint32_t step, uint32_t bytes, uint32_t nslots, uint8_t* out,
-                              uint64_t out_stride, void* stream)
-{
-  using namespace tulips_amd;
-  if (nslots == 0) {
-    return TULIPS_STATUS_OK;
-  }
-  if (!src || !out || per_group == 0 || bytes == 0 || bytes > 0xffffu ||
-      (reinterpret_cast<uintptr_t>(out) & 15) || (out_stride & 15) || out_stride < bytes) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  constexpr int G = 16, SU = 6;
-  const uint64_t blocks = (uint64_t(nslots) * G + 255) / 256;
-  if (blocks > 0xffffffffull) {
-    return TULIPS_STATUS_INVALID_ARGUMENT;
-  }
-  (void)hipGetLastError();
-  hipLaunchKernelGGL((copy_slots_kernel<G, SU>), dim3(uint32_t(blocks)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), reinterpret_cast<uintptr_t>(src),
-                     group_stride, per_group, step, bytes, nslots, out, out_stride);
-  return hipGetLastError() == hipSuccess ? TULIPS_STATUS_OK : TULIPS_STATUS_HARDWARE_ERROR;
-}

@@ -1,6 +1,6 @@
 // stream_state.h — the library's per-(device, stream) state: counter shards
-// for the counting calls (verify, counted frame validation) and the
-// segmentation workspace.
+// for the counting calls (verify, counted frame validation), the split-form
+// span words of the arena calls and the segmentation workspace.
 //
 // Rules (include/tulips_csum.h):
 //  * A call that uses the state holds the stream's `call` mutex from its
@@ -9,29 +9,37 @@
 //    their launches queued as whole sequences, never interleaved.
 //  * The device is the stream's own (hipStreamGetDevice), not the calling
 //    thread's current device; state is allocated on that device.
-//  * A counting call captured in a HIP graph gets shards of its own, owned by
-//    the graph from then on, so replays never share shards with direct calls
-//    on the capture stream: a spare from the set made with the stream's
-//    direct shards, or, when none is left (or no direct counting call came
-//    first), shards made in relaxed capture mode and zeroed on a private
-//    stream.
-//  * Segmentation calls captured in a graph run on a workspace made for that
-//    capture and owned by the graph (no warm-up needed, nothing a later
-//    direct call does can free it under the graph).
-//  * tulips_csum_release_stream frees everything a stream holds, including
-//    the shards and workspaces owned by graphs captured on it (destroy those
-//    graphs first).
+//  * Direct (uncaptured) calls share the stream's arrays, grown on demand;
+//    tulips_csum_release_stream frees them.
+//  * A call captured in a HIP graph runs on arrays made for that capture (in
+//    relaxed capture mode; zeroed by a kernel node of the graph where they
+//    must start at zero). The graph owns them through a HIP user object
+//    (hipUserObjectCreate + hipGraphRetainUserObject, moved to the graph):
+//    instantiated executables hold their own references, and when the last
+//    of the graph and its executables is destroyed the runtime calls the
+//    object's destructor. That only queues the arrays; the library's next
+//    uncaptured call on any stream (or tulips_csum_release_stream) frees
+//    them (reclaim_graph_arrays), so no HIP call runs inside the runtime's
+//    callback. Nothing a direct call does can free or reuse them while a
+//    graph may still replay.
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <map>
 #include <memory>
 #include <mutex>
 #include <vector>
 
 namespace tulips_amd {
+
+// The arrays one capture took on one stream; owned by the graph through a
+// user object whose destructor queues this for reclaim_graph_arrays.
+struct GraphArrays
+{
+  int device = 0;
+  std::vector<void*> ptrs;
+};
 
 struct StreamState
 {
@@ -41,11 +49,10 @@ struct StreamState
   // holds it around launches that take it themselves, e.g. the split span)
   std::recursive_mutex call;
 
-  // counter shards (csum_launch.h CNT_SHARDS x CNT_LINE words each)
-  uint32_t* shards = nullptr;          // direct (uncaptured) calls
-  std::vector<uint32_t*> spare;        // for captured calls, made with `shards`
-  std::vector<uint32_t*> graph_owned;  // handed to captured calls
-  std::vector<uint32_t*> retired;      // dropped after a failed launch
+  // counter shards (csum_launch.h CNT_SHARDS x CNT_LINE words) of the
+  // direct calls, and sets dropped after a failed launch (freed at release)
+  uint32_t* shards = nullptr;
+  std::vector<uint32_t*> retired;
 
   // segmentation workspace (segment.hip): the scan's block totals, the run
   // starts and the per-frame descriptors
@@ -57,57 +64,72 @@ struct StreamState
     void* desc = nullptr; // 16 B per input frame
     uint64_t ndesc = 0;
   };
-  // direct (uncaptured) calls: grown on demand, the old arrays freed once the
-  // stream is idle (no graph ever holds them)
+  // direct calls: grown on demand, the old arrays freed once the stream is
+  // idle (no graph ever holds them)
   SegWs seg;
-  // a capture's calls on this stream share one workspace made for that
-  // capture (relaxed capture mode), owned by its graph: later direct calls
-  // never free or regrow it, and a replay never shares arrays with direct
-  // calls on this stream or with another graph
-  std::map<unsigned long long, SegWs> seg_capture;
-  std::vector<void*> seg_owned;
 
   // SPAN split-form words (span_kernel.h csum_span_kernel): one 64-bit word
-  // per arena range, tagged with the launch's dispatch id and queue, so a word left by
-  // an earlier launch (two-part segments leave theirs as they are) is never
-  // added to. The calls one
-  // capture records on this stream run in order in the graph, so they share
-  // one array (a spare, or made in relaxed capture mode), owned by the graph
-  // from then on and salted apart from other arrays
-  uint32_t span_salt = 0;
+  // per arena range, tagged with the launch's dispatch id and queue, so a
+  // word left by an earlier launch is never added to. Direct calls share
+  // `span_slots`, re-zeroed every 2^20 calls.
   uint64_t* span_slots = nullptr;
   uint64_t span_nslots = 0;
-  uint64_t span_calls = 0; // direct arena calls (the words are re-zeroed every 2^20)
-  std::vector<uint64_t*> span_spare;
-  std::vector<uint64_t*> span_owned;
+  uint64_t span_calls = 0;
+  uint32_t span_salt = 0; // advanced per captured word array
+
+  // The capture in progress on this stream (the last one seen): its calls
+  // share one word array and one segmentation workspace (they run in order
+  // in the graph); every array it takes goes to `owner`, the graph's.
   struct Capture
   {
-    uint64_t* words;
-    uint64_t size;
-    uint32_t salt;
+    bool live = false;
+    unsigned long long id = 0;
+    GraphArrays* owner = nullptr; // null when the runtime refused the user object
+    uint64_t* words = nullptr;
+    uint64_t nwords = 0;
+    uint32_t salt = 0;
+    SegWs seg;
   };
-  std::map<unsigned long long, Capture> span_capture;
+  Capture cap;
+  // arrays of captures whose graph could not take ownership (a runtime
+  // without user objects): freed at tulips_csum_release_stream
+  std::vector<void*> orphans;
 };
 
-constexpr int SPARE_SHARDS = 16;
-
 // The state of `stream` (created on first use). The returned pointer stays
-// valid while held even if the stream is released meanwhile.
+// valid while held even if the stream is released meanwhile. When `stream`
+// is not capturing, first frees the arrays of graphs destroyed since the
+// last call (reclaim_graph_arrays).
 hipError_t stream_state(hipStream_t stream, std::shared_ptr<StreamState>* out);
+
+// Frees the arrays of every graph whose last reference the runtime dropped
+// (queued by the user objects' destructors). Must not run inside a capture
+// on the calling thread's stream; the thread's capture mode is relaxed
+// around the frees.
+void reclaim_graph_arrays();
 
 // Whether `stream` is capturing (a stream that cannot be queried counts as
 // not capturing; the launches will report the error).
 bool stream_capturing(hipStream_t stream);
 
-// Counter shards for one counting call on `s` (caller holds s.call):
-// the stream's direct shards, or, inside a capture, a zeroed set the graph
-// keeps (a spare, or made then). hipErrorStreamCaptureUnsupported when a
-// capture's set cannot be made.
+// The record of the capture in progress on s.stream (caller holds s.call),
+// made on the capture's first call on this stream: a fresh word array and
+// workspace slot, and a user object moved to the capture's graph.
+// hipErrorStreamCaptureUnsupported when the capture cannot be read.
+hipError_t capture_record(StreamState& s, StreamState::Capture** out);
+
+// Hands arrays made for the capture in progress to its graph (or to
+// s.orphans when the graph holds no user object of ours).
+void capture_keep(StreamState& s, const std::vector<void*>& ps);
+
+// Counter shards for one counting call on `s` (caller holds s.call): the
+// stream's direct shards, or, inside a capture, a zeroed set of the graph's.
+// hipErrorStreamCaptureUnsupported when a capture's set cannot be made.
 hipError_t call_shards(StreamState& s, bool capturing, uint32_t** out);
 
-// The split-form span words for one call on `s` (caller holds s.call): at
-// least `need` words (their count in *nslots) and the array's tag salt;
-// inside a capture an array the graph keeps.
+// The split-form span words for one call on `s` (caller holds s.call):
+// at least `need` words (their count in *nslots) and the array's tag salt;
+// inside a capture the capture's array (the graph's).
 // hipErrorStreamCaptureUnsupported when a capture's array cannot be had.
 hipError_t span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out,
                       uint64_t* nslots, uint32_t* salt);
@@ -122,8 +144,5 @@ hipError_t device_malloc(int device, void** p, size_t bytes);
 // hipMalloc on `device` from inside a capture: the thread's capture mode is
 // relaxed around the allocation (plain device_malloc when not capturing).
 hipError_t device_malloc_in_capture(int device, bool capturing, void** p, size_t bytes);
-
-// The id of the capture in progress on `stream` (false when none can be read).
-bool capture_id(hipStream_t stream, unsigned long long* id);
 
 } // namespace tulips_amd

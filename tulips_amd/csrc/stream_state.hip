@@ -1,8 +1,9 @@
-// stream_state.hip — per-(device, stream) state registry (stream_state.h)
-// and tulips_csum_release_stream.
+// stream_state.hip — per-(device, stream) state registry (stream_state.h),
+// graph ownership of captured arrays, and tulips_csum_release_stream.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -19,8 +20,23 @@ namespace {
 std::mutex g_mutex;
 std::map<std::pair<int, hipStream_t>, std::shared_ptr<StreamState>> g_states;
 
+// Arrays of destroyed graphs, queued by the user objects' destructors (which
+// may run on a runtime thread, during any HIP call or at process exit: the
+// queue is never destroyed, and the destructor makes no HIP call).
+std::mutex* const g_reclaim_mutex = new std::mutex;
+std::vector<GraphArrays*>* const g_reclaim = new std::vector<GraphArrays*>;
+std::atomic<uint32_t> g_reclaim_n{ 0 };
+
 constexpr size_t SHARD_BYTES = sizeof(uint32_t) * CNT_LINE * CNT_SHARDS;
 static_assert(SHARD_BYTES % 8 == 0, "shards are made as 64-bit words");
+
+void
+on_graph_destroyed(void* p)
+{
+  std::lock_guard<std::mutex> g(*g_reclaim_mutex);
+  g_reclaim->push_back(static_cast<GraphArrays*>(p));
+  g_reclaim_n.fetch_add(1, std::memory_order_release);
+}
 
 hipError_t
 stream_device(hipStream_t stream, int* dev)
@@ -46,6 +62,62 @@ free_on(int device, const std::vector<void*>& ps)
     }
   }
   (void)hipSetDevice(prev);
+}
+
+// Zeroes words [0, n) of p (a kernel: inside a capture it is a kernel node
+// of the graph, which a captured hipMemsetAsync on an array allocated in the
+// capture did not reliably become).
+__global__ __launch_bounds__(256) void
+zero_words_kernel(uint64_t* __restrict__ p, uint64_t n)
+{
+  for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += uint64_t(gridDim.x) * 256) {
+    p[i] = 0;
+  }
+}
+
+hipError_t
+launch_zero_words(uint64_t* p, uint64_t n, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  const uint64_t want = (n + 255) / 256;
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(zero_words_kernel, dim3(uint32_t(want < 1024 ? want : 1024)), dim3(256), 0,
+                     stream, p, n);
+  return hipGetLastError();
+}
+
+// An array of `words` zeroed words on `device`, zeroed in `stream`'s order:
+// outside a capture the caller synchronises `stream` before anything else
+// can read it; inside a capture (the allocation made in relaxed capture
+// mode) the zeroing is a kernel node of the graph, run before the captured
+// kernels at every replay. Inside a capture the array is handed to the
+// capture's graph (capture_keep) whether or not the zeroing could be
+// recorded, so nothing is freed while the capture is in progress.
+hipError_t
+zeroed_words(StreamState& s, uint64_t words, bool capturing, uint64_t** out)
+{
+  *out = nullptr;
+  void* p = nullptr;
+  hipError_t e = device_malloc_in_capture(s.device, capturing, &p, sizeof(uint64_t) * words);
+  if (e != hipSuccess) {
+    return e;
+  }
+  if (capturing) {
+    capture_keep(s, std::vector<void*>{ p });
+  }
+  e = launch_zero_words(static_cast<uint64_t*>(p), words, s.stream);
+  if (e != hipSuccess) {
+    if (!capturing) {
+      (void)hipStreamSynchronize(s.stream);
+      free_on(s.device, std::vector<void*>{ p });
+    }
+    return e;
+  }
+  *out = static_cast<uint64_t*>(p);
+  return hipSuccess;
 }
 
 } // namespace
@@ -83,15 +155,27 @@ device_malloc_in_capture(int device, bool capturing, void** p, size_t bytes)
   return e;
 }
 
-bool
-capture_id(hipStream_t stream, unsigned long long* id)
+void
+reclaim_graph_arrays()
 {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamGetCaptureInfo(stream, &cs, id) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
+  if (g_reclaim_n.load(std::memory_order_acquire) == 0) {
+    return;
   }
-  return cs == hipStreamCaptureStatusActive;
+  std::vector<GraphArrays*> todo;
+  {
+    std::lock_guard<std::mutex> g(*g_reclaim_mutex);
+    todo.swap(*g_reclaim);
+    g_reclaim_n.store(0, std::memory_order_relaxed);
+  }
+  // another thread may be capturing in global mode: this thread's frees are
+  // allowed by its relaxed mode (the graphs that used them are gone)
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  for (GraphArrays* a : todo) {
+    free_on(a->device, a->ptrs);
+    delete a;
+  }
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
 }
 
 hipError_t
@@ -101,6 +185,9 @@ stream_state(hipStream_t stream, std::shared_ptr<StreamState>* out)
   const hipError_t e = stream_device(stream, &dev);
   if (e != hipSuccess) {
     return e;
+  }
+  if (g_reclaim_n.load(std::memory_order_relaxed) != 0 && !stream_capturing(stream)) {
+    reclaim_graph_arrays();
   }
   std::lock_guard<std::mutex> g(g_mutex);
   std::shared_ptr<StreamState>& s = g_states[std::make_pair(dev, stream)];
@@ -124,126 +211,80 @@ stream_capturing(hipStream_t stream)
   return cs != hipStreamCaptureStatusNone;
 }
 
-hipError_t zeroed_words(int device, uint64_t words, bool capturing, int count,
-                        hipStream_t stream, std::vector<uint64_t*>* out);
+hipError_t
+capture_record(StreamState& s, StreamState::Capture** out)
+{
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t graph = nullptr;
+  if (hipStreamGetCaptureInfo_v2(s.stream, &cs, &id, &graph, nullptr, nullptr) != hipSuccess ||
+      cs != hipStreamCaptureStatusActive || !graph) {
+    (void)hipGetLastError();
+    return hipErrorStreamCaptureUnsupported;
+  }
+  if (!s.cap.live || s.cap.id != id) {
+    // the first call of this capture on this stream: the arrays of an
+    // earlier capture stay with that capture's graph
+    s.cap = StreamState::Capture();
+    s.cap.live = true;
+    s.cap.id = id;
+    GraphArrays* owner = new GraphArrays;
+    owner->device = s.device;
+    hipUserObject_t obj = nullptr;
+    if (hipUserObjectCreate(&obj, owner, on_graph_destroyed, 1,
+                            hipUserObjectNoDestructorSync) != hipSuccess) {
+      (void)hipGetLastError();
+      delete owner;
+      owner = nullptr;
+    } else if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+      (void)hipGetLastError();
+      // our reference is still ours: dropping it runs the destructor, which
+      // queues the (empty) record for the next reclaim
+      (void)hipUserObjectRelease(obj, 1);
+      owner = nullptr;
+    }
+    s.cap.owner = owner;
+    s.span_salt = s.span_salt * 0x9E3779B1u + 0x7F4A7C15u;
+    s.cap.salt = s.span_salt;
+  }
+  *out = &s.cap;
+  return hipSuccess;
+}
+
+void
+capture_keep(StreamState& s, const std::vector<void*>& ps)
+{
+  std::vector<void*>& to = s.cap.owner ? s.cap.owner->ptrs : s.orphans;
+  to.insert(to.end(), ps.begin(), ps.end());
+}
 
 hipError_t
 call_shards(StreamState& s, bool capturing, uint32_t** out)
 {
-  if (capturing && (!s.shards || s.spare.empty())) {
-    // a capture on a stream with no spare left (or none made yet: no direct
-    // counting call before it): shards of its own, made in relaxed capture
-    // mode and zeroed by a kernel node of the graph, owned by the graph
-    std::vector<uint64_t*> made;
-    const hipError_t e = zeroed_words(s.device, SHARD_BYTES / 8, true, 1, s.stream, &made);
-    if (e != hipSuccess) {
+  if (capturing) {
+    // shards of the capture's own, zeroed by a kernel node of the graph
+    StreamState::Capture* c = nullptr;
+    uint64_t* words = nullptr;
+    if (capture_record(s, &c) != hipSuccess ||
+        zeroed_words(s, SHARD_BYTES / 8, true, &words) != hipSuccess) {
       (void)hipGetLastError();
       return hipErrorStreamCaptureUnsupported;
     }
-    *out = reinterpret_cast<uint32_t*>(made[0]);
-    s.graph_owned.push_back(*out);
+    *out = reinterpret_cast<uint32_t*>(words);
     return hipSuccess;
   }
   if (!s.shards) {
-    // direct shards plus the spares captured calls will take, one
-    // allocation each, zeroed in stream order before any kernel uses them
-    std::vector<uint32_t*> made;
-    hipError_t e = hipSuccess;
-    for (int k = 0; k <= SPARE_SHARDS && e == hipSuccess; ++k) {
-      void* p = nullptr;
-      if ((e = device_malloc(s.device, &p, SHARD_BYTES)) == hipSuccess) {
-        made.push_back(static_cast<uint32_t*>(p));
-        e = hipMemsetAsync(p, 0, SHARD_BYTES, s.stream);
-      }
+    void* p = nullptr;
+    hipError_t e = device_malloc(s.device, &p, SHARD_BYTES);
+    if (e == hipSuccess && (e = hipMemsetAsync(p, 0, SHARD_BYTES, s.stream)) != hipSuccess) {
+      free_on(s.device, std::vector<void*>{ p });
     }
     if (e != hipSuccess) {
-      free_on(s.device, std::vector<void*>(made.begin(), made.end()));
       return e;
     }
-    s.shards = made[0];
-    s.spare.assign(made.begin() + 1, made.end());
+    s.shards = static_cast<uint32_t*>(p);
   }
-  if (!capturing) {
-    *out = s.shards;
-    return hipSuccess;
-  }
-  *out = s.spare.back();
-  s.spare.pop_back();
-  s.graph_owned.push_back(*out);
-  return hipSuccess;
-}
-
-// Zeroes words [0, n) of p (a kernel: inside a capture it is a kernel node
-// of the graph, which a captured hipMemsetAsync on an array allocated in the
-// capture did not reliably become).
-__global__ __launch_bounds__(256) void
-zero_words_kernel(uint64_t* __restrict__ p, uint64_t n)
-{
-  for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n;
-       i += uint64_t(gridDim.x) * 256) {
-    p[i] = 0;
-  }
-}
-
-hipError_t
-launch_zero_words(uint64_t* p, uint64_t n, hipStream_t stream)
-{
-  if (n == 0) {
-    return hipSuccess;
-  }
-  const uint64_t want = (n + 255) / 256;
-  (void)hipGetLastError();
-  hipLaunchKernelGGL(zero_words_kernel, dim3(uint32_t(want < 1024 ? want : 1024)), dim3(256), 0,
-                     stream, p, n);
-  return hipGetLastError();
-}
-
-// `count` arrays of zeroed words on `device`, zeroed in `stream`'s order:
-// outside a capture the caller synchronises `stream` before anything else
-// can read them; inside a capture (the thread's capture mode relaxed for the
-// allocations, so hipMalloc is allowed) the zeroing is a kernel node of the
-// graph on the capturing stream, run before the captured kernels at every
-// replay. No stream is created or destroyed while a capture is in progress:
-// doing that (a private zeroing stream, as before) corrupted the HIP
-// runtime's graph state, and a later hipGraphLaunch crashed on it (the r04
-// SIGSEGV; tests/test_fuzz.py::test_fuzz_captured_graphs).
-hipError_t
-zeroed_words(int device, uint64_t words, bool capturing, int count, hipStream_t stream,
-             std::vector<uint64_t*>* out)
-{
-  std::vector<void*> made;
-  hipError_t e = hipSuccess;
-  {
-    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-    if (capturing) {
-      (void)hipThreadExchangeStreamCaptureMode(&mode);
-    }
-    for (int k = 0; k < count && e == hipSuccess; ++k) {
-      void* p = nullptr;
-      if ((e = device_malloc(device, &p, sizeof(uint64_t) * words)) == hipSuccess) {
-        made.push_back(p);
-      }
-    }
-    if (capturing) {
-      (void)hipThreadExchangeStreamCaptureMode(&mode);
-    }
-  }
-  for (void* p : made) {
-    if (e == hipSuccess) {
-      e = launch_zero_words(static_cast<uint64_t*>(p), words, stream);
-    }
-  }
-  if (e != hipSuccess) {
-    if (!capturing) {
-      (void)hipStreamSynchronize(stream);
-    }
-    free_on(device, made);
-    return e;
-  }
-  out->clear();
-  for (void* p : made) {
-    out->push_back(static_cast<uint64_t*>(p));
-  }
+  *out = s.shards;
   return hipSuccess;
 }
 
@@ -253,23 +294,18 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64
 {
   if (!capturing) {
     if (need > s.span_nslots) {
-      // direct words plus spares for captures, all zeroed before use
       const uint64_t want = need < 4096 ? 4096 : need;
-      std::vector<uint64_t*> made;
-      hipError_t e = zeroed_words(s.device, want, false, 1 + SPARE_SHARDS, s.stream, &made);
-      if (e == hipSuccess) {
-        e = hipStreamSynchronize(s.stream); // the old arrays are idle
+      uint64_t* made = nullptr;
+      hipError_t e = zeroed_words(s, want, false, &made);
+      if (e == hipSuccess && (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
+        free_on(s.device, std::vector<void*>{ made });
       }
       if (e != hipSuccess) {
-        free_on(s.device, std::vector<void*>(made.begin(), made.end()));
         return e;
       }
-      std::vector<void*> old(s.span_spare.begin(), s.span_spare.end());
-      old.push_back(s.span_slots);
-      free_on(s.device, old);
-      s.span_slots = made[0];
+      free_on(s.device, std::vector<void*>{ s.span_slots }); // idle: the stream synchronised
+      s.span_slots = made;
       s.span_nslots = want;
-      s.span_spare.assign(made.begin() + 1, made.end());
     }
     // words keep the tags of earlier launches (span_kernel.h): zeroed every
     // 2^20 direct calls, so no word outlives that many calls of this stream
@@ -285,46 +321,29 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64
     *salt = 0;
     return hipSuccess;
   }
-  unsigned long long id = 0;
-  if (!capture_id(s.stream, &id)) {
+  StreamState::Capture* c = nullptr;
+  if (capture_record(s, &c) != hipSuccess) {
     return hipErrorStreamCaptureUnsupported;
   }
-  // only the capture in progress on this stream can add calls to its array
-  for (auto it = s.span_capture.begin(); it != s.span_capture.end();) {
-    it = it->first == id ? std::next(it) : s.span_capture.erase(it);
-  }
-  auto it = s.span_capture.find(id);
-  if (it != s.span_capture.end() && it->second.size >= need) {
-    *out = it->second.words;
-    *nslots = it->second.size;
-    *salt = it->second.salt;
-    return hipSuccess;
-  }
-  uint64_t* p = nullptr;
-  uint64_t size = 0;
-  if (!s.span_spare.empty() && s.span_nslots >= need) {
-    p = s.span_spare.back();
-    s.span_spare.pop_back();
-    size = s.span_nslots;
-  } else {
-    size = need < 4096 ? 4096 : need;
-    std::vector<uint64_t*> made;
-    if (zeroed_words(s.device, size, true, 1, s.stream, &made) != hipSuccess) {
+  if (c->nwords < need) {
+    // a graph may be replayed on other streams (other hardware queues, whose
+    // dispatch ids overlap this one's): the kernel's tag adds a hash of the
+    // queue (span_kernel.h launch_tag), and a salt per captured array sets
+    // its tags apart from every other array's as well. A larger array made
+    // later in the same capture replaces this one for the calls after it
+    // (the graph keeps both).
+    const uint64_t size = need < 4096 ? 4096 : need;
+    uint64_t* words = nullptr;
+    if (zeroed_words(s, size, true, &words) != hipSuccess) {
       (void)hipGetLastError();
       return hipErrorStreamCaptureUnsupported;
     }
-    p = made[0];
+    c->words = words;
+    c->nwords = size;
   }
-  s.span_owned.push_back(p);
-  // a graph may be replayed on other streams (other hardware queues, whose
-  // dispatch ids overlap this one's): the kernel's tag adds a hash of the
-  // queue (span_kernel.h launch_tag), and a salt per captured array sets
-  // its tags apart from every other array's as well
-  s.span_salt = s.span_salt * 0x9E3779B1u + 0x7F4A7C15u;
-  s.span_capture[id] = StreamState::Capture{ p, size, s.span_salt };
-  *out = p;
-  *nslots = size;
-  *salt = s.span_salt;
+  *out = c->words;
+  *nslots = c->nwords;
+  *salt = c->salt;
   return hipSuccess;
 }
 
@@ -333,7 +352,7 @@ drop_shards(StreamState& s, uint32_t* shards)
 {
   if (shards == s.shards) {
     s.retired.push_back(s.shards);
-    s.shards = nullptr; // the next call makes fresh ones (and fresh spares)
+    s.shards = nullptr; // the next call makes fresh ones
   }
 }
 
@@ -365,31 +384,27 @@ tulips_csum_release_stream(void* stream)
       (void)hipGetLastError();
     }
     (void)hipSetDevice(prev);
+    // the stream's direct arrays; those of its captures belong to their
+    // graphs (freed when the graphs are gone), except orphans
     std::vector<void*> ps;
     ps.push_back(s->shards);
-    for (auto* p : s->spare) ps.push_back(p);
-    for (auto* p : s->graph_owned) ps.push_back(p);
     for (auto* p : s->retired) ps.push_back(p);
     ps.push_back(s->seg.blocks);
     ps.push_back(s->seg.runs);
     ps.push_back(s->seg.desc);
-    for (auto* p : s->seg_owned) ps.push_back(p);
     ps.push_back(s->span_slots);
-    for (auto* p : s->span_spare) ps.push_back(p);
-    for (auto* p : s->span_owned) ps.push_back(p);
+    for (auto* p : s->orphans) ps.push_back(p);
     free_on(s->device, ps);
     s->shards = nullptr;
-    s->spare.clear();
-    s->graph_owned.clear();
     s->retired.clear();
     s->seg = StreamState::SegWs();
-    s->seg_owned.clear();
-    s->seg_capture.clear();
     s->span_slots = nullptr;
     s->span_nslots = 0;
-    s->span_spare.clear();
-    s->span_owned.clear();
-    s->span_capture.clear();
+    s->orphans.clear();
+    s->cap = StreamState::Capture();
+  }
+  if (g_reclaim_n.load(std::memory_order_relaxed) != 0 && !stream_capturing(st)) {
+    reclaim_graph_arrays();
   }
   return TULIPS_STATUS_OK;
 }

@@ -63,7 +63,7 @@ KIND_SPAN = 5
 
 
 class Tuning(C.Structure):
-    """tulips_csum_tuning (include/tulips_csum_util.h).
+    """tulips_csum_tuning (include/tulips_csum.h).
 
     kind SUBGROUP: `group` lanes (16/32/64) per segment, `unroll` chunks per
     lane in flight; PACKED (variable only): one wave per `group` segments
@@ -123,16 +123,6 @@ _SIGNATURES = {
     "tulips_csum_batch_tuned": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                           C.c_uint32, C.c_uint32,
                                           C.POINTER(Tuning), _vp]),
-    "tulips_csum_fill_splitmix": (C.c_int, [_vp, C.c_uint64, C.c_uint64,
-                                            C.c_uint64, _vp]),
-    "tulips_csum_stream_read": (C.c_int, [_vp, C.c_uint64, _vp, C.c_uint32, _vp]),
-    "tulips_csum_stream_read_tiles": (C.c_int, [_vp, C.c_uint64, C.c_uint32, _vp, _vp]),
-    "tulips_csum_stream_read_slots": (C.c_int, [_vp, C.c_uint64, C.c_uint32, C.c_uint32, _vp,
-                                                _vp]),
-    "tulips_csum_stream_read_slots_geom": (C.c_int, [_vp, C.c_uint64, C.c_uint32, C.c_uint32,
-                                                     C.c_int, C.c_int, _vp, _vp]),
-    "tulips_csum_stream_copy_slots": (C.c_int, [_vp, C.c_uint64, C.c_uint32, C.c_uint32,
-                                                C.c_uint32, C.c_uint32, _vp, C.c_uint64, _vp]),
     "tulips_rss_toeplitz_host": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16,
                                            _u8p, C.c_size_t, C.c_uint32,
                                            C.POINTER(C.c_uint32)]),
@@ -174,21 +164,14 @@ _SIGNATURES = {
     "tulips_csum_generate_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp]),
     "tulips_csum_validate_frames_zc": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp, _vp]),
     "tulips_csum_ctx_set_lowlat": (C.c_int, [_vp, C.c_int]),
-    "tulips_csum_time_validate": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_uint32,
-                                            C.c_uint32, _vp, _vp]),
     "tulips_csum_segment_frames_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32,
                                                   _vp, C.c_uint64, C.c_uint32, _vp, _vp]),
     "tulips_csum_validate_frames_cpu": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp]),
     "tulips_csum_burst_prefers_cpu": (C.c_int, [C.c_uint32, C.c_uint64]),
-    "tulips_csum_gpu_sleep": (C.c_int, [C.c_uint32, _vp]),
-    "tulips_csum_debug_crash_backtrace": (C.c_int, [C.c_int]),
-    "tulips_csum_time_validate_ring": (C.c_int, [_vp, C.c_int, _vp, C.c_uint64, C.c_uint32,
-                                                 _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp]),
     "tulips_csum_mctx_validate_frames_rss_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32,
                                                               _vp, C.c_size_t, C.c_uint32,
                                                               _vp, C.c_uint32, _vp, _vp, _vp,
                                                               _vp]),
-    "tulips_csum_ctx_debug_set_seq": (C.c_int, [_vp, C.c_uint64]),
     "tulips_csum_mctx_set_peer_mode": (C.c_int, [_vp, C.c_int]),
 }
 
@@ -423,23 +406,6 @@ def default_tuning(fixed_length: int = 0, variable: bool = False) -> Tuning:
     return t
 
 
-def fill_splitmix(dst, nbytes: int | None = None, seed: int = 0x54554C495053,
-                  byte_off: int = 0, stream=None) -> None:
-    """Device fill with the SURVEY.md §8c SplitMix64 byte stream."""
-    nbytes = int(dst.numel()) if nbytes is None else nbytes
-    _check(lib.tulips_csum_fill_splitmix(_addr(dst), nbytes, seed, byte_off,
-                                         _stream(stream)),
-           "tulips_csum_fill_splitmix")
-
-
-def stream_read(buf, sink, nbytes: int | None = None, max_blocks: int = 0,
-                stream=None) -> None:
-    nbytes = int(buf.numel()) if nbytes is None else nbytes
-    _check(lib.tulips_csum_stream_read(_addr(buf), nbytes, _addr(sink),
-                                       max_blocks, _stream(stream)),
-           "tulips_csum_stream_read")
-
-
 @dataclass
 class _Arr:
     ptr: int | None
@@ -519,11 +485,6 @@ class HostContext:
         _check(rc, "tulips_csum_validate_frames_zc" if low_latency else
                "tulips_csum_validate_frames_host")
         return (flags, cnt) if with_counters else flags
-
-    def debug_set_seq(self, seq: int):
-        """Test hook: the last zero-copy request's sequence number
-        (tulips_csum_ctx_debug_set_seq), to reach tag wrap-around."""
-        _check(lib.tulips_csum_ctx_debug_set_seq(self._h, seq), "tulips_csum_ctx_debug_set_seq")
 
     def set_lowlat(self, resident: bool):
         """Low-latency path form: one launch per burst (False) or a resident
