@@ -70,9 +70,9 @@ $(NATIVE): tests/native/runtime_check.cpp include/tulips_csum.h $(LIB)
 
 # Measured variants of rounds 1-2 (hybrid, lane-parallel cursors,
 # workgroup-balanced, halo / boundary-slot / staged span forms, per-wave
-# stamps): tools/variants/, built apart and never loaded by the product.
+# stamps): tools/sessions/variants/, built apart and never loaded by the product.
 variants:
-	$(MAKE) -C tools/variants
+	$(MAKE) -C tools/sessions/variants
 
 # Device assembly + resource usage of the kernels (for inspection).
 asm:

@@ -576,3 +576,176 @@ def test_mctx_rss_device_arguments_without_gpu():
     key = (C.c_uint8 * 40)()
     tab = (C.c_uint16 * 4)()
     assert f(None, 1, 1, 1, 1, key, 40, 0, tab, 4, 1, None, None, None) == 1
+
+
+# -- real peers: every cross-device entry across distinct GPUs -----------------
+#  The tests above run the peer paths on logical device
+# lists of GPU 0. These run them across every visible GPU, xGMI peer DMA where
+# hipDeviceCanAccessPeer allows it and page-locked staging when forced, with
+# the source on the first and on the last device; they skip on a one-GPU box.
+# Reference analogue: NIC multi-queue spreading,
+# /root/reference/src/transport/ena/RedirectionTable.cpp:74-98.
+def _real_devices():
+    import torch
+    nd = torch.cuda.device_count()
+    if nd < 2:
+        pytest.skip("needs two or more GPUs (real peers)")
+    return list(range(nd))
+
+
+def _digest(oracle, t):
+    import torch
+    torch.cuda.synchronize()
+    return f"{oracle.fnv1a_u16(t.cpu().numpy().view(np.uint16)):016x}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["first", "last"])
+def test_real_peers_arena_device_zipf(oracle, source):
+    """tulips_csum_mctx_batch_arena_device across distinct GPUs: the device-side
+    cut plan, each peer's pieces pulled with offs_bias, results sent home:
+    ZIPF and ZIPF-tcp digests in peer and staged mode."""
+    import torch
+    from tulips_amd import csum
+    import benchlib
+    from oracle import ip4
+    devs = _real_devices()
+    src_dev = devs[0] if source == "first" else devs[-1]
+    g = golden()
+    lens = oracle.zipf_lengths(65536)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.astype(np.int64).sum())
+    with torch.cuda.device(src_dev):
+        dev = f"cuda:{src_dev}"
+        arena = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+        benchlib.fill_splitmix(arena, total)
+        do = torch.from_numpy(offs.view(np.int64).copy()).to(dev)
+        dl = torch.from_numpy(lens.copy()).to(dev)
+        src = torch.from_numpy(np.full(65536, ip4(10, 1, 0, 1), np.uint32)).to(dev)
+        dst = torch.from_numpy(np.full(65536, ip4(10, 1, 0, 2), np.uint32)).to(dev)
+        st = torch.cuda.current_stream(src_dev)
+        with csum.MultiContext(devs) as m:
+            for staged in (False, True):
+                m.set_peer_mode(staged)
+                out = m.batch_arena_device(arena, do, dl, arena_bytes=total, stream=st)
+                assert _digest(oracle, out) == g["ZIPF"]["fnv1a64"], staged
+                b = m.bounds()
+                assert b[0] == 0 and b[-1] == 65536 and len(b) == len(devs) + 1
+                out = m.batch_arena_device(arena, do, dl, arena_bytes=total, src=src, dst=dst,
+                                           mode=2, stream=st)
+                assert _digest(oracle, out) == g["ZIPF-tcp"]["fnv1a64"], staged
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("source", ["first", "last"])
+def test_real_peers_fixed_device(oracle, source):
+    """tulips_csum_mctx_batch_fixed_device across distinct GPUs with the
+    source on the first or the last device: F1500 and F1500-tcp digests in
+    peer and staged mode."""
+    import torch
+    from tulips_amd import csum
+    import benchlib
+    from oracle import ip4
+    devs = _real_devices()
+    src_dev = devs[0] if source == "first" else devs[-1]
+    g = golden()
+    n = 65536
+    with torch.cuda.device(src_dev):
+        dev = f"cuda:{src_dev}"
+        arena = torch.empty(n * 1500 + 64, dtype=torch.uint8, device=dev)
+        benchlib.fill_splitmix(arena, n * 1500)
+        src = torch.from_numpy(np.full(n, ip4(10, 1, 0, 1), np.uint32)).to(dev)
+        dst = torch.from_numpy(np.full(n, ip4(10, 1, 0, 2), np.uint32)).to(dev)
+        st = torch.cuda.current_stream(src_dev)
+        with csum.MultiContext(devs) as m:
+            for staged in (False, True):
+                m.set_peer_mode(staged)
+                out = m.batch_fixed_device(arena, 1500, 1500, n, stream=st)
+                assert _digest(oracle, out) == g["F1500"]["fnv1a64"], staged
+                out = m.batch_fixed_device(arena, 1500, 1500, n, src=src, dst=dst, mode=2,
+                                           stream=st)
+                assert _digest(oracle, out) == g["F1500-tcp"]["fnv1a64"], staged
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_i,init", [(0, 0), (9, 0xFFFFFFFF)])
+def test_real_peers_rss_device(oracle, key_i, init):
+    """tulips_csum_mctx_validate_frames_rss_device across distinct GPUs: the
+    source's hash and stable scatter, packed runs pulled by real peers, flags
+    scattered home. device_of equals table[reference hash % len]
+    (tests/golden/rss.npz) and the host form's; flags and counters equal the
+    oracle's; the reference-flagged frames.npz (mutated) validates exactly;
+    peer and staged mode agree."""
+    import torch
+    from test_frames import counters_of, frames_fixture, mutate
+    from test_rss import rss_fixture
+    from tulips_amd import csum
+    devs = _real_devices()
+    nd = len(devs)
+    fx = rss_fixture()
+    key = fx[f"key_{key_i}"].tobytes()
+    exp_hash = fx[f"expect_{key_i}_{'init0' if init == 0 else 'initff'}"]
+    rng = np.random.default_rng(4000 + key_i)
+    arena, offs, lens, flow = _rss_frames(oracle, rng, fx)
+    table = (np.arange(128) * 5 % nd).astype(np.uint16)
+    table[0] = nd - 1
+    exp_flags = oracle.validate_frames(arena, offs, lens)
+    tcp = flow >= 0
+    want_dev = table[exp_hash[flow[tcp]].astype(np.int64) % len(table)]
+    a, o, ln = _dev(arena), _dev(offs.view(np.int64)), _dev(lens.view(np.int16))
+    ffx = frames_fixture()
+    fa = mutate(ffx, np.random.default_rng(77), 1200)
+    fexp = oracle.validate_frames(fa, ffx["offsets"], ffx["lengths"])
+    with csum.MultiContext(devs, chunk_bytes=1 << 20) as m:
+        hflags, hdev = m.validate_frames_rss(arena, offs, lens, key, table, init=init)
+        np.testing.assert_array_equal(hflags, exp_flags)
+        np.testing.assert_array_equal(hdev[tcp], want_dev)
+        got = {}
+        for staged in (False, True):
+            m.set_peer_mode(staged)
+            cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda:0")
+            fl, dv = m.validate_frames_rss_device(a, o, ln, key, table, init=init, counters=cnt)
+            torch.cuda.synchronize()
+            dv = dv.cpu().numpy().view(np.uint16)
+            np.testing.assert_array_equal(fl.cpu().numpy(), exp_flags, err_msg=str(staged))
+            np.testing.assert_array_equal(dv, hdev)
+            np.testing.assert_array_equal(dv[tcp], want_dev)
+            np.testing.assert_array_equal(cnt.cpu().numpy().view(np.uint32),
+                                          counters_of(exp_flags))
+            b = m.bounds()
+            assert list(np.diff(b.astype(np.int64))) == [int((dv == k).sum()) for k in range(nd)]
+            got[staged] = dv
+            fl, _ = m.validate_frames_rss_device(_dev(fa), _dev(ffx["offsets"].view(np.int64)),
+                                                 _dev(ffx["lengths"].view(np.int16)), key, table,
+                                                 init=init)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(fl.cpu().numpy(), fexp, err_msg=str(staged))
+        np.testing.assert_array_equal(got[False], got[True])
+
+
+@pytest.mark.gpu
+def test_real_peers_host_entries(oracle):
+    """tulips_csum_mctx_batch_host and tulips_csum_mctx_validate_frames_host
+    over every visible GPU (each device its own pinned pipeline): ZIPF digest,
+    byte-balanced bounds, frames.npz flags and counters; with the context in
+    peer and in staged mode (the host entries must not depend on it)."""
+    from test_frames import counters_of, frames_fixture, mutate
+    from tulips_amd import csum
+    devs = _real_devices()
+    g = golden()["ZIPF"]
+    lens = oracle.zipf_lengths(65536)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.astype(np.int64).sum())
+    arena = oracle.splitmix_bytes(total + 64)
+    fx = frames_fixture()
+    fa = mutate(fx, np.random.default_rng(5), 900)
+    fexp = oracle.validate_frames(fa, fx["offsets"], fx["lengths"])
+    with csum.MultiContext(devs, chunk_bytes=1 << 22) as m:
+        for staged in (False, True):
+            m.set_peer_mode(staged)
+            out = m.batch(arena, offs, lens)
+            assert f"{oracle.fnv1a_u16(out):016x}" == g["fnv1a64"], staged
+            check_plan(lens, len(devs), m.bounds())
+            fl, cnt = m.validate_frames(fa, fx["offsets"], fx["lengths"], with_counters=True)
+            np.testing.assert_array_equal(fl, fexp)
+            np.testing.assert_array_equal(cnt, counters_of(fexp))

@@ -1,6 +1,6 @@
 // csum_device.h — device-side building blocks shared by the checksum kernels
 // (csum_kernels.hip) and the archived measured variants
-// (tools/variants/csum_variants.hip): 16-byte chunk loads at absolute
+// (tools/sessions/variants/csum_variants.hip): 16-byte chunk loads at absolute
 // alignment, exact boundary masking, per-chunk 16-bit-half sums (v_dot2),
 // DPP wave scans, per-segment side inputs and result emission, and the
 // in-order-arena (SPAN) launch arguments. Semantics: csum_common.h

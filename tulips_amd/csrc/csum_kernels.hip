@@ -18,7 +18,7 @@
 //     parts that meet in a per-range word.
 // The measured losers of rounds 1-2 (hybrid, lane-parallel cursors,
 // workgroup-balanced, halo / boundary-slot / staged span forms, metadata
-// prefetch) live in tools/variants/, outside the product library.
+// prefetch) live in tools/sessions/variants/, outside the product library.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -48,7 +48,7 @@ hipError_t launch_var(const uint8_t* base, const uint64_t* offs,
 // before any HIP call).
 bool span_geometry_ok(int unroll, int group);
 // Chunks per lane of the default arena geometry: 28 KiB per workgroup range
-// (tools/probes/span_stamps.py, profiles/probe_span_geometry_r03.txt: ZIPF
+// (tools/sessions/probes/span_stamps.py, profiles/probe_span_geometry_r03.txt: ZIPF
 // 11.3 us serial and 7.8 us per launch on 4 branches, against 11.5 / 8.0 at
 // 6 and 11.6 / 8.0 at 8).
 constexpr int SPAN_DEFAULT_UNROLL = 7;

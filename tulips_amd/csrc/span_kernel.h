@@ -1,6 +1,6 @@
 // span_kernel.h — the in-order-arena (SPAN) checksum kernel, split form with
 // the chunk prefixes in LDS. The kernel is a template over a
-// probe so that tools/probes/span_stamps.hip can time the product code path
+// probe so that tools/sessions/probes/span_stamps.hip can time the product code path
 // itself; the product launches csum_span_kernel<U> (NoProbe, which compiles
 // to nothing) from csum_kernels.hip. Semantics: src/stack/Utils.cpp:14-42
 // (closed form in csum_common.h).
@@ -83,7 +83,7 @@ launch_tag(uint32_t salt)
   return ((llvm_amdgcn_dispatch_id() + h) ^ salt) & WORD_TAG_MASK;
 }
 
-// The product's probe: no marks. tools/probes/span_stamps.hip instantiates
+// The product's probe: no marks. tools/sessions/probes/span_stamps.hip instantiates
 // the same kernel with a probe that records per-wave realtime stamps at
 // marks 0-5 (and 7 on the rare path), and with other XC / NWIN values.
 struct NoProbe
@@ -98,7 +98,7 @@ struct NoProbe
 // speculative offsets window; MH: range chunks per lane issued before the
 // window is counted (the rest after the boundary chunks, which then arrive
 // before the range's last rows). The product uses NoProbe, 8, 1024 and U / 3
-// (tools/probes/span_stamps.py, profiles/probe_span_geometry_r03.txt).
+// (tools/sessions/probes/span_stamps.py, profiles/probe_span_geometry_r03.txt).
 // XCHG: a segment in two parts (always, when its length is below the range
 // size) meets its other part by one exchange per part, and the word is not
 // re-zeroed: the next launch's tag differs (profiles/probe_span_early_r03.txt:
