@@ -28,6 +28,10 @@
 //       destroy the executable: every replay's outputs equal the direct
 //       calls', and device memory (hipMemGetInfo, after 5 warm-up cycles)
 //       ends within 1 MiB of where it started (also reported half-way).
+//   runtime_check graph-churn SECONDS SEED
+//       the multi-branch capture/replay/destroy churn that faults inside
+//       the runtime torch bundles, on this runtime, with
+//       library calls as the graphs' kernels and every replay checked.
 // Exit status 0 = all checks passed; every result is printed as JSON.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -581,13 +585,164 @@ cmd_graph_cycles(uint32_t cycles)
   return ok ? 0 : 1;
 }
 
+// ---- multi-branch graph churn ---------------------------------------------------
+// The capture/replay/destroy churn that faults inside hipGraphLaunch on the
+// runtime torch bundles (profiles/graph_crash_r05.txt), run here
+// on /opt/rocm's runtime with library calls as the graph's kernels: graphs of
+// 1-6 tulips_csum_batch_fixed calls round-robin over 1-4 side streams forked
+// from and joined to the capture stream, at most 8 live (a new capture
+// destroys a random one), replays on a pool of other streams with every
+// output checked, direct calls between, random drops. Prints one progress
+// line a second; a fault ends the process.
+int
+cmd_graph_churn(double seconds, uint64_t seed)
+{
+  Rng r{ seed * 0x9E3779B97F4A7C15ull + 1 };
+  const uint32_t n = 4096, L = 1500;
+  std::vector<uint8_t> bytes(size_t(n) * L + 64);
+  for (auto& b : bytes) {
+    b = uint8_t(r.next());
+  }
+  uint8_t* arena = to_device(bytes);
+  uint16_t* ref = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&ref), n * 2));
+  CS_OK(tulips_csum_batch_fixed(arena, L, L, nullptr, nullptr, nullptr, ref, n,
+                                TULIPS_CSUM_RAW, nullptr));
+  HIP_OK(hipDeviceSynchronize());
+  const std::vector<uint16_t> want = to_host(ref, n);
+  struct Live
+  {
+    hipGraphExec_t x;
+    std::vector<uint16_t*> outs;
+  };
+  std::vector<Live> live;
+  auto drop = [&](size_t k) {
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipGraphExecDestroy(live[k].x));
+    for (uint16_t* o : live[k].outs) {
+      HIP_OK(hipFree(o));
+    }
+    live.erase(live.begin() + long(k));
+  };
+  std::vector<hipStream_t> pool(4);
+  for (auto& p : pool) {
+    HIP_OK(hipStreamCreateWithFlags(&p, hipStreamNonBlocking));
+  }
+  uint64_t steps = 0, captures = 0, replays = 0, destroyed = 0, bad = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto last = t0;
+  for (;;) {
+    const auto now = std::chrono::steady_clock::now();
+    const double el = std::chrono::duration<double>(now - t0).count();
+    if (el >= seconds) {
+      break;
+    }
+    if (std::chrono::duration<double>(now - last).count() >= 1.0) {
+      last = now;
+      printf("{\"progress_s\": %.0f, \"steps\": %llu}\n", el, (unsigned long long)steps);
+      fflush(stdout);
+    }
+    const uint32_t op = r.next() % 100;
+    if (op < 30 || live.empty()) {
+      const uint32_t ncalls = 1 + r.next() % 6, nside = 1 + r.next() % 4;
+      hipStream_t cap = nullptr;
+      std::vector<hipStream_t> side(nside);
+      HIP_OK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+      for (auto& sd : side) {
+        HIP_OK(hipStreamCreateWithFlags(&sd, hipStreamNonBlocking));
+      }
+      Live g{};
+      for (uint32_t c = 0; c < ncalls; ++c) {
+        uint16_t* o = nullptr;
+        HIP_OK(hipMalloc(reinterpret_cast<void**>(&o), n * 2));
+        g.outs.push_back(o);
+      }
+      hipEvent_t fork = nullptr;
+      std::vector<hipEvent_t> joins(nside);
+      HIP_OK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+      for (auto& e : joins) {
+        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
+      HIP_OK(hipStreamBeginCapture(cap, hipStreamCaptureModeGlobal));
+      HIP_OK(hipEventRecord(fork, cap));
+      for (auto& sd : side) {
+        HIP_OK(hipStreamWaitEvent(sd, fork, 0));
+      }
+      for (uint32_t c = 0; c < ncalls; ++c) {
+        CS_OK(tulips_csum_batch_fixed(arena, L, L, nullptr, nullptr, nullptr, g.outs[c], n,
+                                      TULIPS_CSUM_RAW, side[c % nside]));
+      }
+      for (uint32_t k = 0; k < nside; ++k) {
+        HIP_OK(hipEventRecord(joins[k], side[k]));
+        HIP_OK(hipStreamWaitEvent(cap, joins[k], 0));
+      }
+      hipGraph_t graph = nullptr;
+      HIP_OK(hipStreamEndCapture(cap, &graph));
+      HIP_OK(hipGraphInstantiate(&g.x, graph, nullptr, nullptr, 0));
+      HIP_OK(hipGraphDestroy(graph));
+      HIP_OK(hipEventDestroy(fork));
+      for (auto& e : joins) {
+        HIP_OK(hipEventDestroy(e));
+      }
+      for (auto& sd : side) {
+        HIP_OK(hipStreamDestroy(sd));
+      }
+      HIP_OK(hipStreamDestroy(cap));
+      live.push_back(g);
+      ++captures;
+      if (live.size() > 8) {
+        drop(r.next() % live.size());
+        ++destroyed;
+      }
+    } else if (op < 75) {
+      Live& g = live[r.next() % live.size()];
+      for (uint16_t* o : g.outs) {
+        HIP_OK(hipMemset(o, 0xA5, n * 2));
+      }
+      hipStream_t on = pool[r.next() % pool.size()];
+      HIP_OK(hipGraphLaunch(g.x, on));
+      HIP_OK(hipStreamSynchronize(on));
+      for (uint16_t* o : g.outs) {
+        bad += to_host(o, n) == want ? 0 : 1;
+      }
+      ++replays;
+    } else if (op < 95) {
+      hipStream_t on = pool[r.next() % pool.size()];
+      CS_OK(tulips_csum_batch_fixed(arena, L, L, nullptr, nullptr, nullptr, ref, n,
+                                    TULIPS_CSUM_RAW, on));
+      HIP_OK(hipStreamSynchronize(on));
+      bad += to_host(ref, n) == want ? 0 : 1;
+    } else {
+      drop(r.next() % live.size());
+      ++destroyed;
+    }
+    ++steps;
+  }
+  while (!live.empty()) {
+    drop(0);
+  }
+  printf("{\"graph_churn_s\": %.1f, \"steps\": %llu, \"captures\": %llu, \"replays\": %llu, "
+         "\"destroyed\": %llu, \"mismatches\": %llu, \"ok\": %s, \"runtime\": %s}\n",
+         seconds, (unsigned long long)steps, (unsigned long long)captures,
+         (unsigned long long)replays, (unsigned long long)destroyed, (unsigned long long)bad,
+         bad ? "false" : "true", runtime_json().c_str());
+  for (auto& p : pool) {
+    HIP_OK(hipStreamDestroy(p));
+  }
+  (void)hipFree(arena);
+  (void)hipFree(ref);
+  return bad ? 1 : 0;
+}
+
 } // namespace
 
 int
 main(int argc, char** argv)
 {
   if (argc < 2) {
-    fprintf(stderr, "usage: %s runtime | parity NAME=FNV... | user-object | graph-cycles N\n",
+    fprintf(stderr,
+            "usage: %s runtime | zipf-lengths | parity NAME=FNV... | user-object | "
+            "graph-cycles N | graph-churn SECONDS SEED\n",
             argv[0]);
     return 2;
   }
@@ -611,6 +766,9 @@ main(int argc, char** argv)
   }
   if (cmd == "user-object") {
     return cmd_user_object();
+  }
+  if (cmd == "graph-churn" && argc == 4) {
+    return cmd_graph_churn(strtod(argv[2], nullptr), strtoull(argv[3], nullptr, 10));
   }
   if (cmd == "graph-cycles" && argc == 3) {
     return cmd_graph_cycles(uint32_t(strtoul(argv[2], nullptr, 10)));

@@ -9,8 +9,14 @@ NOEMPTY=1 never forks a side stream that gets no work; SAME=1 replays on the
 current stream instead of a fresh pool stream; NODROP=1 never destroys a
 graph while others live (at most 8 are made); MAXLIVE=k keeps at most k
 graphs (a new capture drops one); KEEPALL=1 never destroys a graph and
-keeps capturing. Prints progress; a crash ends
-the process (exit 139)."""
+keeps capturing; SYNCDROP=1 synchronises the device and collects garbage
+before and after every graph destruction (the teardown-order test ADVICE r05
+asked for). Prints progress; a crash ends the process (exit 139).
+
+The fault (profiles/graph_crash_r05.txt): hip::Graph::UpdateStreams, called
+from hip::GraphExec::Run, reads a NULL or stale entry of the launched
+executable's parallel-stream list."""
+import gc
 import os
 import time
 
@@ -21,6 +27,18 @@ rng = np.random.default_rng(int(os.environ.get("SEED", "1")))
 budget = float(os.environ.get("SECS", "60"))
 xs = [torch.zeros(1 << 16, device="cuda:0") for _ in range(6)]
 graphs = []
+
+
+def drop(k):
+    if os.environ.get("SYNCDROP"):
+        torch.cuda.synchronize()
+        graphs.pop(k)
+        gc.collect()
+        torch.cuda.synchronize()
+    else:
+        graphs.pop(k)
+
+
 t0 = last = time.monotonic()
 steps = 0
 while time.monotonic() - t0 < budget:
@@ -46,7 +64,7 @@ while time.monotonic() - t0 < budget:
                 main.wait_stream(sd)
         graphs.append((g, outs))
         if not os.environ.get("KEEPALL") and len(graphs) > int(os.environ.get("MAXLIVE", "8")):
-            graphs.pop(int(rng.integers(0, len(graphs))))
+            drop(int(rng.integers(0, len(graphs))))
     elif op < 0.75:
         g, outs = graphs[int(rng.integers(0, len(graphs)))]
         for o in outs:
@@ -66,7 +84,7 @@ while time.monotonic() - t0 < budget:
             o.add_(xs[0])
         torch.cuda.synchronize()
     elif not os.environ.get("NODROP") and not os.environ.get("KEEPALL"):
-        graphs.pop(int(rng.integers(0, len(graphs))))
+        drop(int(rng.integers(0, len(graphs))))
     steps += 1
     if time.monotonic() - last > 10:
         last = time.monotonic()
