@@ -696,10 +696,12 @@ cmd_graph_churn(double seconds, uint64_t seed)
       }
     } else if (op < 75) {
       Live& g = live[r.next() % live.size()];
-      for (uint16_t* o : g.outs) {
-        HIP_OK(hipMemset(o, 0xA5, n * 2));
-      }
       hipStream_t on = pool[r.next() % pool.size()];
+      // poisoned in the replay stream's order (a plain hipMemset is not
+      // ordered with non-blocking streams)
+      for (uint16_t* o : g.outs) {
+        HIP_OK(hipMemsetAsync(o, 0xA5, n * 2, on));
+      }
       HIP_OK(hipGraphLaunch(g.x, on));
       HIP_OK(hipStreamSynchronize(on));
       for (uint16_t* o : g.outs) {

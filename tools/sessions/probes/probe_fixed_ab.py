@@ -16,12 +16,13 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
 from tulips_amd import csum  # noqa: E402
+import benchlib  # noqa: E402
 
 N = 65536
 
@@ -48,7 +49,7 @@ def main():
             continue
         bb = N * L
         buf = torch.empty(nb * bb + 256, dtype=torch.uint8, device=dev)
-        csum.fill_splitmix(buf, nb * bb)
+        benchlib.fill_splitmix(buf, nb * bb)
         outs = {k: torch.empty(nb * N, dtype=torch.uint16, device=dev) for k in libs}
 
         def form(k):
@@ -66,10 +67,10 @@ def main():
         def read(i, st):   # the kernel's own load pattern, no arithmetic
             b = i % nb
             if L == 1500:
-                csum.lib.tulips_csum_stream_read_slots_geom(buf.data_ptr() + b * bb, L, L, N, 32,
+                benchlib.lib.tulips_csum_stream_read_slots_geom(buf.data_ptr() + b * bb, L, L, N, 32,
                                                             3, sink.data_ptr(), st)
             else:
-                csum.lib.tulips_csum_stream_read_tiles(buf.data_ptr() + b * bb, L, N,
+                benchlib.lib.tulips_csum_stream_read_tiles(buf.data_ptr() + b * bb, L, N,
                                                        sink.data_ptr(), st)
         forms["read"] = read
         outs["read"] = outs["P"]
