@@ -31,7 +31,10 @@
 //   runtime_check graph-churn SECONDS SEED
 //       the multi-branch capture/replay/destroy churn that faults inside
 //       the runtime torch bundles, on this runtime, with
-//       library calls as the graphs' kernels and every replay checked.
+//       library calls as the graphs' kernels and every replay checked
+//       (diagnostics: CHURN_PRESYNC=1 completes the poison before each
+//       launch, CHURN_DEVSYNC=1 waits for the device instead of the replay
+//       stream; each mismatch is printed).
 // Exit status 0 = all checks passed; every result is printed as JSON.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -614,7 +617,10 @@ cmd_graph_churn(double seconds, uint64_t seed)
   {
     hipGraphExec_t x;
     std::vector<uint16_t*> outs;
+    uint32_t nside;
   };
+  const bool presync = getenv("CHURN_PRESYNC") != nullptr;
+  const bool devsync = getenv("CHURN_DEVSYNC") != nullptr;
   std::vector<Live> live;
   auto drop = [&](size_t k) {
     HIP_OK(hipDeviceSynchronize());
@@ -652,6 +658,7 @@ cmd_graph_churn(double seconds, uint64_t seed)
         HIP_OK(hipStreamCreateWithFlags(&sd, hipStreamNonBlocking));
       }
       Live g{};
+      g.nside = nside;
       for (uint32_t c = 0; c < ncalls; ++c) {
         uint16_t* o = nullptr;
         HIP_OK(hipMalloc(reinterpret_cast<void**>(&o), n * 2));
@@ -702,18 +709,50 @@ cmd_graph_churn(double seconds, uint64_t seed)
       for (uint16_t* o : g.outs) {
         HIP_OK(hipMemsetAsync(o, 0xA5, n * 2, on));
       }
+      if (presync) { // diagnostic: the poison complete before the launch
+        HIP_OK(hipStreamSynchronize(on));
+      }
       HIP_OK(hipGraphLaunch(g.x, on));
-      HIP_OK(hipStreamSynchronize(on));
-      for (uint16_t* o : g.outs) {
-        bad += to_host(o, n) == want ? 0 : 1;
+      if (devsync) { // diagnostic: wait for the whole device, not the stream
+        HIP_OK(hipDeviceSynchronize());
+      } else {
+        HIP_OK(hipStreamSynchronize(on));
+      }
+      for (size_t c = 0; c < g.outs.size(); ++c) {
+        const std::vector<uint16_t> got = to_host(g.outs[c], n);
+        if (got != want) {
+          ++bad;
+          uint32_t poison = 0, wrong = 0, first = n;
+          for (uint32_t k = 0; k < n; ++k) {
+            if (got[k] != want[k]) {
+              poison += got[k] == 0xA5A5 ? 1 : 0;
+              wrong += got[k] != 0xA5A5 ? 1 : 0;
+              first = std::min(first, k);
+            }
+          }
+          if (bad <= 12) {
+            printf("{\"mismatch\": \"replay\", \"step\": %llu, \"call\": %zu, \"calls\": %zu, "
+                   "\"branches\": %u, \"poison_words\": %u, \"wrong_words\": %u, "
+                   "\"first\": %u}\n",
+                   (unsigned long long)steps, c, g.outs.size(), g.nside, poison, wrong, first);
+            fflush(stdout);
+          }
+        }
       }
       ++replays;
     } else if (op < 95) {
       hipStream_t on = pool[r.next() % pool.size()];
+      HIP_OK(hipMemsetAsync(ref, 0xA5, n * 2, on));
       CS_OK(tulips_csum_batch_fixed(arena, L, L, nullptr, nullptr, nullptr, ref, n,
                                     TULIPS_CSUM_RAW, on));
       HIP_OK(hipStreamSynchronize(on));
-      bad += to_host(ref, n) == want ? 0 : 1;
+      if (to_host(ref, n) != want) {
+        ++bad;
+        if (bad <= 12) {
+          printf("{\"mismatch\": \"direct\", \"step\": %llu}\n", (unsigned long long)steps);
+          fflush(stdout);
+        }
+      }
     } else {
       drop(r.next() % live.size());
       ++destroyed;

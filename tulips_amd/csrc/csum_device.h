@@ -250,50 +250,6 @@ masked_value(u32x4 v, int lo, int hi)
   return chunk_value(m);
 }
 
-#ifdef TCS_DOT2_PARTIAL
-// lane_partial with the per-chunk value as the sum of its eight 16-bit
-// halves (4 x v_dot2_u32_u16 into one u32, congruent to the dword sum mod
-// 65535): half the VALU of the 64-bit dword sum. No overflow: a lane holds
-// at most 4,096 / G <= 256 chunks of a 65,535-byte segment, 256 x 8 x 65535
-// < 2^32. (A/B build: tools/sessions/probes/probe_fixed_ab.py.)
-template<int G, int U, bool NT>
-__device__ __forceinline__ uint64_t
-lane_partial_dot2(uintptr_t sa, uint32_t len, int lane)
-{
-  if (len == 0) {
-    return 0;
-  }
-  const uintptr_t a0 = sa & ~uintptr_t(15);
-  const uintptr_t ea = sa + len;
-  const int nch = int((ea - a0 + 15) >> 4);
-  const gchunk_ptr p = reinterpret_cast<gchunk_ptr>(a0);
-  const int head = int(sa - a0);
-  const int last = nch - 1;
-  const int tail = int(ea - a0) - 16 * last;
-  uint32_t acc = 0;
-  for (int c = lane; c < nch; c += U * G) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      v[u] = load_chunk<NT>(p + min(c + u * G, last));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int cc = c + u * G;
-      const uint32_t with = chunk_value_acc(v[u], acc);
-      acc = cc <= last ? with : acc;
-      if (u == 0 && cc == 0 && head != 0) {
-        acc -= masked_value(v[u], 0, head);
-      }
-      if (cc == last && tail != 16) {
-        acc -= masked_value(v[u], tail, 16);
-      }
-    }
-  }
-  return acc;
-}
-#endif
-
 // Inclusive u32 add-scan over the 64 lanes of a wave (csum_common.h).
 __device__ __forceinline__ uint32_t
 wave_incl_scan(uint32_t x)

@@ -52,11 +52,7 @@ csum_kernel(Segs segs, const uint16_t* __restrict__ seeds,
     const uint32_t len = segs.length(seg);
     const uintptr_t sa = reinterpret_cast<uintptr_t>(segs.base) + off;
     const SideIn side = load_side(seg, seeds, src, dst, mode);
-#ifdef TCS_DOT2_PARTIAL
-    const uint64_t acc = lane_partial_dot2<G, U, NT>(sa, len, lane);
-#else
     const uint64_t acc = lane_partial<G, U, NT>(sa, len, lane);
-#endif
     const uint32_t part = subgroup_sum<G>(fold64(acc));
     if (lane == 0) {
       emit_with(seg, part, sa, len, side, out, bad, mode, nt_store);
