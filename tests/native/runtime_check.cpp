@@ -28,6 +28,10 @@
 //       destroy the executable: every replay's outputs equal the direct
 //       calls', and device memory (hipMemGetInfo, after 5 warm-up cycles)
 //       ends within 1 MiB of where it started (also reported half-way).
+//   runtime_check serial-rate L NBATCH FNV
+//       the fixed-stride kernel's one-launch-at-a-time rate on this runtime
+//       (NBATCH rotated batches of 65,536 x L bytes, a captured chain of 256
+//       launches, HIP events, median of 5), batch 0 checked against FNV.
 //   runtime_check graph-churn SECONDS SEED
 //       the multi-branch capture/replay/destroy churn that faults inside
 //       the runtime torch bundles, on this runtime, with
@@ -775,6 +779,78 @@ cmd_graph_churn(double seconds, uint64_t seed)
   return bad ? 1 : 0;
 }
 
+// ---- serial rate ------------------------------------------------------------------
+// The headline kernel's one-launch-at-a-time rate on this runtime: NB batches
+// of 65,536 segments of L bytes (the §8c arena, rotated so every launch
+// streams from HBM), a chain of 256 tulips_csum_batch_fixed launches captured
+// in one single-stream graph, timed with HIP events over 5 replays (median),
+// every batch's digest checked against `want` (the §8c FNV of batch 0).
+int
+cmd_serial_rate(uint32_t L, uint32_t nb, const char* want0)
+{
+  const uint64_t bb = uint64_t(NSEG) * L;
+  std::vector<uint8_t> host(nb * bb + 64, 0);
+  splitmix_fill(host.data(), nb * bb);
+  uint8_t* arena = to_device(host);
+  host.clear();
+  host.shrink_to_fit();
+  uint16_t* out = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&out), size_t(nb) * NSEG * 2));
+  hipStream_t s = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  constexpr int CHAIN = 256;
+  auto launch = [&](int i) {
+    const uint32_t b = uint32_t(i) % nb;
+    CS_OK(tulips_csum_batch_fixed(arena + b * bb, L, L, nullptr, nullptr, nullptr,
+                                  out + size_t(b) * NSEG, NSEG, TULIPS_CSUM_RAW, s));
+  };
+  for (uint32_t i = 0; i < nb; ++i) {
+    launch(int(i));
+  }
+  HIP_OK(hipStreamSynchronize(s));
+  hipGraph_t g = nullptr;
+  HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+  for (int i = 0; i < CHAIN; ++i) {
+    launch(i);
+  }
+  HIP_OK(hipStreamEndCapture(s, &g));
+  hipGraphExec_t x = nullptr;
+  HIP_OK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+  HIP_OK(hipGraphDestroy(g));
+  HIP_OK(hipGraphLaunch(x, s)); // warm
+  HIP_OK(hipStreamSynchronize(s));
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  std::vector<double> us;
+  for (int rep = 0; rep < 5; ++rep) {
+    HIP_OK(hipMemsetAsync(out, 0xA5, size_t(nb) * NSEG * 2, s));
+    HIP_OK(hipEventRecord(e0, s));
+    HIP_OK(hipGraphLaunch(x, s));
+    HIP_OK(hipEventRecord(e1, s));
+    HIP_OK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    us.push_back(double(ms) * 1e3 / CHAIN);
+  }
+  std::sort(us.begin(), us.end());
+  const double med = us[us.size() / 2];
+  const std::vector<uint16_t> b0 = to_host(out, NSEG);
+  const std::string d0 = hex64(fnv1a_u16(b0));
+  const bool ok = d0 == want0;
+  const double frac = double(bb) / (med * 1e-6) / 8e12;
+  printf("{\"serial_rate\": {\"length\": %u, \"batches\": %u, \"chain\": %d, \"us_per_launch\": %.3f, "
+         "\"frac_of_8TBps\": %.4f, \"GiBps\": %.1f, \"batch0_fnv1a64\": \"%s\", \"parity\": \"%s\"}, "
+         "\"runtime\": %s}\n",
+         L, nb, CHAIN, med, frac, double(bb) / (med * 1e-6) / 1073741824.0, d0.c_str(),
+         ok ? "ok" : "MISMATCH", runtime_json().c_str());
+  HIP_OK(hipGraphExecDestroy(x));
+  HIP_OK(hipStreamDestroy(s));
+  (void)hipFree(arena);
+  (void)hipFree(out);
+  return ok ? 0 : 1;
+}
+
 } // namespace
 
 int
@@ -783,7 +859,7 @@ main(int argc, char** argv)
   if (argc < 2) {
     fprintf(stderr,
             "usage: %s runtime | zipf-lengths | parity NAME=FNV... | user-object | "
-            "graph-cycles N | graph-churn SECONDS SEED\n",
+            "graph-cycles N | graph-churn SECONDS SEED | serial-rate L NBATCH FNV\n",
             argv[0]);
     return 2;
   }
@@ -807,6 +883,10 @@ main(int argc, char** argv)
   }
   if (cmd == "user-object") {
     return cmd_user_object();
+  }
+  if (cmd == "serial-rate" && argc == 5) {
+    return cmd_serial_rate(uint32_t(strtoul(argv[2], nullptr, 10)),
+                           uint32_t(strtoul(argv[3], nullptr, 10)), argv[4]);
   }
   if (cmd == "graph-churn" && argc == 4) {
     return cmd_graph_churn(strtod(argv[2], nullptr), strtoull(argv[3], nullptr, 10));

@@ -64,3 +64,17 @@ def test_native_500_graph_cycles():
     rc, res, err = _run("graph-cycles", "500", timeout=540)
     print(json.dumps(res, indent=1))
     assert rc == 0, (res, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_native_serial_rate_on_integrator_runtime(golden):
+    """The headline kernel through the C ABI on /opt/rocm's runtime, one launch
+    at a time over 16 rotated F1500 batches: batch 0 equals the reference
+    digest, and the rate is of the order bench.py measures on torch's runtime
+    (a loose floor: the figure itself is reported, not asserted)."""
+    b = golden.digests()["batches"]["F1500"]
+    rc, res, err = _run("serial-rate", "1500", "16", b["fnv1a64"], timeout=240)
+    print(json.dumps(res, indent=1))
+    assert rc == 0 and res["serial_rate"]["parity"] == "ok", (res, err)
+    assert res["serial_rate"]["frac_of_8TBps"] > 0.5, res
