@@ -38,7 +38,8 @@
 //       library calls as the graphs' kernels and every replay checked
 //       (diagnostics: CHURN_PRESYNC=1 completes the poison before each
 //       launch, CHURN_DEVSYNC=1 waits for the device instead of the replay
-//       stream; each mismatch is printed).
+//       stream, CHURN_KERNEL_POISON=1 poisons with a kernel instead of
+//       hipMemsetAsync; each mismatch is printed).
 // Exit status 0 = all checks passed; every result is printed as JSON.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -625,6 +626,14 @@ cmd_graph_churn(double seconds, uint64_t seed)
   };
   const bool presync = getenv("CHURN_PRESYNC") != nullptr;
   const bool devsync = getenv("CHURN_DEVSYNC") != nullptr;
+  // diagnostic: poison with a kernel (the library's checksum of an all-zero
+  // arena: 0x0000 words) instead of hipMemsetAsync
+  const bool kpoison = getenv("CHURN_KERNEL_POISON") != nullptr;
+  uint8_t* zeros = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&zeros), size_t(n) * L + 64));
+  HIP_OK(hipMemset(zeros, 0, size_t(n) * L + 64));
+  HIP_OK(hipDeviceSynchronize());
+  const uint16_t poison_word = kpoison ? 0x0000 : 0xA5A5;
   std::vector<Live> live;
   auto drop = [&](size_t k) {
     HIP_OK(hipDeviceSynchronize());
@@ -711,7 +720,12 @@ cmd_graph_churn(double seconds, uint64_t seed)
       // poisoned in the replay stream's order (a plain hipMemset is not
       // ordered with non-blocking streams)
       for (uint16_t* o : g.outs) {
-        HIP_OK(hipMemsetAsync(o, 0xA5, n * 2, on));
+        if (kpoison) {
+          CS_OK(tulips_csum_batch_fixed(zeros, L, L, nullptr, nullptr, nullptr, o, n,
+                                        TULIPS_CSUM_RAW, on));
+        } else {
+          HIP_OK(hipMemsetAsync(o, 0xA5, n * 2, on));
+        }
       }
       if (presync) { // diagnostic: the poison complete before the launch
         HIP_OK(hipStreamSynchronize(on));
@@ -729,8 +743,8 @@ cmd_graph_churn(double seconds, uint64_t seed)
           uint32_t poison = 0, wrong = 0, first = n;
           for (uint32_t k = 0; k < n; ++k) {
             if (got[k] != want[k]) {
-              poison += got[k] == 0xA5A5 ? 1 : 0;
-              wrong += got[k] != 0xA5A5 ? 1 : 0;
+              poison += got[k] == poison_word ? 1 : 0;
+              wrong += got[k] != poison_word ? 1 : 0;
               first = std::min(first, k);
             }
           }
@@ -776,6 +790,7 @@ cmd_graph_churn(double seconds, uint64_t seed)
   }
   (void)hipFree(arena);
   (void)hipFree(ref);
+  (void)hipFree(zeros);
   return bad ? 1 : 0;
 }
 
