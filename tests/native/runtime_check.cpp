@@ -39,7 +39,8 @@
 //       (diagnostics: CHURN_PRESYNC=1 completes the poison before each
 //       launch, CHURN_DEVSYNC=1 waits for the device instead of the replay
 //       stream, CHURN_KERNEL_POISON=1 poisons with a kernel instead of
-//       hipMemsetAsync; each mismatch is printed).
+//       hipMemsetAsync, CHURN_NODROP=1 never destroys a graph (8 are made);
+//       each mismatch is printed).
 // Exit status 0 = all checks passed; every result is printed as JSON.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -629,6 +630,8 @@ cmd_graph_churn(double seconds, uint64_t seed)
   // diagnostic: poison with a kernel (the library's checksum of an all-zero
   // arena: 0x0000 words) instead of hipMemsetAsync
   const bool kpoison = getenv("CHURN_KERNEL_POISON") != nullptr;
+  // diagnostic: never destroy a graph (at most 8 are made, then only replays)
+  const bool nodrop = getenv("CHURN_NODROP") != nullptr;
   uint8_t* zeros = nullptr;
   HIP_OK(hipMalloc(reinterpret_cast<void**>(&zeros), size_t(n) * L + 64));
   HIP_OK(hipMemset(zeros, 0, size_t(n) * L + 64));
@@ -661,7 +664,10 @@ cmd_graph_churn(double seconds, uint64_t seed)
       printf("{\"progress_s\": %.0f, \"steps\": %llu}\n", el, (unsigned long long)steps);
       fflush(stdout);
     }
-    const uint32_t op = r.next() % 100;
+    uint32_t op = r.next() % 100;
+    if (nodrop && live.size() >= 8 && (op < 30 || op >= 95)) {
+      op = 50; // a replay instead of a capture or a drop
+    }
     if (op < 30 || live.empty()) {
       const uint32_t ncalls = 1 + r.next() % 6, nside = 1 + r.next() % 4;
       hipStream_t cap = nullptr;
