@@ -39,7 +39,8 @@
 //       (diagnostics: CHURN_PRESYNC=1 completes the poison before each
 //       launch, CHURN_DEVSYNC=1 waits for the device instead of the replay
 //       stream, CHURN_KERNEL_POISON=1 poisons with a kernel instead of
-//       hipMemsetAsync, CHURN_NODROP=1 never destroys a graph (8 are made);
+//       hipMemsetAsync, CHURN_NODROP=1 never destroys a graph (8 are made),
+//       CHURN_ONE_ROOT=1 gives every graph a single root node;
 //       each mismatch is printed).
 // Exit status 0 = all checks passed; every result is printed as JSON.
 #include <dlfcn.h>
@@ -632,6 +633,11 @@ cmd_graph_churn(double seconds, uint64_t seed)
   const bool kpoison = getenv("CHURN_KERNEL_POISON") != nullptr;
   // diagnostic: never destroy a graph (at most 8 are made, then only replays)
   const bool nodrop = getenv("CHURN_NODROP") != nullptr;
+  // diagnostic: give every graph one root node (a 4-byte memset on the
+  // capture stream before the fork), so every branch depends on it
+  const bool one_root = getenv("CHURN_ONE_ROOT") != nullptr;
+  uint32_t* scratch = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&scratch), 64));
   uint8_t* zeros = nullptr;
   HIP_OK(hipMalloc(reinterpret_cast<void**>(&zeros), size_t(n) * L + 64));
   HIP_OK(hipMemset(zeros, 0, size_t(n) * L + 64));
@@ -690,6 +696,9 @@ cmd_graph_churn(double seconds, uint64_t seed)
         HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       }
       HIP_OK(hipStreamBeginCapture(cap, hipStreamCaptureModeGlobal));
+      if (one_root) {
+        HIP_OK(hipMemsetAsync(scratch, 0, 4, cap));
+      }
       HIP_OK(hipEventRecord(fork, cap));
       for (auto& sd : side) {
         HIP_OK(hipStreamWaitEvent(sd, fork, 0));
@@ -797,6 +806,7 @@ cmd_graph_churn(double seconds, uint64_t seed)
   (void)hipFree(arena);
   (void)hipFree(ref);
   (void)hipFree(zeros);
+  (void)hipFree(scratch);
   return bad ? 1 : 0;
 }
 
