@@ -763,11 +763,19 @@ cmd_graph_churn(double seconds, uint64_t seed)
               first = std::min(first, k);
             }
           }
+          // read again after the whole device has idled: right now (the
+          // graph's kernel finished after the replay stream's sync: the end
+          // of the replay unordered) or still poisoned (the kernel ran
+          // before the poison: the start unordered)
+          std::this_thread::sleep_for(std::chrono::milliseconds(2));
+          HIP_OK(hipDeviceSynchronize());
+          const bool late_ok = to_host(g.outs[c], n) == want;
           if (bad <= 12) {
             printf("{\"mismatch\": \"replay\", \"step\": %llu, \"call\": %zu, \"calls\": %zu, "
                    "\"branches\": %u, \"poison_words\": %u, \"wrong_words\": %u, "
-                   "\"first\": %u}\n",
-                   (unsigned long long)steps, c, g.outs.size(), g.nside, poison, wrong, first);
+                   "\"first\": %u, \"right_after_idle\": %s}\n",
+                   (unsigned long long)steps, c, g.outs.size(), g.nside, poison, wrong, first,
+                   late_ok ? "true" : "false");
             fflush(stdout);
           }
         }
