@@ -28,6 +28,10 @@
 //       destroy the executable: every replay's outputs equal the direct
 //       calls', and device memory (hipMemGetInfo, after 5 warm-up cycles)
 //       ends within 1 MiB of where it started (also reported half-way).
+//   runtime_check graph-churn-stateful SECONDS SEED
+//       graph ownership under churn: multi-branch graphs of counting, arena,
+//       segmentation and fixed calls captured, replayed (checked) and
+//       destroyed; device memory flat at the end.
 //   runtime_check serial-rate L NBATCH FNV
 //       the fixed-stride kernel's one-launch-at-a-time rate on this runtime
 //       (NBATCH rotated batches of 65,536 x L bytes, a captured chain of 256
@@ -890,6 +894,304 @@ cmd_serial_rate(uint32_t L, uint32_t nb, const char* want0)
   return ok ? 0 : 1;
 }
 
+// ---- stateful multi-branch churn --------------------------------------------------
+// Graph ownership under churn (stream_state.h): graphs of 1-6 library calls of
+// every stateful kind — counting verify (counter shards), arena batch (span
+// words), segmentation (workspace) — and the stateless fixed batch,
+// round-robin over 1-4 side streams forked from and joined to the capture
+// stream (each side stream's state attaches its own user object to the
+// graph), at most 8 live, a new capture destroying a random one; replays on
+// a pool of other streams with every output checked against the direct
+// calls'; random drops. The launch stream is idle before each replay (the
+// /opt/rocm runtime can start a multi-branch graph before the launch
+// stream's pending work). At the end every graph is destroyed,
+// one direct call reclaims their arrays, and device memory must be back
+// within 4 MiB of where it stood after the warm-up.
+int
+cmd_graph_churn_stateful(double seconds, uint64_t seed)
+{
+  Rng r{ seed * 0x9E3779B97F4A7C15ull + 7 };
+  const uint32_t n = 2048, L = 1500;
+  std::vector<uint8_t> bytes(size_t(n) * 9000 + 64);
+  for (auto& b : bytes) {
+    b = uint8_t(r.next());
+  }
+  std::vector<uint16_t> lens(n);
+  std::vector<uint64_t> offs(n);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    lens[i] = uint16_t(40 + r.next() % 8960);
+    offs[i] = total;
+    total += lens[i];
+  }
+  uint8_t* d_bytes = to_device(bytes);
+  uint64_t* d_offs = to_device(offs);
+  uint16_t* d_lens = to_device(lens);
+  uint32_t* src = to_device(std::vector<uint32_t>(n, ip4(10, 1, 0, 1)));
+  uint32_t* dst = to_device(std::vector<uint32_t>(n, ip4(10, 1, 0, 2)));
+  std::vector<uint8_t> frames;
+  std::vector<uint64_t> foffs;
+  std::vector<uint16_t> flens;
+  for (int k = 0; k < 16; ++k) {
+    const std::vector<uint8_t> f = tcp_frame(r, 1000 + r.next() % 30000);
+    foffs.push_back(frames.size());
+    flens.push_back(uint16_t(f.size()));
+    frames.insert(frames.end(), f.begin(), f.end());
+    frames.resize((frames.size() + 2047) & ~size_t(2047));
+  }
+  const uint32_t nf = uint32_t(foffs.size()), mss = 1460, ostride = 2048, cap_seg = 512;
+  uint8_t* d_frames = to_device(frames);
+  uint64_t* d_foffs = to_device(foffs);
+  uint16_t* d_flens = to_device(flens);
+  // a call's output buffers, by kind: 0 fixed, 1 verify, 2 arena, 3 segmentation
+  struct Out
+  {
+    int kind;
+    std::vector<void*> bufs;
+    std::vector<size_t> sizes;
+  };
+  auto make_out = [&](int kind) {
+    Out o{ kind, {}, {} };
+    std::vector<size_t> sz;
+    switch (kind) {
+      case 0: sz = { n * 2 }; break;
+      case 1: sz = { n * 2, 4 }; break;
+      case 2: sz = { n * 2 }; break;
+      default: sz = { size_t(cap_seg) * ostride, cap_seg * 2, (nf + 1) * 4 }; break;
+    }
+    for (size_t b : sz) {
+      void* p = nullptr;
+      HIP_OK(hipMalloc(&p, b));
+      o.bufs.push_back(p);
+      o.sizes.push_back(b);
+    }
+    return o;
+  };
+  auto call = [&](const Out& o, hipStream_t st) {
+    switch (o.kind) {
+      case 0:
+        CS_OK(tulips_csum_batch_fixed(d_bytes, L, L, nullptr, nullptr, nullptr,
+                                      static_cast<uint16_t*>(o.bufs[0]), n, TULIPS_CSUM_RAW, st));
+        break;
+      case 1:
+        CS_OK(tulips_csum_verify(d_bytes, d_offs, d_lens, src, dst,
+                                 static_cast<uint16_t*>(o.bufs[0]),
+                                 static_cast<uint32_t*>(o.bufs[1]), n, TULIPS_CSUM_TCP, st));
+        break;
+      case 2:
+        CS_OK(tulips_csum_batch_arena(d_bytes, total, d_offs, d_lens, nullptr, nullptr, nullptr,
+                                      static_cast<uint16_t*>(o.bufs[0]), n, TULIPS_CSUM_INET,
+                                      st));
+        break;
+      default:
+        CS_OK(tulips_csum_segment_frames(d_frames, d_foffs, d_flens, nf, mss,
+                                         static_cast<uint8_t*>(o.bufs[0]), ostride, cap_seg,
+                                         static_cast<uint16_t*>(o.bufs[1]),
+                                         static_cast<uint32_t*>(o.bufs[2]), st));
+        break;
+    }
+  };
+  auto poison = [&](const Out& o, hipStream_t st) {
+    for (size_t b = 0; b < o.bufs.size(); ++b) {
+      HIP_OK(hipMemsetAsync(o.bufs[b], 0xA5, o.sizes[b], st));
+    }
+  };
+  auto snap = [&](const Out& o) {
+    std::vector<std::vector<uint8_t>> v;
+    for (size_t b = 0; b < o.bufs.size(); ++b) {
+      v.push_back(to_host(static_cast<const uint8_t*>(o.bufs[b]), o.sizes[b]));
+    }
+    if (o.kind == 3) { // segment slots past each segment's length are not written
+      const uint16_t* ol = reinterpret_cast<const uint16_t*>(v[1].data());
+      const uint32_t segs =
+        std::min<uint32_t>(reinterpret_cast<const uint32_t*>(v[2].data())[nf], cap_seg);
+      for (uint32_t j = 0; j < cap_seg; ++j) {
+        const uint32_t keep = j < segs ? ol[j] : 0;
+        std::fill(v[0].begin() + size_t(j) * ostride + keep,
+                  v[0].begin() + size_t(j + 1) * ostride, uint8_t(0));
+      }
+    }
+    return v;
+  };
+  hipStream_t ds = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&ds, hipStreamNonBlocking));
+  std::vector<std::vector<std::vector<uint8_t>>> want(4);
+  std::vector<Out> ref;
+  for (int k = 0; k < 4; ++k) {
+    ref.push_back(make_out(k));
+    poison(ref[k], ds);
+    call(ref[k], ds);
+    HIP_OK(hipStreamSynchronize(ds));
+    want[k] = snap(ref[k]);
+  }
+  struct Live
+  {
+    hipGraphExec_t x;
+    std::vector<Out> outs;
+  };
+  std::vector<Live> live;
+  auto free_out = [&](Out& o) {
+    for (void* p : o.bufs) {
+      HIP_OK(hipFree(p));
+    }
+  };
+  auto drop = [&](size_t k) {
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipGraphExecDestroy(live[k].x));
+    for (Out& o : live[k].outs) {
+      free_out(o);
+    }
+    live.erase(live.begin() + long(k));
+  };
+  std::vector<hipStream_t> pool(4);
+  for (auto& p : pool) {
+    HIP_OK(hipStreamCreateWithFlags(&p, hipStreamNonBlocking));
+  }
+  auto free_now = [&]() {
+    for (int k = 0; k < 4; ++k) { // direct calls of every kind reclaim
+      call(ref[k], ds);
+    }
+    HIP_OK(hipDeviceSynchronize());
+    size_t f = 0, t = 0;
+    HIP_OK(hipMemGetInfo(&f, &t));
+    return f;
+  };
+  uint64_t steps = 0, captures = 0, replays = 0, destroyed = 0, bad = 0;
+  size_t free0 = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto last = t0;
+  for (;;) {
+    const auto now = std::chrono::steady_clock::now();
+    const double el = std::chrono::duration<double>(now - t0).count();
+    if (el >= seconds) {
+      break;
+    }
+    if (std::chrono::duration<double>(now - last).count() >= 1.0) {
+      last = now;
+      printf("{\"progress_s\": %.0f, \"steps\": %llu}\n", el, (unsigned long long)steps);
+      fflush(stdout);
+    }
+    if (steps == 40) { // after a warm-up of captures, replays and drops
+      while (!live.empty()) {
+        drop(0);
+      }
+      free0 = free_now();
+    }
+    const uint32_t op = r.next() % 100;
+    if (op < 30 || live.empty()) {
+      const uint32_t ncalls = 1 + r.next() % 6, nside = 1 + r.next() % 4;
+      hipStream_t cap = nullptr;
+      std::vector<hipStream_t> side(nside);
+      HIP_OK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+      for (auto& sd : side) {
+        HIP_OK(hipStreamCreateWithFlags(&sd, hipStreamNonBlocking));
+      }
+      Live g{};
+      for (uint32_t c = 0; c < ncalls; ++c) {
+        g.outs.push_back(make_out(int(r.next() % 4)));
+      }
+      hipEvent_t fork = nullptr;
+      std::vector<hipEvent_t> joins(nside);
+      HIP_OK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+      for (auto& e : joins) {
+        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
+      HIP_OK(hipStreamBeginCapture(cap, hipStreamCaptureModeGlobal));
+      HIP_OK(hipEventRecord(fork, cap));
+      for (auto& sd : side) {
+        HIP_OK(hipStreamWaitEvent(sd, fork, 0));
+      }
+      for (uint32_t c = 0; c < ncalls; ++c) {
+        call(g.outs[c], side[c % nside]);
+      }
+      for (uint32_t k = 0; k < nside; ++k) {
+        HIP_OK(hipEventRecord(joins[k], side[k]));
+        HIP_OK(hipStreamWaitEvent(cap, joins[k], 0));
+      }
+      hipGraph_t graph = nullptr;
+      HIP_OK(hipStreamEndCapture(cap, &graph));
+      HIP_OK(hipGraphInstantiate(&g.x, graph, nullptr, nullptr, 0));
+      HIP_OK(hipGraphDestroy(graph));
+      HIP_OK(hipEventDestroy(fork));
+      for (auto& e : joins) {
+        HIP_OK(hipEventDestroy(e));
+      }
+      // the library's state of these streams goes with them; the arrays the
+      // capture took stay with the graph
+      CS_OK(tulips_csum_release_stream(cap));
+      for (auto& sd : side) {
+        CS_OK(tulips_csum_release_stream(sd));
+        HIP_OK(hipStreamDestroy(sd));
+      }
+      HIP_OK(hipStreamDestroy(cap));
+      live.push_back(std::move(g));
+      ++captures;
+      if (live.size() > 8) {
+        drop(r.next() % live.size());
+        ++destroyed;
+      }
+    } else if (op < 75) {
+      Live& g = live[r.next() % live.size()];
+      hipStream_t on = pool[r.next() % pool.size()];
+      for (const Out& o : g.outs) {
+        poison(o, on);
+      }
+      HIP_OK(hipStreamSynchronize(on)); // idle before a multi-branch launch
+      HIP_OK(hipGraphLaunch(g.x, on));
+      HIP_OK(hipStreamSynchronize(on));
+      for (size_t c = 0; c < g.outs.size(); ++c) {
+        if (snap(g.outs[c]) != want[g.outs[c].kind]) {
+          ++bad;
+          if (bad <= 12) {
+            printf("{\"mismatch\": \"replay\", \"step\": %llu, \"kind\": %d}\n",
+                   (unsigned long long)steps, g.outs[c].kind);
+            fflush(stdout);
+          }
+        }
+      }
+      ++replays;
+    } else if (op < 95) {
+      const int k = int(r.next() % 4);
+      hipStream_t on = pool[r.next() % pool.size()];
+      poison(ref[k], on);
+      call(ref[k], on);
+      HIP_OK(hipStreamSynchronize(on));
+      if (snap(ref[k]) != want[k]) {
+        ++bad;
+        if (bad <= 12) {
+          printf("{\"mismatch\": \"direct\", \"step\": %llu, \"kind\": %d}\n",
+                 (unsigned long long)steps, k);
+          fflush(stdout);
+        }
+      }
+    } else {
+      drop(r.next() % live.size());
+      ++destroyed;
+    }
+    ++steps;
+  }
+  while (!live.empty()) {
+    drop(0);
+    ++destroyed;
+  }
+  const size_t free1 = free_now();
+  const long long grew = free0 ? (long long)free0 - (long long)free1 : 0;
+  const bool ok = bad == 0 && free0 != 0 && grew < (4ll << 20);
+  printf("{\"graph_churn_stateful_s\": %.1f, \"steps\": %llu, \"captures\": %llu, "
+         "\"replays\": %llu, \"destroyed\": %llu, \"mismatches\": %llu, \"free_after_warmup\": %zu, "
+         "\"free_after\": %zu, \"device_memory_growth\": %lld, \"ok\": %s, \"runtime\": %s}\n",
+         seconds, (unsigned long long)steps, (unsigned long long)captures,
+         (unsigned long long)replays, (unsigned long long)destroyed, (unsigned long long)bad,
+         free0, free1, grew, ok ? "true" : "false", runtime_json().c_str());
+  for (auto& p : pool) {
+    CS_OK(tulips_csum_release_stream(p));
+    HIP_OK(hipStreamDestroy(p));
+  }
+  CS_OK(tulips_csum_release_stream(ds));
+  HIP_OK(hipStreamDestroy(ds));
+  return ok ? 0 : 1;
+}
+
 } // namespace
 
 int
@@ -898,7 +1200,7 @@ main(int argc, char** argv)
   if (argc < 2) {
     fprintf(stderr,
             "usage: %s runtime | zipf-lengths | parity NAME=FNV... | user-object | "
-            "graph-cycles N | graph-churn SECONDS SEED | serial-rate L NBATCH FNV\n",
+            "graph-cycles N | graph-churn[-stateful] SECONDS SEED | serial-rate L NBATCH FNV\n",
             argv[0]);
     return 2;
   }
@@ -926,6 +1228,9 @@ main(int argc, char** argv)
   if (cmd == "serial-rate" && argc == 5) {
     return cmd_serial_rate(uint32_t(strtoul(argv[2], nullptr, 10)),
                            uint32_t(strtoul(argv[3], nullptr, 10)), argv[4]);
+  }
+  if (cmd == "graph-churn-stateful" && argc == 4) {
+    return cmd_graph_churn_stateful(strtod(argv[2], nullptr), strtoull(argv[3], nullptr, 10));
   }
   if (cmd == "graph-churn" && argc == 4) {
     return cmd_graph_churn(strtod(argv[2], nullptr), strtoull(argv[3], nullptr, 10));

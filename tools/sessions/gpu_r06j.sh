@@ -14,3 +14,8 @@ for v in nodrop churn; do
   rc=$?; echo "   rc=$rc"; grep mismatch $OUT/churn_$v.log | head -6; tail -1 $OUT/churn_$v.log | cut -c1-160
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 done
+unset CHURN_KERNEL_POISON CHURN_NODROP
+echo "== stateful multi-branch churn, graph ownership ($(date +%T))"
+timeout -k 10 100 tests/native/_build/runtime_check graph-churn-stateful 60 $RANDOM > $OUT/churn_stateful.log 2>&1
+rc=$?; echo "   rc=$rc"; grep mismatch $OUT/churn_stateful.log | head -4; tail -1 $OUT/churn_stateful.log | cut -c1-300
+exit $rc
