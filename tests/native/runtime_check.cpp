@@ -1057,7 +1057,7 @@ cmd_graph_churn_stateful(double seconds, uint64_t seed)
     return f;
   };
   uint64_t steps = 0, captures = 0, replays = 0, destroyed = 0, bad = 0;
-  size_t free0 = 0;
+  size_t free0 = 0, free_half = 0;
   const auto t0 = std::chrono::steady_clock::now();
   auto last = t0;
   for (;;) {
@@ -1071,11 +1071,14 @@ cmd_graph_churn_stateful(double seconds, uint64_t seed)
       printf("{\"progress_s\": %.0f, \"steps\": %llu}\n", el, (unsigned long long)steps);
       fflush(stdout);
     }
-    if (steps == 40) { // after a warm-up of captures, replays and drops
+    if (steps == 40 || (!free_half && free0 && el >= seconds / 2)) {
+      // after a warm-up of captures, replays and drops, and half-way: every
+      // graph destroyed, their arrays reclaimed
       while (!live.empty()) {
         drop(0);
+        ++destroyed;
       }
-      free0 = free_now();
+      (free0 ? free_half : free0) = free_now();
     }
     const uint32_t op = r.next() % 100;
     if (op < 30 || live.empty()) {
@@ -1175,14 +1178,20 @@ cmd_graph_churn_stateful(double seconds, uint64_t seed)
     ++destroyed;
   }
   const size_t free1 = free_now();
-  const long long grew = free0 ? (long long)free0 - (long long)free1 : 0;
-  const bool ok = bad == 0 && free0 != 0 && grew < (4ll << 20);
+  // the second half's captures (about as many as the first's) must leave
+  // nothing behind; the first half's growth (runtime pools of the streams and
+  // graphs it made) is reported
+  const long long grew_first = free_half ? (long long)free0 - (long long)free_half : 0;
+  const long long grew_second = free_half ? (long long)free_half - (long long)free1 : 0;
+  const bool ok = bad == 0 && free_half != 0 && grew_second < (4ll << 20);
   printf("{\"graph_churn_stateful_s\": %.1f, \"steps\": %llu, \"captures\": %llu, "
          "\"replays\": %llu, \"destroyed\": %llu, \"mismatches\": %llu, \"free_after_warmup\": %zu, "
-         "\"free_after\": %zu, \"device_memory_growth\": %lld, \"ok\": %s, \"runtime\": %s}\n",
+         "\"free_half\": %zu, \"free_after\": %zu, \"growth_first_half\": %lld, "
+         "\"growth_second_half\": %lld, \"ok\": %s, \"runtime\": %s}\n",
          seconds, (unsigned long long)steps, (unsigned long long)captures,
          (unsigned long long)replays, (unsigned long long)destroyed, (unsigned long long)bad,
-         free0, free1, grew, ok ? "true" : "false", runtime_json().c_str());
+         free0, free_half, free1, grew_first, grew_second, ok ? "true" : "false",
+         runtime_json().c_str());
   for (auto& p : pool) {
     CS_OK(tulips_csum_release_stream(p));
     HIP_OK(hipStreamDestroy(p));
