@@ -78,3 +78,18 @@ def test_native_serial_rate_on_integrator_runtime(golden):
     print(json.dumps(res, indent=1))
     assert rc == 0 and res["serial_rate"]["parity"] == "ok", (res, err)
     assert res["serial_rate"]["frac_of_8TBps"] > 0.5, res
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_native_graph_ownership_under_multibranch_churn():
+    """Graph ownership (stream_state.h) under churn on /opt/rocm's runtime:
+    multi-branch graphs of counting, arena, segmentation and fixed calls
+    (each side stream's state attaching its own user object to the graph)
+    captured, replayed on other streams (every output checked against the
+    direct calls') and destroyed, over 20 s; the second half's graphs leave
+    device memory within 4 MiB of where the first half's left it."""
+    rc, res, err = _run("graph-churn-stateful", "20", "6", timeout=240)
+    print(json.dumps(res, indent=1))
+    assert res is not None, err
+    assert rc == 0 and res["mismatches"] == 0 and res["destroyed"] > 100, (res, err)
