@@ -170,3 +170,73 @@ def test_500_captured_graphs_leave_memory_flat(oracle):
     # words, workspace): ~850 MB over 500 graphs
     assert free0 - free1 < (1 << 20), (free0, free1)
     csum.release_stream(cap.cuda_stream)
+
+
+@pytest.mark.gpu
+def test_graph_outlives_release_and_destruction_of_its_capture_stream(oracle):
+    """include/tulips_csum.h: tulips_csum_release_stream frees a stream's
+    direct arrays; graphs captured on it keep theirs. A counting call and an
+    arena call captured on a raw HIP stream, the stream released and
+    destroyed, then the graph replayed on other streams: exact every time;
+    destroying the graph afterwards returns its arrays."""
+    import torch
+    from tulips_amd import csum
+    hip = _hip()
+    rng = np.random.default_rng(77)
+    n = 6000
+    lens = rng.integers(40, 9000, n).astype(np.uint16)
+    offs = np.zeros(n, np.uint64)
+    np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+    total = int(lens.astype(np.int64).sum())
+    buf = rng.integers(0, 256, total + 16, dtype=np.uint8)
+    src = np.full(n, 0x0100010A, np.uint32)
+    dst = np.full(n, 0x0200010A, np.uint32)
+    exp_tcp = oracle.batch(buf, offs, lens, src=src, dst=dst, mode=MODE_TCP, nthreads=8)
+    exp_inet = oracle.batch(buf, offs, lens, mode=MODE_INET, nthreads=8)
+    a, o, l, ds, dd = _dev(buf, offs.astype(np.int64), lens.view(np.int16), src.view(np.int32),
+                           dst.view(np.int32))
+    out_tcp = torch.empty(n, dtype=torch.int16, device="cuda:0")
+    bad = torch.empty(1, dtype=torch.int32, device="cuda:0")
+    out_inet = torch.empty(n, dtype=torch.int16, device="cuda:0")
+    s = C.c_void_p()
+    assert hip.hipStreamCreateWithFlags(C.byref(s), 1) == 0     # hipStreamNonBlocking
+    st = s.value
+    # the stream's own (direct) arrays exist before the capture
+    assert csum.lib.tulips_csum_verify(a.data_ptr(), o.data_ptr(), l.data_ptr(), ds.data_ptr(),
+                                       dd.data_ptr(), out_tcp.data_ptr(), bad.data_ptr(), n,
+                                       MODE_TCP, st) == 0
+    torch.cuda.synchronize()
+    ext = torch.cuda.ExternalStream(st)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=ext):
+        assert csum.lib.tulips_csum_verify(a.data_ptr(), o.data_ptr(), l.data_ptr(),
+                                           ds.data_ptr(), dd.data_ptr(), out_tcp.data_ptr(),
+                                           bad.data_ptr(), n, MODE_TCP, st) == 0
+        assert csum.lib.tulips_csum_batch_arena(a.data_ptr(), total, o.data_ptr(),
+                                                l.data_ptr(), None, None, None,
+                                                out_inet.data_ptr(), n, MODE_INET, st) == 0
+    torch.cuda.synchronize()
+    assert csum.lib.tulips_csum_release_stream(st) == 0
+    del ext
+    assert hip.hipStreamDestroy(s) == 0
+    others = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for rep in range(6):
+        for t in (out_tcp, bad, out_inet):
+            t.fill_(-91)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(others[rep % 2]):
+            g.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out_tcp.cpu().numpy().view(np.uint16), exp_tcp)
+        assert int(bad.item()) == int(np.count_nonzero(exp_tcp != 0xFFFF))
+        np.testing.assert_array_equal(out_inet.cpu().numpy().view(np.uint16), exp_inet)
+    del g
+    gc.collect()
+    # the next uncaptured call reclaims what the graph held
+    assert csum.lib.tulips_csum_batch_arena(a.data_ptr(), total, o.data_ptr(), l.data_ptr(),
+                                            None, None, None, out_inet.data_ptr(), n, MODE_INET,
+                                            others[0].cuda_stream) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out_inet.cpu().numpy().view(np.uint16), exp_inet)
+    for x in others:
+        csum.release_stream(x)
