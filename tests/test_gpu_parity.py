@@ -22,7 +22,7 @@ import benchlib  # noqa: E402
 DEV = "cuda:0"
 
 SUB, PCK = csum.KIND_SUBGROUP, csum.KIND_PACKED
-# The shipped geometries (include/tulips_csum_util.h). The library's defaults
+# The shipped geometries (include/tulips_csum.h, explicit kernel geometry). The library's defaults
 # pick SUBGROUP 16x4 / 32x4 / 64x8 / 64x12 by fixed length and PACKED 8x4
 # (double-buffered) for variable lengths at any offsets.
 # (kind, group, unroll, nontemporal bits, sps)
