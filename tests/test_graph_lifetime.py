@@ -240,3 +240,129 @@ def test_graph_outlives_release_and_destruction_of_its_capture_stream(oracle):
     np.testing.assert_array_equal(out_inet.cpu().numpy().view(np.uint16), exp_inet)
     for x in others:
         csum.release_stream(x)
+
+
+@pytest.mark.gpu
+def test_first_calls_beside_a_global_mode_capture_in_another_thread(oracle):
+    """include/tulips_csum.h, per-stream state: a thread's FIRST calls on a
+    fresh stream allocate that stream's arrays (counter shards, span words,
+    segmentation workspace), and a pending reclaim frees a destroyed graph's.
+    Another thread capturing in torch's default global mode must neither
+    refuse those allocations and frees nor be broken by them (they are made
+    in relaxed capture mode). Thread A captures verify + arena + segment on
+    its stream; while the capture is open, thread B makes the same calls on a
+    new raw stream, with a destroyed graph's arrays pending; both threads'
+    results are exact and A's graph replays exactly."""
+    import torch
+    from tulips_amd import csum
+    hip = _hip()
+    rng = np.random.default_rng(4242)
+    n = 5000
+    lens = rng.integers(40, 9000, n).astype(np.uint16)
+    offs = np.zeros(n, np.uint64)
+    np.cumsum(lens[:-1], dtype=np.uint64, out=offs[1:])
+    total = int(lens.astype(np.int64).sum())
+    buf = rng.integers(0, 256, total + 16, dtype=np.uint8)
+    src = np.full(n, 0x0300010A, np.uint32)
+    dst = np.full(n, 0x0400010A, np.uint32)
+    exp_tcp = oracle.batch(buf, offs, lens, src=src, dst=dst, mode=MODE_TCP, nthreads=8)
+    exp_inet = oracle.batch(buf, offs, lens, mode=MODE_INET, nthreads=8)
+    exp_bad = int(np.count_nonzero(exp_tcp != 0xFFFF))
+    a, o, l, ds, dd = _dev(buf, offs.astype(np.int64), lens.view(np.int16), src.view(np.int32),
+                           dst.view(np.int32))
+    frames = [super_frame(oracle, rng, int(p)) for p in rng.integers(1000, 60000, 16)]
+    farena, foffs, flens = seg_pack(frames, rng)
+    mss, stride = 1460, 2048
+    efirst, eout, elens = oracle.segment_frames(farena, foffs, flens, mss, stride)
+    nseg = int(efirst[-1])
+    fa, fo, fl = _dev(farena, foffs.astype(np.int64), flens.view(np.int16))
+
+    def outputs():
+        return dict(tcp=torch.full((n,), -91, dtype=torch.int16, device="cuda:0"),
+                    bad=torch.full((1,), -91, dtype=torch.int32, device="cuda:0"),
+                    inet=torch.full((n,), -91, dtype=torch.int16, device="cuda:0"),
+                    seg=torch.full((nseg * stride,), 0x5B, dtype=torch.uint8, device="cuda:0"),
+                    seg_lens=torch.full((nseg,), -91, dtype=torch.int16, device="cuda:0"),
+                    seg_first=torch.full((len(frames) + 1,), -91, dtype=torch.int32,
+                                         device="cuda:0"))
+
+    def calls(st, x):
+        return (csum.lib.tulips_csum_verify(a.data_ptr(), o.data_ptr(), l.data_ptr(),
+                                            ds.data_ptr(), dd.data_ptr(), x["tcp"].data_ptr(),
+                                            x["bad"].data_ptr(), n, MODE_TCP, st),
+                csum.lib.tulips_csum_batch_arena(a.data_ptr(), total, o.data_ptr(), l.data_ptr(),
+                                                 None, None, None, x["inet"].data_ptr(), n,
+                                                 MODE_INET, st),
+                csum.lib.tulips_csum_segment_frames(fa.data_ptr(), fo.data_ptr(), fl.data_ptr(),
+                                                    len(frames), mss, x["seg"].data_ptr(), stride,
+                                                    nseg, x["seg_lens"].data_ptr(),
+                                                    x["seg_first"].data_ptr(), st))
+
+    def check(x, who):
+        np.testing.assert_array_equal(x["tcp"].cpu().numpy().view(np.uint16), exp_tcp, who)
+        assert int(x["bad"].item()) == exp_bad, who
+        np.testing.assert_array_equal(x["inet"].cpu().numpy().view(np.uint16), exp_inet, who)
+        np.testing.assert_array_equal(x["seg_first"].cpu().numpy().view(np.uint32), efirst, who)
+        got_lens = x["seg_lens"].cpu().numpy().view(np.uint16)
+        np.testing.assert_array_equal(got_lens, elens, who)
+        got = x["seg"].cpu().numpy().reshape(nseg, stride)
+        want = eout.reshape(nseg, stride)
+        for k in range(nseg):
+            assert np.array_equal(got[k, :elens[k]], want[k, :elens[k]]), (who, k)
+
+    # a destroyed graph's arrays pending reclaim when thread B makes its calls
+    pend = torch.cuda.Stream()
+    x_pend = outputs()
+    g0 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g0, stream=pend):
+        assert calls(pend.cuda_stream, x_pend) == (0, 0, 0)
+    g0.replay()
+    torch.cuda.synchronize()
+    check(x_pend, "pending graph")
+    del g0
+    gc.collect()
+
+    cap = torch.cuda.Stream()
+    sb = C.c_void_p()
+    assert hip.hipStreamCreateWithFlags(C.byref(sb), 1) == 0       # hipStreamNonBlocking
+    x_a, x_b = outputs(), outputs()
+    torch.cuda.synchronize()
+    go, done = threading.Event(), threading.Event()
+    rc_b = []
+
+    def thread_b():
+        go.wait(60)
+        try:
+            rc_b.append(calls(sb.value, x_b))
+        finally:
+            done.set()
+
+    tb = threading.Thread(target=thread_b)
+    tb.start()
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g, stream=cap):                     # global capture mode
+            rc_a = calls(cap.cuda_stream, x_a)
+            go.set()
+            assert done.wait(60), "thread B did not finish"
+    finally:
+        go.set()
+        tb.join(60)
+    assert rc_a == (0, 0, 0)
+    assert rc_b == [(0, 0, 0)], f"B's calls beside the capture returned {rc_b}"
+    torch.cuda.synchronize()
+    assert hip.hipStreamSynchronize(sb) == 0
+    check(x_b, "thread B (direct, beside the capture)")
+    for rep in range(3):
+        for t in x_a.values():
+            t.fill_(-91 if t.dtype != torch.uint8 else 0x5B)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        check(x_a, f"thread A's graph, replay {rep}")
+    del g
+    gc.collect()
+    assert csum.lib.tulips_csum_release_stream(sb.value) == 0
+    assert hip.hipStreamDestroy(sb) == 0
+    csum.release_stream(cap.cuda_stream)
+    csum.release_stream(pend.cuda_stream)

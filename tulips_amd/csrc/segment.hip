@@ -717,7 +717,7 @@ segment_planned_kernel(const uint8_t* base, const uint64_t* __restrict__ offs,
 // under the graph nor race a replay on it. The caller holds the stream's call
 // mutex.
 hipError_t
-ws_alloc(int device, bool capturing, uint64_t nruns, uint64_t ndesc, StreamState::SegWs* w,
+ws_alloc(int device, uint64_t nruns, uint64_t ndesc, StreamState::SegWs* w,
          std::vector<void*>* made)
 {
   struct Part
@@ -733,7 +733,7 @@ ws_alloc(int device, bool capturing, uint64_t nruns, uint64_t ndesc, StreamState
     if (*q.p) {
       continue;
     }
-    const hipError_t e = device_malloc_in_capture(device, capturing, q.p, q.bytes);
+    const hipError_t e = device_malloc(device, q.p, q.bytes);
     if (e != hipSuccess) {
       *q.p = nullptr;
       return e;
@@ -762,7 +762,7 @@ workspace(StreamState& s, bool capturing, uint32_t capacity, uint32_t n,
       // of this capture stays with the calls recorded on it)
       StreamState::SegWs fresh;
       std::vector<void*> made;
-      const hipError_t e = ws_alloc(s.device, true, need_runs ? need_runs : 1,
+      const hipError_t e = ws_alloc(s.device, need_runs ? need_runs : 1,
                                     need_desc ? need_desc : 1, &fresh, &made);
       capture_keep(s, made);
       if (e != hipSuccess) {
@@ -785,31 +785,17 @@ workspace(StreamState& s, bool capturing, uint32_t capacity, uint32_t n,
       std::vector<void*> made;
       const uint64_t nr = std::max<uint64_t>(std::max<uint64_t>(need_runs, 65536), w->nruns);
       const uint64_t nd = std::max<uint64_t>(std::max<uint64_t>(need_desc, 65536), w->ndesc);
-      hipError_t e = ws_alloc(s.device, false, grown.runs ? w->nruns : nr,
+      hipError_t e = ws_alloc(s.device, grown.runs ? w->nruns : nr,
                               grown.desc ? w->ndesc : nd, &grown, &made);
       if (e == hipSuccess) {
-        e = hipStreamSynchronize(s.stream); // the arrays replaced are idle
+        e = sync_stream(s.stream); // the arrays replaced are idle
       }
       if (e != hipSuccess) {
-        int prev = 0;
-        (void)hipGetDevice(&prev);
-        (void)hipSetDevice(s.device);
-        for (void* p : made) {
-          (void)hipFree(p);
-        }
-        (void)hipSetDevice(prev);
+        device_free(s.device, made);
         return e;
       }
-      int prev = 0;
-      (void)hipGetDevice(&prev);
-      (void)hipSetDevice(s.device);
-      if (grown.runs != w->runs) {
-        (void)hipFree(w->runs);
-      }
-      if (grown.desc != w->desc) {
-        (void)hipFree(w->desc);
-      }
-      (void)hipSetDevice(prev);
+      device_free(s.device, { grown.runs != w->runs ? w->runs : nullptr,
+                              grown.desc != w->desc ? w->desc : nullptr });
       *w = grown;
     }
   }

@@ -138,11 +138,19 @@ hipError_t span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** 
 // partial sums, so the stream gets fresh zeroed ones on its next call.
 void drop_shards(StreamState& s, uint32_t* shards);
 
-// hipMalloc on `device` (restores the caller's current device).
+// hipMalloc / hipFree on `device` (restoring the caller's current device),
+// with the thread's capture mode relaxed around them: inside a capture the
+// allocation is the graph's (capture_keep), and outside one it must not be
+// refused, nor break the capture, because ANOTHER thread is capturing in
+// global mode (torch.cuda.graph's default) — what the library allocates or
+// frees is never used by that capture.
 hipError_t device_malloc(int device, void** p, size_t bytes);
+void device_free(int device, const std::vector<void*>& ps);
 
-// hipMalloc on `device` from inside a capture: the thread's capture mode is
-// relaxed around the allocation (plain device_malloc when not capturing).
-hipError_t device_malloc_in_capture(int device, bool capturing, void** p, size_t bytes);
+// hipStreamSynchronize, in relaxed capture mode for the same reason: on both
+// runtimes a global-mode sync (like a global-mode hipMalloc / hipFree) from
+// one thread invalidates another thread's global-mode capture
+// (tools/probe_capture_modes.py, profiles/capture_modes_r06o.jsonl).
+hipError_t sync_stream(hipStream_t stream);
 
 } // namespace tulips_amd

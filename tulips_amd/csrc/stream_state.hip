@@ -50,19 +50,16 @@ stream_device(hipStream_t stream, int* dev)
   return hipSuccess;
 }
 
-void
-free_on(int device, const std::vector<void*>& ps)
+// The thread's capture mode, relaxed for the guard's scope (stream_state.h,
+// device_malloc).
+struct RelaxedCapture
 {
-  int prev = 0;
-  (void)hipGetDevice(&prev);
-  (void)hipSetDevice(device);
-  for (void* p : ps) {
-    if (p) {
-      (void)hipFree(p);
-    }
-  }
-  (void)hipSetDevice(prev);
-}
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&mode); }
+  ~RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&mode); }
+  RelaxedCapture(const RelaxedCapture&) = delete;
+  RelaxedCapture& operator=(const RelaxedCapture&) = delete;
+};
 
 // Zeroes words [0, n) of p (a kernel: inside a capture it is a kernel node
 // of the graph, which a captured hipMemsetAsync on an array allocated in the
@@ -101,7 +98,7 @@ zeroed_words(StreamState& s, uint64_t words, bool capturing, uint64_t** out)
 {
   *out = nullptr;
   void* p = nullptr;
-  hipError_t e = device_malloc_in_capture(s.device, capturing, &p, sizeof(uint64_t) * words);
+  hipError_t e = device_malloc(s.device, &p, sizeof(uint64_t) * words);
   if (e != hipSuccess) {
     return e;
   }
@@ -111,8 +108,8 @@ zeroed_words(StreamState& s, uint64_t words, bool capturing, uint64_t** out)
   e = launch_zero_words(static_cast<uint64_t*>(p), words, s.stream);
   if (e != hipSuccess) {
     if (!capturing) {
-      (void)hipStreamSynchronize(s.stream);
-      free_on(s.device, std::vector<void*>{ p });
+      (void)sync_stream(s.stream);
+      device_free(s.device, std::vector<void*>{ p });
     }
     return e;
   }
@@ -125,6 +122,7 @@ zeroed_words(StreamState& s, uint64_t words, bool capturing, uint64_t** out)
 hipError_t
 device_malloc(int device, void** p, size_t bytes)
 {
+  *p = nullptr;
   int prev = 0;
   hipError_t e = hipGetDevice(&prev);
   if (e != hipSuccess) {
@@ -133,26 +131,38 @@ device_malloc(int device, void** p, size_t bytes)
   if (prev != device && (e = hipSetDevice(device)) != hipSuccess) {
     return e;
   }
-  *p = nullptr;
-  e = hipMalloc(p, bytes);
+  {
+    RelaxedCapture relaxed;
+    e = hipMalloc(p, bytes);
+  }
   if (prev != device) {
     (void)hipSetDevice(prev);
   }
   return e;
 }
 
-hipError_t
-device_malloc_in_capture(int device, bool capturing, void** p, size_t bytes)
+void
+device_free(int device, const std::vector<void*>& ps)
 {
-  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-  if (capturing) {
-    (void)hipThreadExchangeStreamCaptureMode(&mode);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(device);
+  {
+    RelaxedCapture relaxed;
+    for (void* p : ps) {
+      if (p) {
+        (void)hipFree(p);
+      }
+    }
   }
-  const hipError_t e = device_malloc(device, p, bytes);
-  if (capturing) {
-    (void)hipThreadExchangeStreamCaptureMode(&mode);
-  }
-  return e;
+  (void)hipSetDevice(prev);
+}
+
+hipError_t
+sync_stream(hipStream_t stream)
+{
+  RelaxedCapture relaxed;
+  return hipStreamSynchronize(stream);
 }
 
 void
@@ -167,15 +177,12 @@ reclaim_graph_arrays()
     todo.swap(*g_reclaim);
     g_reclaim_n.store(0, std::memory_order_relaxed);
   }
-  // another thread may be capturing in global mode: this thread's frees are
-  // allowed by its relaxed mode (the graphs that used them are gone)
-  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  // another thread may be capturing in global mode: device_free's relaxed
+  // mode allows these frees (the graphs that used them are gone)
   for (GraphArrays* a : todo) {
-    free_on(a->device, a->ptrs);
+    device_free(a->device, a->ptrs);
     delete a;
   }
-  (void)hipThreadExchangeStreamCaptureMode(&mode);
 }
 
 hipError_t
@@ -277,7 +284,7 @@ call_shards(StreamState& s, bool capturing, uint32_t** out)
     void* p = nullptr;
     hipError_t e = device_malloc(s.device, &p, SHARD_BYTES);
     if (e == hipSuccess && (e = hipMemsetAsync(p, 0, SHARD_BYTES, s.stream)) != hipSuccess) {
-      free_on(s.device, std::vector<void*>{ p });
+      device_free(s.device, std::vector<void*>{ p });
     }
     if (e != hipSuccess) {
       return e;
@@ -297,13 +304,13 @@ span_slots(StreamState& s, bool capturing, uint64_t need, uint64_t** out, uint64
       const uint64_t want = need < 4096 ? 4096 : need;
       uint64_t* made = nullptr;
       hipError_t e = zeroed_words(s, want, false, &made);
-      if (e == hipSuccess && (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
-        free_on(s.device, std::vector<void*>{ made });
+      if (e == hipSuccess && (e = sync_stream(s.stream)) != hipSuccess) {
+        device_free(s.device, std::vector<void*>{ made });
       }
       if (e != hipSuccess) {
         return e;
       }
-      free_on(s.device, std::vector<void*>{ s.span_slots }); // idle: the stream synchronised
+      device_free(s.device, std::vector<void*>{ s.span_slots }); // idle: the stream synchronised
       s.span_slots = made;
       s.span_nslots = want;
     }
@@ -380,7 +387,7 @@ tulips_csum_release_stream(void* stream)
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(s->device);
-    if (hipStreamSynchronize(st) != hipSuccess) {
+    if (sync_stream(st) != hipSuccess) {
       (void)hipGetLastError();
     }
     (void)hipSetDevice(prev);
@@ -394,7 +401,7 @@ tulips_csum_release_stream(void* stream)
     ps.push_back(s->seg.desc);
     ps.push_back(s->span_slots);
     for (auto* p : s->orphans) ps.push_back(p);
-    free_on(s->device, ps);
+    device_free(s->device, ps);
     s->shards = nullptr;
     s->retired.clear();
     s->seg = StreamState::SegWs();
