@@ -620,7 +620,10 @@ int tulips_csum_frames_tuned(int op, uint8_t* base, const uint64_t* offsets,
  * tulips_csum_segment_frames keep a small device workspace per (device,
  * stream), on the stream's own device. A call holds the stream's lock from
  * its first launch to its last, so host threads sharing a stream (e.g. the
- * NULL stream) never interleave their launch sequences.
+ * NULL stream) never interleave their launch sequences. The workspace is
+ * allocated, freed and waited for in relaxed capture mode, so these calls
+ * may run beside another thread's global-mode stream capture without
+ * invalidating it.
  *
  * A call captured in a HIP graph (stream capture) runs on arrays made for
  * that capture, so no warm-up call is needed and replays never share arrays
