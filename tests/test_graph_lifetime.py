@@ -249,10 +249,12 @@ def test_first_calls_beside_a_global_mode_capture_in_another_thread(oracle):
     segmentation workspace), and a pending reclaim frees a destroyed graph's.
     Another thread capturing in torch's default global mode must neither
     refuse those allocations and frees nor be broken by them (they are made
-    in relaxed capture mode). Thread A captures verify + arena + segment on
+    in relaxed capture mode), and neither may the host-buffer contexts'
+    staging, streams and waits. Thread A captures verify + arena + segment on
     its stream; while the capture is open, thread B makes the same calls on a
-    new raw stream, with a destroyed graph's arrays pending; both threads'
-    results are exact and A's graph replays exactly."""
+    new raw stream, with a destroyed graph's arrays pending, then creates,
+    uses and destroys a host context and a two-entry multi-device context;
+    every result is exact and A's graph replays exactly."""
     import torch
     from tulips_amd import csum
     hip = _hip()
@@ -330,10 +332,20 @@ def test_first_calls_beside_a_global_mode_capture_in_another_thread(oracle):
     go, done = threading.Event(), threading.Event()
     rc_b = []
 
+    host_b = {}
+
     def thread_b():
         go.wait(60)
         try:
             rc_b.append(calls(sb.value, x_b))
+            # the host-buffer contexts (pinned staging, their own streams and,
+            # for the multi-device one, worker threads) made, used and freed
+            with csum.HostContext(0) as hc:
+                host_b["ctx"] = hc.batch(buf, offs, lens, src=src, dst=dst, mode=MODE_TCP)
+            with csum.MultiContext([0, 0]) as m:
+                host_b["mctx"] = m.batch(buf, offs, lens, src=src, dst=dst, mode=MODE_TCP)
+        except Exception as e:                                   # reported below
+            host_b["error"] = repr(e)
         finally:
             done.set()
 
@@ -350,6 +362,9 @@ def test_first_calls_beside_a_global_mode_capture_in_another_thread(oracle):
         tb.join(60)
     assert rc_a == (0, 0, 0)
     assert rc_b == [(0, 0, 0)], f"B's calls beside the capture returned {rc_b}"
+    assert "error" not in host_b, host_b.get("error")
+    np.testing.assert_array_equal(host_b["ctx"], exp_tcp)
+    np.testing.assert_array_equal(host_b["mctx"], exp_tcp)
     torch.cuda.synchronize()
     assert hip.hipStreamSynchronize(sb) == 0
     check(x_b, "thread B (direct, beside the capture)")

@@ -532,12 +532,14 @@ extern "C" {
 int
 tulips_csum_ctx_create(int device, uint64_t chunk_bytes, tulips_csum_ctx** ctx)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   return tulips_amd::ctx_create(device, chunk_bytes, pack_threads(), ctx);
 }
 
 int
 tulips_csum_ctx_destroy(tulips_csum_ctx* ctx)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!ctx) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -708,6 +710,7 @@ extern "C" {
 int
 tulips_csum_host_alloc(size_t bytes, void** ptr)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!ptr || bytes == 0) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -718,6 +721,7 @@ tulips_csum_host_alloc(size_t bytes, void** ptr)
 int
 tulips_csum_host_free(void* ptr)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   return ptr ? status_of(hipHostFree(ptr)) : TULIPS_STATUS_OK;
 }
 
@@ -728,6 +732,7 @@ tulips_csum_batch_host(tulips_csum_ctx* ctx, const uint8_t* base,
                        const uint32_t* dst, uint16_t* out, uint32_t n,
                        uint32_t mode)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!ctx) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -755,6 +760,7 @@ tulips_csum_validate_frames_host(tulips_csum_ctx* ctx, const uint8_t* base,
                                  const uint16_t* lengths, uint32_t n,
                                  uint8_t* flags, uint32_t* counters)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!ctx) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -1031,6 +1037,7 @@ zc_validate(tulips_csum_ctx* ctx, const uint8_t* base, const uint64_t* offsets,
 extern "C" int
 tulips_csum_ctx_set_lowlat(tulips_csum_ctx* ctx, int resident)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!ctx || (resident != 0 && resident != 1)) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -1050,6 +1057,7 @@ tulips_csum_validate_frames_zc(tulips_csum_ctx* ctx, const uint8_t* base,
                                const uint64_t* offsets, const uint16_t* lengths, uint32_t n,
                                uint8_t* flags, uint32_t* counters)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!ctx) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -1192,6 +1200,7 @@ tulips_csum_generate_frames_host(tulips_csum_ctx* ctx, uint8_t* base,
                                  const uint64_t* offsets, const uint16_t* lengths,
                                  uint32_t n, uint8_t* flags)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!ctx) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -1218,6 +1227,7 @@ tulips_csum_segment_frames_host(tulips_csum_ctx* ctx, const uint8_t* in_base,
                                 uint64_t out_stride, uint32_t out_capacity,
                                 uint16_t* out_lengths, uint32_t* out_first)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!ctx || !out_first || mss == 0 || mss > 0xffffu) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }

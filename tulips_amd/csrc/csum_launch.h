@@ -7,6 +7,21 @@
 
 namespace tulips_amd {
 
+// The calling thread's stream-capture mode, relaxed for the guard's scope.
+// In global mode (the default) a hipMalloc, hipFree or hipStreamSynchronize
+// from any thread invalidates every other thread's global-mode capture
+// (tools/probe_capture_modes.py, profiles/capture_modes_r06o.jsonl); the
+// library's own allocations, frees and waits never touch such a capture, so
+// they are made relaxed.
+struct RelaxedCapture
+{
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&mode); }
+  ~RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&mode); }
+  RelaxedCapture(const RelaxedCapture&) = delete;
+  RelaxedCapture& operator=(const RelaxedCapture&) = delete;
+};
+
 struct LaunchArgs
 {
   const uint16_t* seeds; // nullable

@@ -90,6 +90,10 @@ public:
 private:
   void loop(int k)
   {
+    // the library's own thread: every HIP call it makes is the library's
+    // (allocations, copies, waits on the context's streams)
+    hipStreamCaptureMode relaxed = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&relaxed);
     uint64_t seen = 0;
     for (;;) {
       const std::function<void(int)>* f;
@@ -236,6 +240,7 @@ int
 tulips_csum_mctx_create(const int* devices, uint32_t ndevices, uint64_t chunk_bytes,
                         tulips_csum_mctx** out)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!out || !devices || ndevices == 0 || ndevices > 64) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -272,6 +277,7 @@ tulips_csum_mctx_create(const int* devices, uint32_t ndevices, uint64_t chunk_by
 int
 tulips_csum_mctx_destroy(tulips_csum_mctx* m)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!m) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -408,6 +414,7 @@ tulips_csum_mctx_batch_host(tulips_csum_mctx* m, const uint8_t* base,
                             const uint32_t* dst, uint16_t* out, uint32_t n,
                             uint32_t mode)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!m) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -429,6 +436,7 @@ tulips_csum_mctx_validate_frames_host(tulips_csum_mctx* m, const uint8_t* base,
                                       const uint64_t* offsets, const uint16_t* lengths,
                                       uint32_t n, uint8_t* flags, uint32_t* counters)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!m) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -466,6 +474,7 @@ tulips_csum_mctx_validate_frames_rss_host(tulips_csum_mctx* m, const uint8_t* ba
                                           uint32_t table_len, uint8_t* flags,
                                           uint32_t* counters, uint16_t* device_of)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (!m || !key || key_len < 4 || !table || table_len == 0) {
     return TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -1149,6 +1158,7 @@ tulips_csum_mctx_batch_fixed_device(tulips_csum_mctx* m, const uint8_t* base, ui
                                     const uint32_t* src, const uint32_t* dst, uint16_t* out,
                                     uint32_t n, uint32_t mode, void* stream)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (n == 0) {
     return m ? TULIPS_STATUS_OK : TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -1197,6 +1207,7 @@ tulips_csum_mctx_batch_arena_device(tulips_csum_mctx* m, const uint8_t* base,
                                     const uint32_t* src, const uint32_t* dst, uint16_t* out,
                                     uint32_t n, uint32_t mode, void* stream)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   if (n == 0) {
     return m ? TULIPS_STATUS_OK : TULIPS_STATUS_INVALID_ARGUMENT;
   }
@@ -1586,6 +1597,7 @@ tulips_csum_mctx_validate_frames_rss_device(tulips_csum_mctx* m, const uint8_t* 
                                             uint32_t* counters, uint16_t* device_of,
                                             void* stream)
 {
+  tulips_amd::RelaxedCapture relaxed; // beside other threads' captures
   tulips_amd::RouteWindows win;
   if (!m || !table || table_len == 0 || table_len > 65536 ||
       !rss_route_windows(key, key_len, &win)) {

@@ -50,17 +50,6 @@ stream_device(hipStream_t stream, int* dev)
   return hipSuccess;
 }
 
-// The thread's capture mode, relaxed for the guard's scope (stream_state.h,
-// device_malloc).
-struct RelaxedCapture
-{
-  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-  RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&mode); }
-  ~RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&mode); }
-  RelaxedCapture(const RelaxedCapture&) = delete;
-  RelaxedCapture& operator=(const RelaxedCapture&) = delete;
-};
-
 // Zeroes words [0, n) of p (a kernel: inside a capture it is a kernel node
 // of the graph, which a captured hipMemsetAsync on an array allocated in the
 // capture did not reliably become).
