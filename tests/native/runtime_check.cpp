@@ -36,6 +36,15 @@
 //       the fixed-stride kernel's one-launch-at-a-time rate on this runtime
 //       (NBATCH rotated batches of 65,536 x L bytes, a captured chain of 256
 //       launches, HIP events, median of 5), batch 0 checked against FNV.
+//   runtime_check capture-neutral F1500=FNV ZIPF=FNV ZIPF-tcp=FNV
+//       the library beside another thread's global-mode capture: thread A
+//       captures a fixed-stride F1500 call (hipStreamCaptureModeGlobal);
+//       while the capture is open thread B makes first calls on a fresh
+//       stream (counting verify_arena and batch_arena over ZIPF, which
+//       allocate that stream's state and synchronise it) and creates, uses
+//       and destroys a host context and a two-entry multi-device context over
+//       F1500 host bytes. A's capture must survive and replay to F1500's
+//       digest; every B result must equal its digest.
 //   runtime_check graph-churn SECONDS SEED
 //       the multi-branch capture/replay/destroy churn that faults inside
 //       the runtime torch bundles, on this runtime, with
@@ -302,6 +311,133 @@ cmd_parity(int argc, char** argv)
   (void)hipFree(d_zoffs);
   (void)hipFree(d_zlens);
   return bad ? 1 : 0;
+}
+
+// ---- capture-mode neutrality -------------------------------------------------------
+int
+cmd_capture_neutral(int argc, char** argv)
+{
+  std::map<std::string, std::string> want;
+  for (int i = 0; i < argc; ++i) {
+    const char* eq = strchr(argv[i], '=');
+    if (!eq) {
+      fprintf(stderr, "expected NAME=FNV, got %s\n", argv[i]);
+      return 2;
+    }
+    want[std::string(argv[i], size_t(eq - argv[i]))] = eq + 1;
+  }
+  const std::vector<uint16_t> zl = zipf_lengths(NSEG);
+  uint64_t ztotal = 0;
+  std::vector<uint64_t> zoffs(NSEG);
+  for (uint32_t i = 0; i < NSEG; ++i) {
+    zoffs[i] = ztotal;
+    ztotal += zl[i];
+  }
+  const uint64_t nbytes = uint64_t(NSEG) * 1500;
+  std::vector<uint8_t> host(std::max<uint64_t>(nbytes, ztotal) + 64, 0);
+  splitmix_fill(host.data(), host.size() - 64);
+  uint8_t* arena = to_device(host);
+  const std::vector<uint32_t> hsrc(NSEG, ip4(10, 1, 0, 1)), hdst(NSEG, ip4(10, 1, 0, 2));
+  uint32_t* src = to_device(hsrc);
+  uint32_t* dst = to_device(hdst);
+  uint64_t* d_zoffs = to_device(zoffs);
+  uint16_t* d_zlens = to_device(zl);
+  std::vector<uint64_t> foffs(NSEG);
+  for (uint32_t i = 0; i < NSEG; ++i) {
+    foffs[i] = uint64_t(i) * 1500;
+  }
+  const std::vector<uint16_t> flens(NSEG, 1500);
+  uint16_t *out_a = nullptr, *out_v = nullptr, *out_z = nullptr;
+  uint32_t* bad = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&out_a), NSEG * 2));
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&out_v), NSEG * 2));
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&out_z), NSEG * 2));
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&bad), 16));
+  hipStream_t sa = nullptr, sb = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+  HIP_OK(hipDeviceSynchronize());
+
+  std::atomic<int> stage{ 0 };
+  int rc_v = -1, rc_z = -1, rc_ctx = -1, rc_mctx = -1;
+  std::vector<uint16_t> h_ctx(NSEG, 0xA5A5), h_mctx(NSEG, 0xA5A5);
+  std::thread tb([&] {
+    while (stage.load() < 1) {
+      std::this_thread::yield();
+    }
+    rc_v = tulips_csum_verify_arena(arena, ztotal, d_zoffs, d_zlens, src, dst, out_v, bad, NSEG,
+                                    TULIPS_CSUM_TCP, sb);
+    rc_z = tulips_csum_batch_arena(arena, ztotal, d_zoffs, d_zlens, nullptr, nullptr, nullptr,
+                                   out_z, NSEG, TULIPS_CSUM_RAW, sb);
+    tulips_csum_ctx* ctx = nullptr;
+    rc_ctx = tulips_csum_ctx_create(0, 0, &ctx);
+    if (rc_ctx == TULIPS_STATUS_OK) {
+      rc_ctx = tulips_csum_batch_host(ctx, host.data(), foffs.data(), flens.data(), nullptr,
+                                      nullptr, nullptr, h_ctx.data(), NSEG, TULIPS_CSUM_RAW);
+      tulips_csum_ctx_destroy(ctx);
+    }
+    const int devs[2] = { 0, 0 };
+    tulips_csum_mctx* m = nullptr;
+    rc_mctx = tulips_csum_mctx_create(devs, 2, 0, &m);
+    if (rc_mctx == TULIPS_STATUS_OK) {
+      rc_mctx = tulips_csum_mctx_batch_host(m, host.data(), foffs.data(), flens.data(), nullptr,
+                                            nullptr, nullptr, h_mctx.data(), NSEG,
+                                            TULIPS_CSUM_RAW);
+      tulips_csum_mctx_destroy(m);
+    }
+    stage.store(2);
+  });
+  HIP_OK(hipStreamBeginCapture(sa, hipStreamCaptureModeGlobal));
+  const int rc_a = tulips_csum_batch_fixed(arena, 1500, 1500, nullptr, nullptr, nullptr, out_a,
+                                           NSEG, TULIPS_CSUM_RAW, sa);
+  stage.store(1);
+  while (stage.load() < 2) {
+    std::this_thread::yield();
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(sa, &cs);
+  hipGraph_t g = nullptr;
+  const hipError_t e_end = hipStreamEndCapture(sa, &g);
+  tb.join();
+  (void)hipGetLastError();
+  bool replay_ok = false;
+  std::string d_a;
+  if (e_end == hipSuccess && g) {
+    hipGraphExec_t x = nullptr;
+    HIP_OK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+    HIP_OK(hipMemsetAsync(out_a, 0xA5, NSEG * 2, sa));
+    HIP_OK(hipGraphLaunch(x, sa));
+    HIP_OK(hipStreamSynchronize(sa));
+    d_a = hex64(fnv1a_u16(to_host(out_a, NSEG)));
+    replay_ok = d_a == want["F1500"];
+    HIP_OK(hipGraphExecDestroy(x));
+    HIP_OK(hipGraphDestroy(g));
+  }
+  HIP_OK(hipStreamSynchronize(sb));
+  const std::string d_v = hex64(fnv1a_u16(to_host(out_v, NSEG)));
+  const std::string d_z = hex64(fnv1a_u16(to_host(out_z, NSEG)));
+  const std::string d_ctx = hex64(fnv1a_u16(h_ctx)), d_mctx = hex64(fnv1a_u16(h_mctx));
+  const bool ok = rc_a == 0 && cs == hipStreamCaptureStatusActive && e_end == hipSuccess &&
+                  replay_ok && rc_v == 0 && rc_z == 0 && rc_ctx == 0 && rc_mctx == 0 &&
+                  d_v == want["ZIPF-tcp"] && d_z == want["ZIPF"] && d_ctx == want["F1500"] &&
+                  d_mctx == want["F1500"];
+  printf("{\"capture_neutral\": {\"capture_status_after_b\": %d, \"end_capture\": %d, "
+         "\"replay_F1500\": \"%s\", \"b_rc\": [%d, %d, %d, %d], \"b_verify_arena_tcp\": \"%s\", "
+         "\"b_batch_arena\": \"%s\", \"b_ctx_host\": \"%s\", \"b_mctx_host\": \"%s\", "
+         "\"ok\": %s}, \"runtime\": %s}\n",
+         int(cs), int(e_end), d_a.c_str(), rc_v, rc_z, rc_ctx, rc_mctx, d_v.c_str(), d_z.c_str(),
+         d_ctx.c_str(), d_mctx.c_str(), ok ? "true" : "false", runtime_json().c_str());
+  CS_OK(tulips_csum_release_stream(sa));
+  CS_OK(tulips_csum_release_stream(sb));
+  HIP_OK(hipStreamDestroy(sa));
+  HIP_OK(hipStreamDestroy(sb));
+  for (void* q : { static_cast<void*>(arena), static_cast<void*>(src), static_cast<void*>(dst),
+                   static_cast<void*>(d_zoffs), static_cast<void*>(d_zlens),
+                   static_cast<void*>(out_a), static_cast<void*>(out_v),
+                   static_cast<void*>(out_z), static_cast<void*>(bad) }) {
+    (void)hipFree(q);
+  }
+  return ok ? 0 : 1;
 }
 
 // ---- user objects ---------------------------------------------------------------
@@ -1230,6 +1366,9 @@ main(int argc, char** argv)
   }
   if (cmd == "parity") {
     return cmd_parity(argc - 2, argv + 2);
+  }
+  if (cmd == "capture-neutral") {
+    return cmd_capture_neutral(argc - 2, argv + 2);
   }
   if (cmd == "user-object") {
     return cmd_user_object();

@@ -93,3 +93,19 @@ def test_native_graph_ownership_under_multibranch_churn():
     print(json.dumps(res, indent=1))
     assert res is not None, err
     assert rc == 0 and res["mismatches"] == 0 and res["destroyed"] > 100, (res, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_native_calls_beside_a_global_mode_capture(golden):
+    """include/tulips_csum.h, per-stream state, on /opt/rocm's runtime: first
+    calls on a fresh stream (verify_arena, batch_arena) and a host and a
+    multi-device context made, used and destroyed by one thread while another
+    holds a global-mode capture open; the capture survives and replays to
+    F1500's digest, and every result equals the reference digests."""
+    b = golden.digests()["batches"]
+    want = [f"{k}={b[k]['fnv1a64']}" for k in ("F1500", "ZIPF", "ZIPF-tcp")]
+    rc, res, err = _run("capture-neutral", *want, timeout=240)
+    print(json.dumps(res, indent=1))
+    assert res is not None, err
+    assert rc == 0 and res["capture_neutral"]["ok"], (res, err)
