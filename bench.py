@@ -65,6 +65,7 @@ def parse():
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal only: every rank uses cuda:0 (use with gloo)")
     p.add_argument("--extras-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--mctx-child", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--streams", type=int, default=0,
                    help="independent graph branches the timed steps round-robin over "
                         "(batches are independent). 0 = by step count (branches_for): "
@@ -330,6 +331,8 @@ def main():
     START_DELAY_US = max(0, args.start_delay_us)
     if args.extras_child:
         return extras_child()
+    if args.mctx_child:
+        return mctx_child(args.mctx_child, args.one_device)
     if args.streams <= 0:
         args.streams = branches_for(args.steps)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -880,59 +883,88 @@ def mctx_device_leg(torch, dist, csum, cdev, rank, world, args):
     whole world x 1,048,576 x 1500 B batch (at N = 8: M8x1500, 12.6 GB) in
     GPU 0's HBM and spreads it over every GPU of the node from one process -
     each peer pulls its ~32 MiB pieces over xGMI while checksumming the
-    previous ones, results come back to GPU 0 in segment order. The other
-    ranks wait at a barrier. Timed end to end on GPU 0's stream (best of 3;
+    previous ones, results come back to GPU 0 in segment order. Rank 0 runs
+    it in a child process (bench.py --mctx-child: one process driving every
+    device, as an integrator's would), so that a failure on real peers - an
+    exception or a crash - costs this entry, never the line; the other ranks
+    wait at a barrier. Timed end to end on GPU 0's stream (best of 3;
     exchange-inclusive). Parity: every shard's digest equals the reference's
     M8 shard digest, and at N = 8 the whole batch's digest equals M8x1500's."""
-    from tulips_amd.shard import SHARD_SEGMENTS, gather_strings
-    devs = [0] * world if args.one_device else list(range(world))
+    from tulips_amd.shard import gather_strings
     res = {}
     if rank == 0:
         # rank 0 alone works here: an error must still reach the barrier below,
         # or the other ranks would meet rank 0's next collective there
+        import subprocess
+        cmd = [sys.executable, "-u", os.path.abspath(__file__), "--mctx-child", str(world)]
+        if args.one_device:
+            cmd.append("--one-device")
         try:
-            n = world * SHARD_SEGMENTS
-            d0 = torch.device("cuda", 0)
-            with torch.cuda.device(d0):
-                arena = torch.empty(n * SEG + 64, dtype=torch.uint8, device=d0)
-                _bench().fill_splitmix(arena, n * SEG, seed=DATA_SEED)
-                out = torch.empty(n, dtype=torch.uint16, device=d0)
-                st = torch.cuda.current_stream(d0)
-                with csum.MultiContext(devs, chunk_bytes=1 << 20) as m:
-                    m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)   # buffers made
-                    st.synchronize()
-                    best = None
-                    for _ in range(3):
-                        st.synchronize()
-                        t0 = time.perf_counter()
-                        m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)
-                        st.synchronize()
-                        t = time.perf_counter() - t0
-                        best = t if best is None else min(best, t)
-                    bounds = m.bounds().tolist()
-                o = out.cpu().numpy().view(np.uint16)
-            gold = golden_digests().get("M8x1500", {})
-            shards = gold.get("shards", [])
-            ok = all(fnv1a_u16(o[k * SHARD_SEGMENTS:(k + 1) * SHARD_SEGMENTS]) ==
-                     shards[k]["fnv1a64"] for k in range(min(world, len(shards))))
-            if world == 8:
-                ok = ok and fnv1a_u16(o) == gold.get("fnv1a64")
-            nbytes = float(n) * SEG
-            res = {"entry": "tulips_csum_mctx_batch_fixed_device (one process, devices "
-                            f"{devs})",
-                   "workload": f"{n:,} x 1500 B resident on GPU 0 ({nbytes / 1e9:.2f} GB)",
-                   "bytes_pulled_by_peers": int(nbytes * (world - 1) / world),
-                   "ms": round(best * 1e3, 3),
-                   "value_exchange_inclusive_GiBps": round(nbytes / best / GIB, 2),
-                   "shard_bounds": bounds,
-                   "parity": "ok" if ok else "MISMATCH"}
-            del arena, out
-            res["kernel_only"] = single_process_kernel_only(torch, csum, devs)
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                               cwd=ROOT, timeout=600)
+            lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            if r.returncode == 0 and lines:
+                res = json.loads(lines[-1])["mctx"]
+            else:
+                sys.stderr.write(r.stderr[-4000:])
+                res = {"error": f"mctx process exited with status {r.returncode}",
+                       "stderr_tail": r.stderr[-1500:]}
         except Exception as e:  # noqa: BLE001 - reported, never hidden
             res = {"error": f"{type(e).__name__}: {e}"}
     dist.barrier()
-    import json as _json
-    return _json.loads(gather_strings(_json.dumps(res), dist)[0])
+    return json.loads(gather_strings(json.dumps(res), dist)[0])
+
+
+def mctx_child(world, one_device):
+    """bench.py --mctx-child WORLD: mctx_device_leg's work in its own process;
+    one JSON line {"mctx": ...}."""
+    import torch
+    from tulips_amd import csum
+    from tulips_amd.shard import SHARD_SEGMENTS
+    _bench().crash_backtrace()
+    devs = [0] * world if one_device else list(range(world))
+    res = {}
+    try:
+        n = world * SHARD_SEGMENTS
+        d0 = torch.device("cuda", 0)
+        with torch.cuda.device(d0):
+            arena = torch.empty(n * SEG + 64, dtype=torch.uint8, device=d0)
+            _bench().fill_splitmix(arena, n * SEG, seed=DATA_SEED)
+            out = torch.empty(n, dtype=torch.uint16, device=d0)
+            st = torch.cuda.current_stream(d0)
+            with csum.MultiContext(devs, chunk_bytes=1 << 20) as m:
+                m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)   # buffers made
+                st.synchronize()
+                best = None
+                for _ in range(3):
+                    st.synchronize()
+                    t0 = time.perf_counter()
+                    m.batch_fixed_device(arena, SEG, SEG, n, out=out, stream=st)
+                    st.synchronize()
+                    t = time.perf_counter() - t0
+                    best = t if best is None else min(best, t)
+                bounds = m.bounds().tolist()
+            o = out.cpu().numpy().view(np.uint16)
+        gold = golden_digests().get("M8x1500", {})
+        shards = gold.get("shards", [])
+        ok = all(fnv1a_u16(o[k * SHARD_SEGMENTS:(k + 1) * SHARD_SEGMENTS]) ==
+                 shards[k]["fnv1a64"] for k in range(min(world, len(shards))))
+        if world == 8:
+            ok = ok and fnv1a_u16(o) == gold.get("fnv1a64")
+        nbytes = float(n) * SEG
+        res = {"entry": "tulips_csum_mctx_batch_fixed_device (one process, devices "
+                        f"{devs})",
+               "workload": f"{n:,} x 1500 B resident on GPU 0 ({nbytes / 1e9:.2f} GB)",
+               "bytes_pulled_by_peers": int(nbytes * (world - 1) / world),
+               "ms": round(best * 1e3, 3),
+               "value_exchange_inclusive_GiBps": round(nbytes / best / GIB, 2),
+               "shard_bounds": bounds,
+               "parity": "ok" if ok else "MISMATCH"}
+        del arena, out
+        res["kernel_only"] = single_process_kernel_only(torch, csum, devs)
+    except Exception as e:  # noqa: BLE001 - reported, never hidden
+        res = {"error": f"{type(e).__name__}: {e}"}
+    print(json.dumps({"mctx": res}), flush=True)
 
 
 def single_process_kernel_only(torch, csum, devs, rotations=4):
