@@ -36,6 +36,16 @@
 //       the fixed-stride kernel's one-launch-at-a-time rate on this runtime
 //       (NBATCH rotated batches of 65,536 x L bytes, a captured chain of 256
 //       launches, HIP events, median of 5), batch 0 checked against FNV.
+//   runtime_check fixtures DIR
+//       the §8f kernels on this runtime against fixtures the driving test
+//       writes to DIR as raw little-endian arrays (test infrastructure):
+//       frame validation flags == the reference-computed flags of
+//       tests/golden/frames.npz; in-place generation restores the checksum
+//       fields of every frame the reference found valid, after they were
+//       zeroed, and touches no other byte; compact fields equal the stored
+//       fields of those frames; Toeplitz RSS == tests/golden/rss.npz (10
+//       keys x 2 inits); segmentation == the oracle's segments (LSO fix-ups
+//       parity-unpinned).
 //   runtime_check capture-neutral F1500=FNV ZIPF=FNV ZIPF-tcp=FNV
 //       the library beside another thread's global-mode capture: thread A
 //       captures a fixed-stride F1500 call (hipStreamCaptureModeGlobal);
@@ -310,6 +320,225 @@ cmd_parity(int argc, char** argv)
   (void)hipFree(dst);
   (void)hipFree(d_zoffs);
   (void)hipFree(d_zlens);
+  return bad ? 1 : 0;
+}
+
+// ---- §8f kernels against fixtures -----------------------------------------------------
+template<class T>
+std::vector<T>
+read_raw(const std::string& path)
+{
+  std::vector<T> v;
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) {
+    fprintf(stderr, "cannot open %s\n", path.c_str());
+    exit(2);
+  }
+  fseek(f, 0, SEEK_END);
+  const long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  v.resize(size_t(n) / sizeof(T));
+  if (!v.empty() && fread(v.data(), sizeof(T), v.size(), f) != v.size()) {
+    fprintf(stderr, "short read %s\n", path.c_str());
+    exit(2);
+  }
+  fclose(f);
+  return v;
+}
+
+int
+cmd_fixtures(const std::string& dir)
+{
+  hipStream_t st = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  std::string out = "{\"fixtures\": {";
+  int bad = 0;
+  auto report = [&](const char* name, bool ok, const std::string& detail) {
+    bad += ok ? 0 : 1;
+    out += std::string(out.back() == '{' ? "" : ", ") + "\"" + name + "\": {\"ok\": " +
+           (ok ? "true" : "false") + detail + "}";
+  };
+
+  // frames: validation, in-place generation, compact fields
+  {
+    const auto arena = read_raw<uint8_t>(dir + "/frames.arena.bin");
+    const auto offs = read_raw<uint64_t>(dir + "/frames.offsets.bin");
+    const auto lens = read_raw<uint16_t>(dir + "/frames.lengths.bin");
+    const auto expect = read_raw<uint8_t>(dir + "/frames.expect.bin");
+    const uint32_t n = uint32_t(offs.size());
+    uint8_t* d_arena = to_device(arena);
+    uint64_t* d_offs = to_device(offs);
+    uint16_t* d_lens = to_device(lens);
+    uint8_t* d_flags = to_device(std::vector<uint8_t>(n, 0xA5));
+    uint32_t* d_cnt = to_device(std::vector<uint32_t>(4, 0xA5A5A5A5u));
+    CS_OK(tulips_csum_validate_frames(d_arena, d_offs, d_lens, n, d_flags, d_cnt, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const auto flags = to_host(d_flags, n);
+    const auto cnt = to_host(d_cnt, 4);
+    uint32_t want_cnt[4] = { 0, 0, 0, 0 };
+    uint32_t mism = 0, valid = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      mism += flags[i] != expect[i];
+      const uint8_t e = expect[i];
+      want_cnt[0] += (e & TULIPS_FRAME_IPV4) != 0;
+      want_cnt[1] += (e & TULIPS_FRAME_IPV4) && !(e & TULIPS_FRAME_IP_CSUM_OK);
+      want_cnt[2] += (e & TULIPS_FRAME_TCP) != 0;
+      want_cnt[3] += (e & TULIPS_FRAME_TCP) && !(e & TULIPS_FRAME_L4_CSUM_OK);
+      valid += e == 0x0F;
+    }
+    const bool cnt_ok = std::equal(cnt.begin(), cnt.end(), want_cnt);
+    report("frames_validate", mism == 0 && cnt_ok,
+           ", \"frames\": " + std::to_string(n) + ", \"flag_mismatches\": " +
+             std::to_string(mism) + ", \"counters_ok\": " + (cnt_ok ? "true" : "false"));
+
+    // compact fields of the frames the reference found valid: their stored words
+    uint32_t* d_fields = to_device(std::vector<uint32_t>(n, 0xA5A5A5A5u));
+    CS_OK(tulips_csum_generate_fields(d_arena, d_offs, d_lens, n, d_fields, nullptr, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const auto fields = to_host(d_fields, n);
+    uint32_t fmism = 0;
+    auto word = [&](const std::vector<uint8_t>& a, uint64_t at) {
+      return uint32_t(a[at]) | uint32_t(a[at + 1]) << 8;
+    };
+    for (uint32_t i = 0; i < n; ++i) {
+      if (expect[i] == 0x0F) {
+        const uint32_t w = word(arena, offs[i] + 24) | word(arena, offs[i] + 50) << 16;
+        fmism += fields[i] != w;
+      }
+    }
+    report("frames_generate_fields", fmism == 0 && valid > 0,
+           ", \"valid_frames\": " + std::to_string(valid) + ", \"mismatches\": " +
+             std::to_string(fmism));
+
+    // in place: zero the fields of the valid frames, regenerate every frame
+    std::vector<uint8_t> zeroed = arena;
+    std::vector<uint8_t> field_byte(arena.size(), 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      for (uint64_t at : { offs[i] + 24, offs[i] + 25, offs[i] + 50, offs[i] + 51 }) {
+        if (at < arena.size()) {
+          field_byte[at] = 1;
+          if (expect[i] == 0x0F) {
+            zeroed[at] = 0;
+          }
+        }
+      }
+    }
+    HIP_OK(hipMemcpy(d_arena, zeroed.data(), zeroed.size(), hipMemcpyHostToDevice));
+    CS_OK(tulips_csum_generate_frames(d_arena, d_offs, d_lens, n, nullptr, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const auto gen = to_host(d_arena, arena.size());
+    uint64_t restored_bad = 0, other_bad = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (expect[i] == 0x0F) {
+        for (uint64_t at : { offs[i] + 24, offs[i] + 25, offs[i] + 50, offs[i] + 51 }) {
+          restored_bad += gen[at] != arena[at];
+        }
+      }
+    }
+    for (size_t b = 0; b < arena.size(); ++b) {
+      other_bad += !field_byte[b] && gen[b] != zeroed[b];
+    }
+    report("frames_generate_in_place", restored_bad == 0 && other_bad == 0,
+           ", \"field_bytes_wrong\": " + std::to_string(restored_bad) +
+             ", \"other_bytes_changed\": " + std::to_string(other_bad));
+    for (void* q : { static_cast<void*>(d_arena), static_cast<void*>(d_offs),
+                     static_cast<void*>(d_lens), static_cast<void*>(d_flags),
+                     static_cast<void*>(d_cnt), static_cast<void*>(d_fields) }) {
+      (void)hipFree(q);
+    }
+  }
+
+  // Toeplitz RSS
+  {
+    const auto sa = read_raw<uint32_t>(dir + "/rss.saddr.bin");
+    const auto da = read_raw<uint32_t>(dir + "/rss.daddr.bin");
+    const auto sp = read_raw<uint16_t>(dir + "/rss.sport.bin");
+    const auto dp = read_raw<uint16_t>(dir + "/rss.dport.bin");
+    const uint32_t n = uint32_t(sa.size());
+    uint32_t* d_sa = to_device(sa);
+    uint32_t* d_da = to_device(da);
+    uint16_t* d_sp = to_device(sp);
+    uint16_t* d_dp = to_device(dp);
+    uint32_t* d_h = to_device(std::vector<uint32_t>(n, 0));
+    uint32_t keys = 0, mism = 0;
+    for (int k = 0;; ++k) {
+      const std::string kp = dir + "/rss.key_" + std::to_string(k) + ".bin";
+      FILE* f = fopen(kp.c_str(), "rb");
+      if (!f) {
+        break;
+      }
+      fclose(f);
+      const auto key = read_raw<uint8_t>(kp);
+      for (const char* tag : { "init0", "initff" }) {
+        const uint32_t init = strcmp(tag, "init0") == 0 ? 0u : 0xFFFFFFFFu;
+        const auto want = read_raw<uint32_t>(dir + "/rss.expect_" + std::to_string(k) + "_" +
+                                             tag + ".bin");
+        HIP_OK(hipMemsetAsync(d_h, 0xA5, n * 4, st));
+        CS_OK(tulips_rss_toeplitz_batch(d_sa, d_da, d_sp, d_dp, n, key.data(), key.size(), init,
+                                        d_h, st));
+        HIP_OK(hipStreamSynchronize(st));
+        const auto got = to_host(d_h, n);
+        for (uint32_t i = 0; i < n; ++i) {
+          mism += got[i] != want[i];
+        }
+      }
+      ++keys;
+    }
+    report("rss_toeplitz", mism == 0 && keys > 0,
+           ", \"tuples\": " + std::to_string(n) + ", \"keys\": " + std::to_string(keys) +
+             ", \"mismatches\": " + std::to_string(mism));
+    for (void* q : { static_cast<void*>(d_sa), static_cast<void*>(d_da), static_cast<void*>(d_sp),
+                     static_cast<void*>(d_dp), static_cast<void*>(d_h) }) {
+      (void)hipFree(q);
+    }
+  }
+
+  // segmentation against the oracle's segments
+  {
+    const auto arena = read_raw<uint8_t>(dir + "/seg.arena.bin");
+    const auto offs = read_raw<uint64_t>(dir + "/seg.offsets.bin");
+    const auto lens = read_raw<uint16_t>(dir + "/seg.lengths.bin");
+    const auto params = read_raw<uint32_t>(dir + "/seg.params.bin"); // mss, stride
+    const auto efirst = read_raw<uint32_t>(dir + "/seg.first.bin");
+    const auto eout = read_raw<uint8_t>(dir + "/seg.out.bin");
+    const auto elens = read_raw<uint16_t>(dir + "/seg.out_lengths.bin");
+    const uint32_t n = uint32_t(offs.size()), mss = params[0], stride = params[1];
+    const uint32_t total = efirst[n];
+    uint8_t* d_in = to_device(arena);
+    uint64_t* d_offs = to_device(offs);
+    uint16_t* d_lens = to_device(lens);
+    uint8_t* d_out = to_device(std::vector<uint8_t>(size_t(total) * stride, 0x5B));
+    uint16_t* d_olens = to_device(std::vector<uint16_t>(total, 0xA5A5));
+    uint32_t* d_first = to_device(std::vector<uint32_t>(n + 1, 0xA5A5A5A5u));
+    CS_OK(tulips_csum_segment_frames(d_in, d_offs, d_lens, n, mss, d_out, stride, total, d_olens,
+                                     d_first, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const auto first = to_host(d_first, n + 1);
+    const auto olens = to_host(d_olens, total);
+    const auto sout = to_host(d_out, size_t(total) * stride);
+    uint64_t bytes_bad = 0;
+    const bool plan_ok = first == efirst && olens == elens;
+    if (plan_ok) {
+      for (uint32_t j = 0; j < total; ++j) {
+        for (uint32_t b = 0; b < elens[j]; ++b) {
+          bytes_bad += sout[size_t(j) * stride + b] != eout[size_t(j) * stride + b];
+        }
+      }
+    }
+    report("segment_frames", plan_ok && bytes_bad == 0,
+           ", \"super_frames\": " + std::to_string(n) + ", \"segments\": " +
+             std::to_string(total) + ", \"plan_ok\": " + (plan_ok ? "true" : "false") +
+             ", \"bytes_wrong\": " + std::to_string(bytes_bad));
+    for (void* q : { static_cast<void*>(d_in), static_cast<void*>(d_offs),
+                     static_cast<void*>(d_lens), static_cast<void*>(d_out),
+                     static_cast<void*>(d_olens), static_cast<void*>(d_first) }) {
+      (void)hipFree(q);
+    }
+  }
+  CS_OK(tulips_csum_release_stream(st));
+  HIP_OK(hipStreamDestroy(st));
+  out += "}, \"runtime\": " + runtime_json() + "}";
+  printf("%s\n", out.c_str());
   return bad ? 1 : 0;
 }
 
@@ -1366,6 +1595,9 @@ main(int argc, char** argv)
   }
   if (cmd == "parity") {
     return cmd_parity(argc - 2, argv + 2);
+  }
+  if (cmd == "fixtures" && argc == 3) {
+    return cmd_fixtures(argv[2]);
   }
   if (cmd == "capture-neutral") {
     return cmd_capture_neutral(argc - 2, argv + 2);

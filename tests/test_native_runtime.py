@@ -109,3 +109,48 @@ def test_native_calls_beside_a_global_mode_capture(golden):
     print(json.dumps(res, indent=1))
     assert res is not None, err
     assert rc == 0 and res["capture_neutral"]["ok"], (res, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_native_section8f_kernels_against_fixtures(tmp_path, oracle):
+    """The §8f kernels through the C ABI on /opt/rocm's runtime: frame
+    validation flags and counters against tests/golden/frames.npz (flags the
+    reference's own stack computed), in-place generation restoring the zeroed
+    checksum fields of the frames the reference found valid (no other byte
+    touched), compact fields equal to those frames' stored fields, Toeplitz RSS
+    against tests/golden/rss.npz (the reference's utils::toeplitz, 10 keys x 2
+    inits), and segmentation against the oracle (orc_segment_frames; the LSO
+    fix-ups are parity-unpinned)."""
+    import numpy as np
+    from test_segment import pack as seg_pack, super_frame
+    gdir = os.path.join(ROOT, "tests", "golden")
+    fr = np.load(os.path.join(gdir, "frames.npz"))
+    for k, name in (("arena", "arena"), ("offsets", "offsets"), ("lengths", "lengths"),
+                    ("expect", "expect")):
+        fr[k].tofile(tmp_path / f"frames.{name}.bin")
+    rs = np.load(os.path.join(gdir, "rss.npz"))
+    for k in ("saddr", "daddr", "sport", "dport"):
+        rs[k].tofile(tmp_path / f"rss.{k}.bin")
+    for i in range(len(rs["key_names"])):
+        rs[f"key_{i}"].tofile(tmp_path / f"rss.key_{i}.bin")
+        for tag in ("init0", "initff"):
+            rs[f"expect_{i}_{tag}"].tofile(tmp_path / f"rss.expect_{i}_{tag}.bin")
+    rng = np.random.default_rng(8)
+    payloads = [int(p) for p in rng.integers(1, 64000, 40)] + [1460, 1461, 2920, 0]
+    frames = [super_frame(oracle, rng, p) for p in payloads]
+    arena, offs, lens = seg_pack(frames, rng)
+    mss, stride = 1460, 2048
+    first, out, olens = oracle.segment_frames(arena, offs, lens, mss, stride)
+    arena.tofile(tmp_path / "seg.arena.bin")
+    offs.tofile(tmp_path / "seg.offsets.bin")
+    lens.tofile(tmp_path / "seg.lengths.bin")
+    np.array([mss, stride], np.uint32).tofile(tmp_path / "seg.params.bin")
+    first.tofile(tmp_path / "seg.first.bin")
+    out.tofile(tmp_path / "seg.out.bin")
+    olens.tofile(tmp_path / "seg.out_lengths.bin")
+    rc, res, err = _run("fixtures", str(tmp_path), timeout=240)
+    print(json.dumps(res, indent=1))
+    assert res is not None, err
+    bad = {k: v for k, v in res["fixtures"].items() if not v["ok"]}
+    assert rc == 0 and not bad and len(res["fixtures"]) == 5, (bad, err)
