@@ -2,7 +2,9 @@
 (a plain C++ process, no torch, the library's NEEDED libamdhip64.so.7
 resolved through its RUNPATH to /opt/rocm) drives the C ABI and compares the
 SURVEY.md §8c golden digests (tests/golden/digests.json, made by the
-reference's own compiled sources) bit-exactly, checks the HIP user-object
+reference's own compiled sources) bit-exactly, checks the §8f kernels
+(frames, generation, RSS, segmentation) against the golden fixtures and the
+oracle, checks the HIP user-object
 contract the graph ownership relies on, and runs 500 capture/replay/destroy
 cycles with device memory flat. Every pytest GPU run otherwise uses the HIP
 runtime torch bundles (tests/test_graph_lifetime.py covers that one).
