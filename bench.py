@@ -233,7 +233,7 @@ class Timer:
         self._streams = []
         # every graph this timer captured, kept alive until the process ends:
         # the HIP runtime torch bundles can crash in hipGraphLaunch after a
-        # multi-branch graph was destroyed (DESIGN.md §5 "The r04 SIGSEGV",
+        # multi-branch graph was destroyed (DESIGN.md §8,
         # tools/probe_graph_churn.py), and no launch follows the teardown
         self._kept = []
 

@@ -463,7 +463,7 @@ int tulips_csum_validate_frames_cpu(const uint8_t* base, const uint64_t* offsets
 /*
  * The CPU / GPU crossover for one receive poll burst, measured on MI355X
  * with frames a NIC has just written (outside the CPU caches; bench.py
- * extras.burst_latency_host.cold_ring, DESIGN.md §5): 1514 B frames cost the
+ * extras.burst_latency_host.cold_ring, INTEGRATION.md §3): 1514 B frames cost the
  * host code ~0.13-0.16 us each, the zero-copy GPU path ~13 us + ~0.02 us
  * each (64 frames: 8.5 against 14.4 us; 256: 41.4 against 18.3), so they
  * cross near 96 frames; the host cost follows the bytes, so larger frames

@@ -6,7 +6,7 @@
  *
  * The ceiling kernels here are the product kernels' load (and store)
  * patterns without their arithmetic: the roofline each kernel is compared
- * against in bench.py's `summary` and DESIGN.md §3.
+ * against in bench.py's `summary` and DESIGN.md §1 / §5 ("ceiling").
  */
 #ifndef TULIPS_CSUM_BENCH_H
 #define TULIPS_CSUM_BENCH_H

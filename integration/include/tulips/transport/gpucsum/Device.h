@@ -79,8 +79,8 @@ public:
 
   static constexpr uint32_t DEFAULT_BURST = 1024;
   // bursts up to this size take the zero-copy path (on MI355X it beats the
-  // staged one at every burst size up to its 1,024-frame limit: DESIGN.md §5
-  // "Latency per poll burst")
+  // staged one at every burst size up to its 1,024-frame limit: INTEGRATION.md
+  // §3, the latency-per-burst table)
   static constexpr uint32_t DEFAULT_LOWLAT = 1024;
   // bursts of fewer frames (and bytes) are validated on the polling thread
   // by the library's host code (tulips_csum_validate_frames_cpu): below
@@ -88,7 +88,7 @@ public:
   // checks do on the CPU. The library's measured crossover
   // (tulips_csum_burst_prefers_cpu, include/tulips_csum.h): cold 1514 B
   // frames cost ~0.15 us each on the host against ~13 us + 0.02 us each on
-  // the zero-copy path, crossing near 96 frames (DESIGN.md §5)
+  // the zero-copy path, crossing near 96 frames (INTEGRATION.md §3)
   static constexpr uint32_t DEFAULT_CPU_BELOW = TULIPS_CSUM_CPU_BELOW_FRAMES;
   static constexpr uint64_t DEFAULT_CPU_BELOW_BYTES = TULIPS_CSUM_CPU_BELOW_BYTES;
 

@@ -588,7 +588,7 @@ def test_fuzz_captured_graphs(oracle):
     # A dropped graph is kept alive, not destroyed: destroying a multi-branch
     # graph makes a later hipGraphLaunch of the HIP runtime torch bundles
     # crash, with torch kernels alone too (tools/probe_graph_churn.py;
-    # DESIGN.md §5). TULIPS_FUZZ_GRAPH_DESTROY=1 destroys them (that crash).
+    # DESIGN.md §8). TULIPS_FUZZ_GRAPH_DESTROY=1 destroys them (that crash).
     destroy = bool(os.environ.get("TULIPS_FUZZ_GRAPH_DESTROY"))
     kept = _KEPT_GRAPHS    # (alive to the end of the process: later tests launch graphs)
     budget = float(os.environ.get("TULIPS_FUZZ_SECONDS", "8"))

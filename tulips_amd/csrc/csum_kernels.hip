@@ -3,7 +3,7 @@
 // src/stack/tcpv4/Processor.cpp:337-357 (a2), src/stack/IPv4.cpp:75-82 (a5),
 // src/stack/ICMPv4.cpp:10-15 (a6); closed form in csum_common.h.
 //
-// Design (DESIGN.md §4): the op is an HBM-read-bound integer reduction
+// Design (DESIGN.md §5): the op is an HBM-read-bound integer reduction
 // (~0.5 VALU op per byte), so the kernels are built for bytes in flight, not
 // arithmetic. Three shipped families, one per batch shape:
 //   * csum_kernel — fixed stride and length (F1500, F9000): a SUBGROUP of G

@@ -1,5 +1,5 @@
 // span_kernel.h — the in-order-arena (SPAN) checksum kernel, split form with
-// the chunk prefixes in LDS. The kernel is a template over a
+// the chunk prefixes in LDS (its history profiles/HISTORY.md §4). The kernel is a template over a
 // probe so that tools/sessions/probes/span_stamps.hip can time the product code path
 // itself; the product launches csum_span_kernel<U> (NoProbe, which compiles
 // to nothing) from csum_kernels.hip. Semantics: src/stack/Utils.cpp:14-42
