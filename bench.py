@@ -153,7 +153,7 @@ SERIAL_LAUNCHES = 256
 
 def branches_for(steps):
     """Graph branches for a K-step timed replay. A replay costs about a + b K
-    (tools/probe_graph_k.py, profiles/probe_graph_k_r04.txt, one box; b from
+    (tools/sessions/probes/probe_graph_k.py, profiles/probe_graph_k_r04.txt, one box; b from
     K = 4..64): 1 branch a = 10 us, b = 15.6 us; 2 branches a = 24 us,
     b = 13.47 us; 4-16 branches a = 39-40 us, b = 13.36-13.41 us. The
     per-replay cost grows with the hardware queues the graph spans, so 2

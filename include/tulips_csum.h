@@ -535,7 +535,7 @@ int tulips_csum_segment_frames_host(tulips_csum_ctx* ctx, const uint8_t* in_base
  */
 /* Kernel families (tulips_csum_tuning.kind). Kinds 2 and 4 (hybrid,
    workgroup-balanced) and the other span forms are measured variants kept
-   outside the library (tools/variants/); the library rejects them. */
+   outside the library (tools/sessions/variants/); the library rejects them. */
 #define TULIPS_CSUM_KIND_DEFAULT 0
 #define TULIPS_CSUM_KIND_SUBGROUP 1 /* `group` lanes (16/32/64) per segment,
                                        `unroll` chunks per lane in flight

@@ -223,7 +223,7 @@ def test_default_tuning():
     t = csum.default_tuning(0, variable=True)
     assert t.kind == csum.KIND_PACKED and t.group == 8 and t.unroll == 4 and t.sps == 2
     # packed geometries are for variable-length batches only; kinds 2 and 4
-    # (hybrid, workgroup-balanced) live in tools/variants, not the library
+    # (hybrid, workgroup-balanced) live in tools/sessions/variants, not the library
     for kind in (2, 4, csum.KIND_PACKED):
         bad = csum.Tuning(kind=kind, group=16, unroll=4, nontemporal=1)
         assert csum.lib.tulips_csum_batch_fixed_tuned(FAKE, 1500, 1500, None, None, None,

@@ -264,7 +264,7 @@ geometry_ok(int kind, int group, int unroll, int spw, bool variable)
   }
 }
 
-// Default geometry (measured on MI355X by tools/sweep.py,
+// Default geometry (measured on MI355X by tools/sessions/probes/sweep.py,
 // profiles/sweep_r01.json): nt loads everywhere; the subgroup is sized so a
 // lane holds about one batch of chunks.
 tulips_csum_tuning
@@ -278,7 +278,7 @@ default_tuning(uint32_t len, bool variable)
   t.sps = 1;
   if (variable) {
     // one wave per 8 segments, chunks packed end to end, 4 windows in
-    // flight, double-buffered (tools/probe_packed.py,
+    // flight, double-buffered (tools/sessions/probes/probe_packed.py,
     // profiles/probe_packed_r01.json: ZIPF 14.8 us vs 16.8 single-buffered
     // and 18.7 hybrid; 1500 B through offsets 19.1 vs 34.2 hybrid).
     // 256-thread blocks: 1024-thread blocks are 0.6 us faster alone but
@@ -292,7 +292,7 @@ default_tuning(uint32_t len, bool variable)
   }
   const uint32_t nch = len / 16 + 2;
   if (nch > 512) {        // > ~8 KiB (F9000): whole wave, 12 chunks per lane,
-    t.group = 64;         // a 9000 B segment in one batch (tools/probe_fixed.py:
+    t.group = 64;         // a 9000 B segment in one batch (tools/sessions/probes/probe_fixed.py:
     t.unroll = 12;        // 82.3 vs 84.0 us for 64 x 8)
   } else if (nch > 256) { // > ~4 KiB: whole wave, 8 chunks in flight per lane
     t.group = 64;
@@ -302,7 +302,7 @@ default_tuning(uint32_t len, bool variable)
     t.unroll = 4;
   } else if (nch > 64) {  // ~1-1.5 KiB (F1500): 32 lanes x 3, the 96 chunks a
     t.group = 32;         // 1500 B segment touches at any alignment in one batch
-    t.unroll = 3;         // with no redundant loads (tools/probe_fixed.py,
+    t.unroll = 3;         // with no redundant loads (tools/sessions/probes/probe_fixed.py,
                           // profiles/probe_fixed_r05.txt: 15.73 vs 15.95 us)
   } else {
     t.group = 16;

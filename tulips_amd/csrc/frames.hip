@@ -55,7 +55,7 @@ using namespace frame;
 //   (field_contrib), so the frame is read once and 4 bytes are written.
 // Geometry: FG lanes x FU chunks in flight per frame. The default, 16 x 6
 // (4 frames per wave, 96 chunks = a 1514 B frame in one batch, nt loads), is
-// the best of tools/probe_frames.py's sweep on 1514 B frames
+// the best of tools/sessions/probes/probe_frames.py's sweep on 1514 B frames
 // (profiles/probe_frames_r01.json).
 // Minimum waves per SIMD the register allocator must leave room for
 // (0 = no bound). Generation: 94 -> 80 VGPRs, 5 -> 6 waves/SIMD, no spill;
@@ -93,7 +93,7 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
   // per block into one of CNT_SHARDS line-sized shards (finalised by
   // frame_counters_finalize). Adding every frame to the caller's 4 words
   // directly serialised ~33k same-address atomics: 378 us per 65,536-frame
-  // launch instead of 18 (tools/probe_counters.py).
+  // launch instead of 18 (tools/sessions/probes/probe_counters.py).
   __shared__ uint32_t s_cnt[4];
   const bool count = !GENERATE && shards != nullptr;   // grid-uniform
   if (count) {

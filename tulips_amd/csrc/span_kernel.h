@@ -104,10 +104,10 @@ struct NoProbe
 // re-zeroed: the next launch's tag differs (profiles/probe_span_early_r03.txt:
 // 0.2-0.4 us per ZIPF launch against compare-and-swap + re-zero).
 // TR > 0: the tail-shaped cut (measured against the uniform
-// one by tools/probe_span_tail.py): ranges k < p.k1 hold U rows, the last
+// one by tools/sessions/probes/probe_span_tail.py): ranges k < p.k1 hold U rows, the last
 // ones (dispatched last) TR rows, so the final workgroups on each CU finish
 // their data sooner and their tails overlap. TR = 0: every range U rows.
-// PRIO (the one ZIPF experiment, tools/probe_span_prio.py):
+// PRIO (the one ZIPF experiment, tools/sessions/probes/probe_span_prio.py):
 // a launch is one generation of workgroups whose post-data phases bunch in
 // its last ~2 us; the waves of ranges in the first quarter of the arena run
 // at instruction priority 3, the next quarters 2, 1, 0, so on a CU the
