@@ -46,6 +46,11 @@
 //       fields of those frames; Toeplitz RSS == tests/golden/rss.npz (10
 //       keys x 2 inits); segmentation == the oracle's segments (LSO fix-ups
 //       parity-unpinned).
+//   runtime_check thread-churn SECONDS THREADS
+//       graph ownership across host threads: each thread on its own stream
+//       captures (thread-local mode), instantiates, replays (checked) and
+//       destroys graphs of counting, arena and segmentation calls, with
+//       direct calls between; device memory back within 8 MiB at the end.
 //   runtime_check capture-neutral F1500=FNV ZIPF=FNV ZIPF-tcp=FNV
 //       the library beside another thread's global-mode capture: thread A
 //       captures a fixed-stride F1500 call (hipStreamCaptureModeGlobal);
@@ -964,6 +969,217 @@ cmd_graph_cycles(uint32_t cycles)
   return ok ? 0 : 1;
 }
 
+// ---- graph ownership across threads --------------------------------------------
+// THREADS host threads, each on its own stream, capture (thread-local mode)
+// counting verify + arena batch + segmentation, instantiate, destroy the
+// template, replay, check, destroy the executable - so user-object
+// destructors fire on every thread and several threads reclaim at once -
+// with direct calls between, for SECONDS. Every replay's outputs equal the
+// direct calls' made before the threads start; at the end (streams released)
+// device memory is back within 8 MiB of where it was after a warm-up.
+int
+cmd_thread_churn(double seconds, uint32_t nthreads)
+{
+  Rng r{ 0x7468726561647321ull };
+  const uint32_t n = 4096;
+  std::vector<uint16_t> lens(n);
+  std::vector<uint64_t> offs(n);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    lens[i] = uint16_t(40 + r.next() % 8960);
+    offs[i] = total;
+    total += lens[i];
+  }
+  std::vector<uint8_t> bytes(total + 64);
+  for (auto& b : bytes) {
+    b = uint8_t(r.next());
+  }
+  uint8_t* d_arena = to_device(bytes);
+  uint64_t* d_offs = to_device(offs);
+  uint16_t* d_lens = to_device(lens);
+  uint32_t* src = to_device(std::vector<uint32_t>(n, ip4(10, 1, 0, 1)));
+  uint32_t* dst = to_device(std::vector<uint32_t>(n, ip4(10, 1, 0, 2)));
+  std::vector<uint8_t> frames;
+  std::vector<uint64_t> foffs;
+  std::vector<uint16_t> flens;
+  for (int k = 0; k < 16; ++k) {
+    const std::vector<uint8_t> f = tcp_frame(r, 1000 + r.next() % 59000);
+    foffs.push_back(frames.size());
+    flens.push_back(uint16_t(f.size()));
+    frames.insert(frames.end(), f.begin(), f.end());
+    frames.resize((frames.size() + 2047) & ~size_t(2047));
+  }
+  const uint32_t nf = uint32_t(foffs.size()), mss = 1460, ostride = 2048, cap = 1024;
+  uint8_t* d_frames = to_device(frames);
+  uint64_t* d_foffs = to_device(foffs);
+  uint16_t* d_flens = to_device(flens);
+
+  struct Outs
+  {
+    uint16_t* csum = nullptr;
+    uint32_t* bad = nullptr;
+    uint16_t* arena = nullptr;
+    uint8_t* seg = nullptr;
+    uint16_t* seg_lens = nullptr;
+    uint32_t* first = nullptr;
+  };
+  auto make_outs = [&]() {
+    Outs o;
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.csum), n * 2));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.bad), 4));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.arena), n * 2));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.seg), size_t(cap) * ostride));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.seg_lens), cap * 2));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&o.first), (nf + 1) * 4));
+    return o;
+  };
+  auto free_outs = [](const Outs& o) {
+    for (void* q : { static_cast<void*>(o.csum), static_cast<void*>(o.bad),
+                     static_cast<void*>(o.arena), static_cast<void*>(o.seg),
+                     static_cast<void*>(o.seg_lens), static_cast<void*>(o.first) }) {
+      (void)hipFree(q);
+    }
+  };
+  auto clear = [&](const Outs& o, hipStream_t s) {
+    HIP_OK(hipMemsetAsync(o.csum, 0xA5, n * 2, s));
+    HIP_OK(hipMemsetAsync(o.bad, 0xA5, 4, s));
+    HIP_OK(hipMemsetAsync(o.arena, 0xA5, n * 2, s));
+    HIP_OK(hipMemsetAsync(o.seg, 0xA5, size_t(cap) * ostride, s));
+    HIP_OK(hipMemsetAsync(o.seg_lens, 0xA5, cap * 2, s));
+    HIP_OK(hipMemsetAsync(o.first, 0xA5, (nf + 1) * 4, s));
+  };
+  auto calls = [&](const Outs& o, hipStream_t s) {
+    CS_OK(tulips_csum_verify(d_arena, d_offs, d_lens, src, dst, o.csum, o.bad, n,
+                             TULIPS_CSUM_TCP, s));
+    CS_OK(tulips_csum_batch_arena(d_arena, total, d_offs, d_lens, nullptr, nullptr, nullptr,
+                                  o.arena, n, TULIPS_CSUM_INET, s));
+    CS_OK(tulips_csum_segment_frames(d_frames, d_foffs, d_flens, nf, mss, o.seg, ostride, cap,
+                                     o.seg_lens, o.first, s));
+  };
+  // outputs copied back on the thread's own stream
+  auto back = [](const void* p, size_t bytes, hipStream_t s) {
+    std::vector<uint8_t> v(bytes);
+    HIP_OK(hipMemcpyAsync(v.data(), p, bytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return v;
+  };
+  struct Snap
+  {
+    std::vector<uint8_t> csum, bad, arena, seg, seg_lens, first;
+    bool operator==(const Snap& b) const
+    {
+      return csum == b.csum && bad == b.bad && arena == b.arena && seg == b.seg &&
+             seg_lens == b.seg_lens && first == b.first;
+    }
+  };
+  auto snap = [&](const Outs& o, hipStream_t s) {
+    Snap x;
+    x.csum = back(o.csum, n * 2, s);
+    x.bad = back(o.bad, 4, s);
+    x.arena = back(o.arena, n * 2, s);
+    x.seg = back(o.seg, size_t(cap) * ostride, s);
+    x.seg_lens = back(o.seg_lens, cap * 2, s);
+    x.first = back(o.first, (nf + 1) * 4, s);
+    return x;
+  };
+
+  // reference outputs, and a single-thread warm-up of the same cycle
+  hipStream_t s0 = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+  const Outs o0 = make_outs();
+  clear(o0, s0);
+  calls(o0, s0);
+  HIP_OK(hipStreamSynchronize(s0));
+  const Snap want = snap(o0, s0);
+  auto cycle = [&](hipStream_t s, const Outs& o, bool full) {
+    hipGraph_t g = nullptr;
+    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    calls(o, s);
+    HIP_OK(hipStreamEndCapture(s, &g));
+    hipGraphExec_t x = nullptr;
+    HIP_OK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+    HIP_OK(hipGraphDestroy(g));
+    clear(o, s);
+    HIP_OK(hipStreamSynchronize(s)); // the launch stream idle
+    HIP_OK(hipGraphLaunch(x, s));
+    HIP_OK(hipStreamSynchronize(s));
+    bool ok;
+    if (full) {
+      ok = snap(o, s) == want;
+    } else {
+      ok = back(o.bad, 4, s) == want.bad && back(o.arena, n * 2, s) == want.arena &&
+           back(o.first, (nf + 1) * 4, s) == want.first;
+    }
+    HIP_OK(hipGraphExecDestroy(x));
+    return ok;
+  };
+  for (int c = 0; c < 5; ++c) {
+    if (!cycle(s0, o0, true)) {
+      fprintf(stderr, "warm-up cycle %d mismatched\n", c);
+      return 1;
+    }
+  }
+  calls(o0, s0); // reclaims the warm-up graphs' arrays
+  HIP_OK(hipDeviceSynchronize());
+  size_t free0 = 0, tot = 0;
+  HIP_OK(hipMemGetInfo(&free0, &tot));
+
+  std::atomic<uint64_t> cycles{ 0 }, mism{ 0 }, directs{ 0 };
+  const auto t_end =
+    std::chrono::steady_clock::now() + std::chrono::milliseconds(int64_t(seconds * 1000));
+  std::vector<std::thread> ts;
+  for (uint32_t t = 0; t < nthreads; ++t) {
+    ts.emplace_back([&, t] {
+      hipStream_t s = nullptr;
+      HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      const Outs o = make_outs(), od = make_outs();
+      uint64_t c = 0;
+      while (std::chrono::steady_clock::now() < t_end) {
+        mism += cycle(s, o, c % 10 == t % 10) ? 0 : 1;
+        ++c;
+        if (c % 4 == 0) { // a direct call on the stream between graphs
+          clear(od, s);
+          calls(od, s);
+          HIP_OK(hipStreamSynchronize(s));
+          mism += back(od.arena, n * 2, s) == want.arena ? 0 : 1;
+          ++directs;
+        }
+      }
+      cycles += c;
+      CS_OK(tulips_csum_release_stream(s));
+      HIP_OK(hipStreamDestroy(s));
+      free_outs(o);
+      free_outs(od);
+    });
+  }
+  for (auto& th : ts) {
+    th.join();
+  }
+  calls(o0, s0); // frees what the last destroyed graphs held
+  HIP_OK(hipDeviceSynchronize());
+  mism += snap(o0, s0) == want ? 0 : 1;
+  size_t free1 = 0;
+  HIP_OK(hipMemGetInfo(&free1, &tot));
+  const long long grew = (long long)free0 - (long long)free1;
+  const bool ok = mism.load() == 0 && cycles.load() > 0 && grew < (8ll << 20);
+  printf("{\"thread_churn\": {\"threads\": %u, \"seconds\": %.1f, \"graphs\": %llu, "
+         "\"direct_calls\": %llu, \"mismatches\": %llu, \"device_memory_growth\": %lld, "
+         "\"ok\": %s}, \"runtime\": %s}\n",
+         nthreads, seconds, (unsigned long long)cycles.load(),
+         (unsigned long long)directs.load(), (unsigned long long)mism.load(), grew,
+         ok ? "true" : "false", runtime_json().c_str());
+  CS_OK(tulips_csum_release_stream(s0));
+  HIP_OK(hipStreamDestroy(s0));
+  free_outs(o0);
+  for (void* q : { static_cast<void*>(d_arena), static_cast<void*>(d_offs),
+                   static_cast<void*>(d_lens), static_cast<void*>(src), static_cast<void*>(dst),
+                   static_cast<void*>(d_frames), static_cast<void*>(d_foffs),
+                   static_cast<void*>(d_flens) }) {
+    (void)hipFree(q);
+  }
+  return ok ? 0 : 1;
+}
+
 // ---- multi-branch graph churn ---------------------------------------------------
 // The capture/replay/destroy churn that faults inside hipGraphLaunch on the
 // runtime torch bundles (profiles/graph_crash_r05.txt), run here
@@ -1595,6 +1811,9 @@ main(int argc, char** argv)
   }
   if (cmd == "parity") {
     return cmd_parity(argc - 2, argv + 2);
+  }
+  if (cmd == "thread-churn" && argc == 4) {
+    return cmd_thread_churn(atof(argv[2]), uint32_t(atoi(argv[3])));
   }
   if (cmd == "fixtures" && argc == 3) {
     return cmd_fixtures(argv[2]);

@@ -156,3 +156,18 @@ def test_native_section8f_kernels_against_fixtures(tmp_path, oracle):
     assert res is not None, err
     bad = {k: v for k, v in res["fixtures"].items() if not v["ok"]}
     assert rc == 0 and not bad and len(res["fixtures"]) == 5, (bad, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_native_graph_ownership_across_threads():
+    """Graph ownership (stream_state.h) with six host threads on /opt/rocm's
+    runtime: each captures (thread-local mode), replays and destroys graphs of
+    counting, arena and segmentation calls on its own stream for 15 s, direct
+    calls between, so user-object destructors fire and reclaims run on every
+    thread at once; every replay exact, device memory back within 8 MiB."""
+    rc, res, err = _run("thread-churn", "15", "6", timeout=240)
+    print(json.dumps(res, indent=1))
+    assert res is not None, err
+    r = res["thread_churn"]
+    assert rc == 0 and r["ok"] and r["mismatches"] == 0 and r["graphs"] > 100, (res, err)
