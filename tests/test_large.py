@@ -145,3 +145,42 @@ def test_frames_and_segmentation_past_4gib(big, oracle):
     want = eout.reshape(-1, stride)
     for j in range(len(elens)):
         assert np.array_equal(got[j, :elens[j]], want[j, :elens[j]]), j
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_segmentation_at_max_frames(oracle):
+    """tulips_csum_segment_frames at its limit, n = 2^24 frames
+    (include/tulips_csum.h): small TCP frames of 0-10 payload bytes in 64 B
+    slots, MSS 4, so frames become 1-3 segments and the count scan runs over
+    all 65,536 of its blocks; first[], every segment length and every segment
+    byte against the oracle (orc_segment_frames)."""
+    import torch
+    from tulips_amd import csum
+    n = 1 << 24
+    slot, mss = 64, 4
+    rng = np.random.default_rng(24)
+    pay = rng.integers(0, 11, n).astype(np.uint16)
+    f = rng.integers(0, 256, (n, slot), dtype=np.uint8)
+    f[:, 12], f[:, 13], f[:, 14], f[:, 15] = 0x08, 0x00, 0x45, 0x00
+    tot = 40 + pay
+    f[:, 16], f[:, 17] = (tot >> 8).astype(np.uint8), (tot & 0xFF).astype(np.uint8)
+    f[:, 20], f[:, 21], f[:, 22], f[:, 23] = 0x40, 0x00, 64, 6
+    f[:, 46] = 0x50
+    arena = f.reshape(-1)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    lens = (54 + pay).astype(np.uint16)
+    efirst, eout, elens = oracle.segment_frames(arena, offs, lens, mss, slot)
+    total = int(efirst[-1])
+    assert total > n
+    d_ar = torch.from_numpy(arena).to("cuda:0")
+    d_offs = torch.from_numpy(offs.view(np.int64)).to("cuda:0")
+    d_lens = torch.from_numpy(lens.view(np.int16)).to("cuda:0")
+    out, olens, first = csum.segment_frames(d_ar, d_offs, d_lens, mss, stride=slot)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(first.cpu().numpy().view(np.uint32), efirst)
+    np.testing.assert_array_equal(olens.cpu().numpy().view(np.uint16)[:total], elens)
+    got = out.cpu().numpy()[:total * slot].reshape(total, slot)
+    want = eout.reshape(total, slot)
+    keep = np.arange(slot)[None, :] < elens.astype(np.int64)[:, None]
+    assert np.array_equal(got[keep], want[keep])
