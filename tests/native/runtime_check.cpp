@@ -50,7 +50,8 @@
 //       graph ownership across host threads: each thread on its own stream
 //       captures (thread-local mode), instantiates, replays (checked) and
 //       destroys graphs of counting, arena and segmentation calls, with
-//       direct calls between; device memory back within 8 MiB at the end.
+//       direct calls between; device memory back within 32 MiB at the end
+//       (a leak of the graphs' arrays would be >= 4 KiB x every graph).
 //   runtime_check capture-neutral F1500=FNV ZIPF=FNV ZIPF-tcp=FNV
 //       the library beside another thread's global-mode capture: thread A
 //       captures a fixed-stride F1500 call (hipStreamCaptureModeGlobal);
@@ -976,7 +977,9 @@ cmd_graph_cycles(uint32_t cycles)
 // destructors fire on every thread and several threads reclaim at once -
 // with direct calls between, for SECONDS. Every replay's outputs equal the
 // direct calls' made before the threads start; at the end (streams released)
-// device memory is back within 8 MiB of where it was after a warm-up.
+// device memory is back within 32 MiB of where it was after a warm-up (the
+// runtime keeps per-thread pools, 4 MiB measured; the graphs' own arrays,
+// leaked, would be at least 4 KiB each, hundreds of MiB).
 int
 cmd_thread_churn(double seconds, uint32_t nthreads)
 {
@@ -1161,7 +1164,7 @@ cmd_thread_churn(double seconds, uint32_t nthreads)
   size_t free1 = 0;
   HIP_OK(hipMemGetInfo(&free1, &tot));
   const long long grew = (long long)free0 - (long long)free1;
-  const bool ok = mism.load() == 0 && cycles.load() > 0 && grew < (8ll << 20);
+  const bool ok = mism.load() == 0 && cycles.load() > 0 && grew < (32ll << 20);
   printf("{\"thread_churn\": {\"threads\": %u, \"seconds\": %.1f, \"graphs\": %llu, "
          "\"direct_calls\": %llu, \"mismatches\": %llu, \"device_memory_growth\": %lld, "
          "\"ok\": %s}, \"runtime\": %s}\n",
