@@ -45,7 +45,9 @@
 //       zeroed, and touches no other byte; compact fields equal the stored
 //       fields of those frames; Toeplitz RSS == tests/golden/rss.npz (10
 //       keys x 2 inits); segmentation == the oracle's segments (LSO fix-ups
-//       parity-unpinned).
+//       parity-unpinned); and the host-memory forms of
+//       validation (staged, host code, zero-copy per burst and resident),
+//       generation and segmentation through a host context.
 //   runtime_check thread-churn SECONDS THREADS
 //       graph ownership across host threads: each thread on its own stream
 //       captures (thread-local mode), instantiates, replays (checked) and
@@ -540,6 +542,109 @@ cmd_fixtures(const std::string& dir)
                      static_cast<void*>(d_olens), static_cast<void*>(d_first) }) {
       (void)hipFree(q);
     }
+  }
+  // the host-memory forms: the same fixtures through a host context
+  {
+    const auto arena = read_raw<uint8_t>(dir + "/frames.arena.bin");
+    const auto offs = read_raw<uint64_t>(dir + "/frames.offsets.bin");
+    const auto lens = read_raw<uint16_t>(dir + "/frames.lengths.bin");
+    const auto expect = read_raw<uint8_t>(dir + "/frames.expect.bin");
+    const uint32_t n = uint32_t(offs.size());
+    tulips_csum_ctx* ctx = nullptr;
+    CS_OK(tulips_csum_ctx_create(0, 0, &ctx));
+    auto flags_ok = [&](const std::vector<uint8_t>& f) {
+      return std::equal(f.begin(), f.end(), expect.begin());
+    };
+    std::vector<uint8_t> f(n, 0xA5);
+    CS_OK(tulips_csum_validate_frames_host(ctx, arena.data(), offs.data(), lens.data(), n,
+                                           f.data(), nullptr));
+    const bool host_ok = flags_ok(f);
+    std::fill(f.begin(), f.end(), 0xA5);
+    CS_OK(tulips_csum_validate_frames_cpu(arena.data(), offs.data(), lens.data(), n, f.data(),
+                                          nullptr));
+    const bool cpu_ok = flags_ok(f);
+    // zero-copy bursts of at most TULIPS_CSUM_ZC_MAX_FRAMES from page-locked
+    // memory, one launch per burst and then the resident server
+    void* pinned = nullptr;
+    CS_OK(tulips_csum_host_alloc(arena.size(), &pinned));
+    memcpy(pinned, arena.data(), arena.size());
+    bool zc_ok[2] = { false, false };
+    for (int resident = 0; resident < 2; ++resident) {
+      CS_OK(tulips_csum_ctx_set_lowlat(ctx, resident));
+      std::fill(f.begin(), f.end(), 0xA5);
+      for (uint32_t i = 0; i < n; i += TULIPS_CSUM_ZC_MAX_FRAMES) {
+        const uint32_t m = std::min<uint32_t>(TULIPS_CSUM_ZC_MAX_FRAMES, n - i);
+        CS_OK(tulips_csum_validate_frames_zc(ctx, static_cast<const uint8_t*>(pinned),
+                                             offs.data() + i, lens.data() + i, m, f.data() + i,
+                                             nullptr));
+      }
+      zc_ok[resident] = flags_ok(f);
+    }
+    CS_OK(tulips_csum_ctx_set_lowlat(ctx, 0));
+    CS_OK(tulips_csum_host_free(pinned));
+    report("ctx_validate_frames", host_ok && cpu_ok && zc_ok[0] && zc_ok[1],
+           std::string(", \"host\": ") + (host_ok ? "true" : "false") + ", \"cpu\": " +
+             (cpu_ok ? "true" : "false") + ", \"zc\": " + (zc_ok[0] ? "true" : "false") +
+             ", \"zc_resident\": " + (zc_ok[1] ? "true" : "false"));
+    // in-place generation of host frames: the valid frames' fields zeroed
+    std::vector<uint8_t> zeroed = arena;
+    std::vector<uint8_t> field_byte(arena.size(), 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      for (uint64_t at : { offs[i] + 24, offs[i] + 25, offs[i] + 50, offs[i] + 51 }) {
+        if (at < arena.size()) {
+          field_byte[at] = 1;
+          if (expect[i] == 0x0F) {
+            zeroed[at] = 0;
+          }
+        }
+      }
+    }
+    std::vector<uint8_t> gen = zeroed;
+    CS_OK(tulips_csum_generate_frames_host(ctx, gen.data(), offs.data(), lens.data(), n,
+                                           nullptr));
+    uint64_t restored_bad = 0, other_bad = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (expect[i] == 0x0F) {
+        for (uint64_t at : { offs[i] + 24, offs[i] + 25, offs[i] + 50, offs[i] + 51 }) {
+          restored_bad += gen[at] != arena[at];
+        }
+      }
+    }
+    for (size_t b = 0; b < arena.size(); ++b) {
+      other_bad += !field_byte[b] && gen[b] != zeroed[b];
+    }
+    report("ctx_generate_frames", restored_bad == 0 && other_bad == 0,
+           ", \"field_bytes_wrong\": " + std::to_string(restored_bad) +
+             ", \"other_bytes_changed\": " + std::to_string(other_bad));
+    // segmentation of host super-frames
+    const auto sarena = read_raw<uint8_t>(dir + "/seg.arena.bin");
+    const auto soffs = read_raw<uint64_t>(dir + "/seg.offsets.bin");
+    const auto slens = read_raw<uint16_t>(dir + "/seg.lengths.bin");
+    const auto params = read_raw<uint32_t>(dir + "/seg.params.bin");
+    const auto efirst = read_raw<uint32_t>(dir + "/seg.first.bin");
+    const auto eout = read_raw<uint8_t>(dir + "/seg.out.bin");
+    const auto elens = read_raw<uint16_t>(dir + "/seg.out_lengths.bin");
+    const uint32_t sn = uint32_t(soffs.size()), mss = params[0], stride = params[1];
+    const uint32_t total = efirst[sn];
+    std::vector<uint8_t> sout(size_t(total) * stride, 0x5B);
+    std::vector<uint16_t> solens(total, 0xA5A5);
+    std::vector<uint32_t> sfirst(sn + 1, 0xA5A5A5A5u);
+    CS_OK(tulips_csum_segment_frames_host(ctx, sarena.data(), soffs.data(), slens.data(), sn, mss,
+                                          sout.data(), stride, total, solens.data(),
+                                          sfirst.data()));
+    uint64_t bytes_bad = 0;
+    const bool plan_ok = sfirst == efirst && solens == elens;
+    if (plan_ok) {
+      for (uint32_t j = 0; j < total; ++j) {
+        for (uint32_t b = 0; b < elens[j]; ++b) {
+          bytes_bad += sout[size_t(j) * stride + b] != eout[size_t(j) * stride + b];
+        }
+      }
+    }
+    report("ctx_segment_frames", plan_ok && bytes_bad == 0,
+           std::string(", \"plan_ok\": ") + (plan_ok ? "true" : "false") +
+             ", \"bytes_wrong\": " + std::to_string(bytes_bad));
+    tulips_csum_ctx_destroy(ctx);
   }
   CS_OK(tulips_csum_release_stream(st));
   HIP_OK(hipStreamDestroy(st));

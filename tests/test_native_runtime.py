@@ -155,7 +155,7 @@ def test_native_section8f_kernels_against_fixtures(tmp_path, oracle):
     print(json.dumps(res, indent=1))
     assert res is not None, err
     bad = {k: v for k, v in res["fixtures"].items() if not v["ok"]}
-    assert rc == 0 and not bad and len(res["fixtures"]) == 5, (bad, err)
+    assert rc == 0 and not bad and len(res["fixtures"]) == 8, (bad, err)
 
 
 @pytest.mark.gpu
