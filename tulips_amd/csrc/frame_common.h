@@ -403,12 +403,17 @@ header_words(const u32x4& v0, int h0, int sub0, uint32_t (&F)[13])
   F[0] = F[1] = F[2] = 0;
 }
 
+// The frame's header fields from its first register row (header_words), and
+// the IPv4 header's LE 16-bit word sum (frame bytes 14..33, from the same
+// broadcast words: frame-relative, so the header starts at an even offset of
+// this word grid) folded to 32 bits.
 template<int G, int U>
 __device__ __forceinline__ Header
-frame_header(const FrameChunks<G, U>& fc, uint32_t flen, int sub0)
+frame_header_ip(const FrameChunks<G, U>& fc, uint32_t flen, int sub0, uint32_t& ipsum)
 {
   uint32_t F[13];
   header_words<G>(fc.v[0], fc.h0, sub0, F);
+  ipsum = fold64(uint64_t(F[3] >> 16) + F[4] + F[5] + F[6] + F[7] + (F[8] & 0xffffu));
   return parse_header<true>(
     [&](int k) -> uint32_t {
       return uint32_t(k) < flen ? (F[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
