@@ -354,6 +354,18 @@ read_raw(const std::string& path)
   return v;
 }
 
+// progress of `fixtures` on stderr (the driving test shows it when a run
+// fails or stalls)
+void
+phase(const char* what)
+{
+  static const auto t0 = std::chrono::steady_clock::now();
+  const double t =
+    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  fprintf(stderr, "[fixtures %.3f s] %s\n", t, what);
+  fflush(stderr);
+}
+
 int
 cmd_fixtures(const std::string& dir)
 {
@@ -368,6 +380,7 @@ cmd_fixtures(const std::string& dir)
   };
 
   // frames: validation, in-place generation, compact fields
+  phase("frames");
   {
     const auto arena = read_raw<uint8_t>(dir + "/frames.arena.bin");
     const auto offs = read_raw<uint64_t>(dir + "/frames.offsets.bin");
@@ -457,6 +470,7 @@ cmd_fixtures(const std::string& dir)
   }
 
   // Toeplitz RSS
+  phase("rss");
   {
     const auto sa = read_raw<uint32_t>(dir + "/rss.saddr.bin");
     const auto da = read_raw<uint32_t>(dir + "/rss.daddr.bin");
@@ -502,6 +516,7 @@ cmd_fixtures(const std::string& dir)
   }
 
   // segmentation against the oracle's segments
+  phase("segmentation");
   {
     const auto arena = read_raw<uint8_t>(dir + "/seg.arena.bin");
     const auto offs = read_raw<uint64_t>(dir + "/seg.offsets.bin");
@@ -544,6 +559,7 @@ cmd_fixtures(const std::string& dir)
     }
   }
   // the host-memory forms: the same fixtures through a host context
+  phase("host context");
   {
     const auto arena = read_raw<uint8_t>(dir + "/frames.arena.bin");
     const auto offs = read_raw<uint64_t>(dir + "/frames.offsets.bin");
@@ -556,10 +572,12 @@ cmd_fixtures(const std::string& dir)
       return std::equal(f.begin(), f.end(), expect.begin());
     };
     std::vector<uint8_t> f(n, 0xA5);
+    phase("ctx validate_frames_host");
     CS_OK(tulips_csum_validate_frames_host(ctx, arena.data(), offs.data(), lens.data(), n,
                                            f.data(), nullptr));
     const bool host_ok = flags_ok(f);
     std::fill(f.begin(), f.end(), 0xA5);
+    phase("validate_frames_cpu");
     CS_OK(tulips_csum_validate_frames_cpu(arena.data(), offs.data(), lens.data(), n, f.data(),
                                           nullptr));
     const bool cpu_ok = flags_ok(f);
@@ -569,7 +587,9 @@ cmd_fixtures(const std::string& dir)
     CS_OK(tulips_csum_host_alloc(arena.size(), &pinned));
     memcpy(pinned, arena.data(), arena.size());
     bool zc_ok[2] = { false, false };
+    phase("zc");
     for (int resident = 0; resident < 2; ++resident) {
+      phase(resident ? "zc resident" : "zc launch per burst");
       CS_OK(tulips_csum_ctx_set_lowlat(ctx, resident));
       std::fill(f.begin(), f.end(), 0xA5);
       for (uint32_t i = 0; i < n; i += TULIPS_CSUM_ZC_MAX_FRAMES) {
@@ -580,6 +600,7 @@ cmd_fixtures(const std::string& dir)
       }
       zc_ok[resident] = flags_ok(f);
     }
+    phase("zc back to launch per burst");
     CS_OK(tulips_csum_ctx_set_lowlat(ctx, 0));
     CS_OK(tulips_csum_host_free(pinned));
     report("ctx_validate_frames", host_ok && cpu_ok && zc_ok[0] && zc_ok[1],
@@ -600,6 +621,7 @@ cmd_fixtures(const std::string& dir)
       }
     }
     std::vector<uint8_t> gen = zeroed;
+    phase("ctx generate_frames_host");
     CS_OK(tulips_csum_generate_frames_host(ctx, gen.data(), offs.data(), lens.data(), n,
                                            nullptr));
     uint64_t restored_bad = 0, other_bad = 0;
@@ -629,6 +651,7 @@ cmd_fixtures(const std::string& dir)
     std::vector<uint8_t> sout(size_t(total) * stride, 0x5B);
     std::vector<uint16_t> solens(total, 0xA5A5);
     std::vector<uint32_t> sfirst(sn + 1, 0xA5A5A5A5u);
+    phase("ctx segment_frames_host");
     CS_OK(tulips_csum_segment_frames_host(ctx, sarena.data(), soffs.data(), slens.data(), sn, mss,
                                           sout.data(), stride, total, solens.data(),
                                           sfirst.data()));
@@ -644,10 +667,13 @@ cmd_fixtures(const std::string& dir)
     report("ctx_segment_frames", plan_ok && bytes_bad == 0,
            std::string(", \"plan_ok\": ") + (plan_ok ? "true" : "false") +
              ", \"bytes_wrong\": " + std::to_string(bytes_bad));
+    phase("ctx destroy");
     tulips_csum_ctx_destroy(ctx);
   }
+  phase("release");
   CS_OK(tulips_csum_release_stream(st));
   HIP_OK(hipStreamDestroy(st));
+  phase("done");
   out += "}, \"runtime\": " + runtime_json() + "}";
   printf("%s\n", out.c_str());
   return bad ? 1 : 0;

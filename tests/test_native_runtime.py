@@ -24,7 +24,11 @@ BATCHES = ("F1500", "F1500-tcp", "F9000", "F9000-tcp", "ZIPF", "ZIPF-tcp")
 def _run(*args, timeout=300):
     if not os.path.exists(EXE):
         pytest.fail(f"{EXE} is missing: `make native` (or __graft_entry__.build())")
-    p = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=timeout)
+    try:
+        p = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired as e:      # the stall's stderr names its phase
+        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
+        return -9, None, f"runtime_check {' '.join(args)}: no exit in {timeout} s\n{err}"
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     res = json.loads(lines[-1]) if lines else None
     return p.returncode, res, p.stderr
@@ -113,6 +117,39 @@ def test_native_calls_beside_a_global_mode_capture(golden):
     assert rc == 0 and res["capture_neutral"]["ok"], (res, err)
 
 
+def write_fixtures(d, oracle):
+    """The raw little-endian arrays `runtime_check fixtures` reads from d:
+    tests/golden/frames.npz and rss.npz as they are, and super-frames with
+    the oracle's segmentation of them."""
+    import numpy as np
+    from test_segment import pack as seg_pack, super_frame
+    d = str(d)
+    gdir = os.path.join(ROOT, "tests", "golden")
+    fr = np.load(os.path.join(gdir, "frames.npz"))
+    for k in ("arena", "offsets", "lengths", "expect"):
+        fr[k].tofile(os.path.join(d, f"frames.{k}.bin"))
+    rs = np.load(os.path.join(gdir, "rss.npz"))
+    for k in ("saddr", "daddr", "sport", "dport"):
+        rs[k].tofile(os.path.join(d, f"rss.{k}.bin"))
+    for i in range(len(rs["key_names"])):
+        rs[f"key_{i}"].tofile(os.path.join(d, f"rss.key_{i}.bin"))
+        for tag in ("init0", "initff"):
+            rs[f"expect_{i}_{tag}"].tofile(os.path.join(d, f"rss.expect_{i}_{tag}.bin"))
+    rng = np.random.default_rng(8)
+    payloads = [int(p) for p in rng.integers(1, 64000, 40)] + [1460, 1461, 2920, 0]
+    frames = [super_frame(oracle, rng, p) for p in payloads]
+    arena, offs, lens = seg_pack(frames, rng)
+    mss, stride = 1460, 2048
+    first, out, olens = oracle.segment_frames(arena, offs, lens, mss, stride)
+    arena.tofile(os.path.join(d, "seg.arena.bin"))
+    offs.tofile(os.path.join(d, "seg.offsets.bin"))
+    lens.tofile(os.path.join(d, "seg.lengths.bin"))
+    np.array([mss, stride], np.uint32).tofile(os.path.join(d, "seg.params.bin"))
+    first.tofile(os.path.join(d, "seg.first.bin"))
+    out.tofile(os.path.join(d, "seg.out.bin"))
+    olens.tofile(os.path.join(d, "seg.out_lengths.bin"))
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
 def test_native_section8f_kernels_against_fixtures(tmp_path, oracle):
@@ -124,34 +161,8 @@ def test_native_section8f_kernels_against_fixtures(tmp_path, oracle):
     against tests/golden/rss.npz (the reference's utils::toeplitz, 10 keys x 2
     inits), and segmentation against the oracle (orc_segment_frames; the LSO
     fix-ups are parity-unpinned)."""
-    import numpy as np
-    from test_segment import pack as seg_pack, super_frame
-    gdir = os.path.join(ROOT, "tests", "golden")
-    fr = np.load(os.path.join(gdir, "frames.npz"))
-    for k, name in (("arena", "arena"), ("offsets", "offsets"), ("lengths", "lengths"),
-                    ("expect", "expect")):
-        fr[k].tofile(tmp_path / f"frames.{name}.bin")
-    rs = np.load(os.path.join(gdir, "rss.npz"))
-    for k in ("saddr", "daddr", "sport", "dport"):
-        rs[k].tofile(tmp_path / f"rss.{k}.bin")
-    for i in range(len(rs["key_names"])):
-        rs[f"key_{i}"].tofile(tmp_path / f"rss.key_{i}.bin")
-        for tag in ("init0", "initff"):
-            rs[f"expect_{i}_{tag}"].tofile(tmp_path / f"rss.expect_{i}_{tag}.bin")
-    rng = np.random.default_rng(8)
-    payloads = [int(p) for p in rng.integers(1, 64000, 40)] + [1460, 1461, 2920, 0]
-    frames = [super_frame(oracle, rng, p) for p in payloads]
-    arena, offs, lens = seg_pack(frames, rng)
-    mss, stride = 1460, 2048
-    first, out, olens = oracle.segment_frames(arena, offs, lens, mss, stride)
-    arena.tofile(tmp_path / "seg.arena.bin")
-    offs.tofile(tmp_path / "seg.offsets.bin")
-    lens.tofile(tmp_path / "seg.lengths.bin")
-    np.array([mss, stride], np.uint32).tofile(tmp_path / "seg.params.bin")
-    first.tofile(tmp_path / "seg.first.bin")
-    out.tofile(tmp_path / "seg.out.bin")
-    olens.tofile(tmp_path / "seg.out_lengths.bin")
-    rc, res, err = _run("fixtures", str(tmp_path), timeout=240)
+    write_fixtures(tmp_path, oracle)
+    rc, res, err = _run("fixtures", str(tmp_path), timeout=90)
     print(json.dumps(res, indent=1))
     assert res is not None, err
     bad = {k: v for k, v in res["fixtures"].items() if not v["ok"]}

@@ -18,11 +18,12 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+import benchlib  # noqa: E402
 from tulips_amd import csum  # noqa: E402
 
 
@@ -41,7 +42,7 @@ def main():
     nsf, pay, mss = 1024, 44 * 1460, 1460
     sflen, sslot, sb = 54 + pay, 65536, 4
     sa = torch.empty(sb * nsf * sslot, dtype=torch.uint8, device=dev)
-    csum.fill_splitmix(sa, seed=0x7505)
+    benchlib.fill_splitmix(sa, seed=0x7505)
     sv = sa.view(sb * nsf, sslot)
     tot = sflen - 14
     for off, val in ((12, 0x08), (13, 0), (14, 0x45), (15, 0), (16, tot >> 8),

@@ -371,7 +371,7 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
   hw.b = next_chunk<G>(H, H, lane, sub0);
   hw.m = uint32_t(F.fa & 15);
 
-  uint64_t ip_acc = 0, l4_acc = 0;
+  uint64_t l4_acc = 0;
   u32x4 keep = {0, 0, 0, 0};
   // first: batch 0, whose slot u = 0 holds output chunks c = lane < G, the
   // only ones that can touch a header byte (hlen <= 94 < 16 * 16 <= 16 * G);
@@ -426,9 +426,7 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
       if (c == 3 && l4_on) {
         v.x &= 0x0000ffffu; // chksum = 0
       }
-      if (ip_on && cb < 34) {
-        ip_acc += masked_hsum(v, max(14 - cb, 0), min(34 - cb, 16));
-      }
+
       if (l4_on && cb + 16 > 34 && uint32_t(cb) < tcp_end) {
         l4_acc += masked_hsum(v, max(34 - cb, 0), min(int(tcp_end) - cb, 16));
       }
@@ -448,7 +446,17 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
     }
     load_batch(b0);
   }
-  const uint32_t ip = sub_sum<G>(fold64(ip_acc));
+  // The output IPv4 header's sum from the frame's header words every lane
+  // holds: bytes 14..33 with total length and id as written (bytes 16..19)
+  // and the checksum field zero (the output is 16-byte aligned, so the word
+  // grids agree); no masked sums over chunks 0..2 and no subgroup reduction
+  // for it (as frame_kernel; profiles/ab_frame_ip_header_r06.txt: 0.2-1.5 %
+  // per call serially here).
+  const uint32_t len_id = si.seg_ok ? (total >> 8) | ((total & 0xffu) << 8) |
+                                        ((id >> 8) << 16) | ((id & 0xffu) << 24)
+                                    : FW[4];
+  const uint32_t ip = fold64(uint64_t(FW[3] >> 16) + len_id + FW[5] +
+                             (FW[6] & 0xffff0000u) + FW[7] + (FW[8] & 0xffffu));
   const uint32_t l4 = sub_sum<G>(fold64(l4_acc));
   // lanes 0..3 write the first 64 bytes in one instruction: nontemporal
   // stores are not merged in L2, and separate stores of chunks 1 and 3 wrote
