@@ -421,34 +421,63 @@ frame_header_ip(const FrameChunks<G, U>& fc, uint32_t flen, int sub0, uint32_t& 
     flen);
 }
 
-// This lane's LE dword sum of the bytes at chunk-relative offsets [lo, hi)
-// (offsets from a0; the range must lie inside the frame). Only the first UM
-// rows of registers are looked at: a range known to end inside them (the
-// IPv4 header, UM = 1) skips the others at compile time. With UM == U,
-// bytes beyond the G*U chunks held in registers are loaded by a trailing
-// lane_sum (jumbo). (A branch-free form - whole chunks by select, the
-// boundary chunks picked by a runtime-indexed select - took 10 % fewer
-// instructions at 16 x 6 but spilled at 16 x 8 and 8 x 8/16, where
-// generation then ran 4x slower: profiles/probe_frames_r03.txt.)
+// This lane's sum of the bytes at chunk-relative offsets [lo, hi) (offsets
+// from a0; the range must lie inside the frame), as 32-bit accumulated
+// 16-bit halves (v_dot2: congruent to the LE dword sum mod 65535, at most
+// 8 * 0xffff per chunk, so no 64-bit adds), with byte masks only where a
+// chunk straddles lo or hi: the whole-chunk test is a compare and a select
+// per row, and the masked sum runs under a branch rows without a boundary
+// skip. Only the first UM rows of registers are looked at; with UM == U,
+// bytes beyond the G*U chunks held in registers are summed by a trailing
+// lane_sum (jumbo). (A branch-free form with 64-bit adds took 10 % fewer
+// instructions at 16 x 6 but spilled at 16 x 8 and 8 x 8/16:
+// profiles/probe_frames_r03.txt.)
+typedef unsigned short fr_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t
+dot2_acc(uint32_t x, uint32_t acc)
+{
+  const fr_u16x2 one = {1, 1};
+  fr_u16x2 h;
+  __builtin_memcpy(&h, &x, sizeof(h));
+  return __builtin_amdgcn_udot2(h, one, acc, false);
+}
+
+// bytes [ml, mh) of a dword, 0 <= ml, mh <= 4 (32-bit shifts only)
+__device__ __forceinline__ uint32_t
+dword_mask(int ml, int mh)
+{
+  const uint32_t below_h = mh >= 4 ? 0xffffffffu : (1u << (8 * mh)) - 1u;
+  const uint32_t below_l = ml >= 4 ? 0xffffffffu : (1u << (8 * ml)) - 1u;
+  return below_h & ~below_l;
+}
+
 template<int G, int U, bool NT, int UM = U>
-__device__ __forceinline__ uint64_t
-range_sum(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
+__device__ __forceinline__ uint32_t
+range_sum32(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
 {
   static_assert(UM >= 1 && UM <= U, "rows");
-  uint64_t acc = 0;
+  uint32_t acc = 0;
 #pragma unroll
   for (int u = 0; u < UM; ++u) {
     const int b = 16 * (lane + u * G);
-    const int l = max(lo - b, 0), h = min(hi - b, 16);
-    if (l < h) {
-      acc += (l == 0 && h == 16) ? hsum(fc.v[u]) : masked_hsum(fc.v[u], l, h);
+    const u32x4 v = fc.v[u];
+    const bool full = b >= lo && b + 16 <= hi;
+    const uint32_t w = dot2_acc(v.w, dot2_acc(v.z, dot2_acc(v.y, dot2_acc(v.x, 0u))));
+    acc += full ? w : 0u;
+    if (!full && b < hi && b + 16 > lo) {
+      const int l = max(lo - b, 0), h = min(hi - b, 16);
+      acc = dot2_acc(v.x & dword_mask(min(l, 4), min(h, 4)), acc);
+      acc = dot2_acc(v.y & dword_mask(min(max(l - 4, 0), 4), min(max(h - 4, 0), 4)), acc);
+      acc = dot2_acc(v.z & dword_mask(min(max(l - 8, 0), 4), min(max(h - 8, 0), 4)), acc);
+      acc = dot2_acc(v.w & dword_mask(min(max(l - 12, 0), 4), min(max(h - 12, 0), 4)), acc);
     }
   }
   if constexpr (UM == U) {
     constexpr int held = 16 * G * U;
     if (hi > held) {
       const int from = max(lo, held);
-      acc += lane_sum<G, U, NT>(fc.a0 + uintptr_t(from), uint32_t(hi - from), lane);
+      acc += fold64(lane_sum<G, U, NT>(fc.a0 + uintptr_t(from), uint32_t(hi - from), lane));
     }
   }
   return acc;
