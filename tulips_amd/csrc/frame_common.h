@@ -403,6 +403,22 @@ header_words(const u32x4& v0, int h0, int sub0, uint32_t (&F)[13])
   F[0] = F[1] = F[2] = 0;
 }
 
+// Header bytes past the frame end read as 0 (parse_header's contract): the
+// words are masked once, and only for frames shorter than the 52 bytes they
+// hold (a test per subgroup), instead of a compare and a select per byte
+// read (the frame kernels' per-frame VALU count is what bounds them).
+__device__ __forceinline__ void
+mask_past_end(uint32_t (&F)[13], uint32_t flen)
+{
+  if (flen < 52u) {
+#pragma unroll
+    for (int j = 3; j < 13; ++j) {
+      const int n = min(max(int(flen) - 4 * j, 0), 4);
+      F[j] &= n >= 4 ? 0xffffffffu : (1u << (8 * n)) - 1u;
+    }
+  }
+}
+
 // The frame's header fields from its first register row (header_words), and
 // the IPv4 header's LE 16-bit word sum (frame bytes 14..33, from the same
 // broadcast words: frame-relative, so the header starts at an even offset of
@@ -413,12 +429,10 @@ frame_header_ip(const FrameChunks<G, U>& fc, uint32_t flen, int sub0, uint32_t& 
 {
   uint32_t F[13];
   header_words<G>(fc.v[0], fc.h0, sub0, F);
+  mask_past_end(F, flen);
   ipsum = fold64(uint64_t(F[3] >> 16) + F[4] + F[5] + F[6] + F[7] + (F[8] & 0xffffu));
   return parse_header<true>(
-    [&](int k) -> uint32_t {
-      return uint32_t(k) < flen ? (F[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
-    },
-    flen);
+    [&](int k) -> uint32_t { return (F[k >> 2] >> (8 * (k & 3))) & 0xffu; }, flen);
 }
 
 // This lane's sum of the bytes at chunk-relative offsets [lo, hi) (offsets

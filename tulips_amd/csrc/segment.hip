@@ -334,11 +334,9 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
   // ---- header fields (chunks 0..4 from lanes 0..4) -------------------------
   uint32_t FW[13];
   header_words<G>(H, int(F.fa - F.lo), sub0, FW);
+  mask_past_end(FW, F.flen);
   const Header h = parse_header<true>(
-    [&](int b) -> uint32_t {
-      return uint32_t(b) < F.flen ? (FW[b >> 2] >> (8 * (b & 3))) & 0xffu : 0u;
-    },
-    F.flen);
+    [&](int b) -> uint32_t { return (FW[b >> 2] >> (8 * (b & 3))) & 0xffu; }, F.flen);
   if constexpr (!KNOWN) {
     si = seg_info(h, mss);
     slice = si.seg_ok && k < si.nseg ? min(mss, si.payload - k * mss) : 0u;
