@@ -466,6 +466,22 @@ dword_mask(int ml, int mh)
   return below_h & ~below_l;
 }
 
+// acc plus the 16-bit halves of v (all 16 bytes, or bytes [lo, hi) only)
+__device__ __forceinline__ uint32_t
+chunk_dot2(u32x4 v, uint32_t acc)
+{
+  return dot2_acc(v.w, dot2_acc(v.z, dot2_acc(v.y, dot2_acc(v.x, acc))));
+}
+
+__device__ __forceinline__ uint32_t
+masked_dot2(u32x4 v, int l, int h, uint32_t acc)
+{
+  acc = dot2_acc(v.x & dword_mask(min(l, 4), min(h, 4)), acc);
+  acc = dot2_acc(v.y & dword_mask(min(max(l - 4, 0), 4), min(max(h - 4, 0), 4)), acc);
+  acc = dot2_acc(v.z & dword_mask(min(max(l - 8, 0), 4), min(max(h - 8, 0), 4)), acc);
+  return dot2_acc(v.w & dword_mask(min(max(l - 12, 0), 4), min(max(h - 12, 0), 4)), acc);
+}
+
 template<int G, int U, bool NT, int UM = U>
 __device__ __forceinline__ uint32_t
 range_sum32(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
@@ -477,14 +493,10 @@ range_sum32(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
     const int b = 16 * (lane + u * G);
     const u32x4 v = fc.v[u];
     const bool full = b >= lo && b + 16 <= hi;
-    const uint32_t w = dot2_acc(v.w, dot2_acc(v.z, dot2_acc(v.y, dot2_acc(v.x, 0u))));
+    const uint32_t w = chunk_dot2(v, 0u);
     acc += full ? w : 0u;
     if (!full && b < hi && b + 16 > lo) {
-      const int l = max(lo - b, 0), h = min(hi - b, 16);
-      acc = dot2_acc(v.x & dword_mask(min(l, 4), min(h, 4)), acc);
-      acc = dot2_acc(v.y & dword_mask(min(max(l - 4, 0), 4), min(max(h - 4, 0), 4)), acc);
-      acc = dot2_acc(v.z & dword_mask(min(max(l - 8, 0), 4), min(max(h - 8, 0), 4)), acc);
-      acc = dot2_acc(v.w & dword_mask(min(max(l - 12, 0), 4), min(max(h - 12, 0), 4)), acc);
+      acc = masked_dot2(v, max(lo - b, 0), min(hi - b, 16), acc);
     }
   }
   if constexpr (UM == U) {

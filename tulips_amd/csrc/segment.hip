@@ -369,7 +369,7 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
   hw.b = next_chunk<G>(H, H, lane, sub0);
   hw.m = uint32_t(F.fa & 15);
 
-  uint64_t l4_acc = 0;
+  uint32_t l4_acc = 0; // 16-bit halves, 32-bit v_dot2 accumulation (as range_sum32)
   u32x4 keep = {0, 0, 0, 0};
   // first: batch 0, whose slot u = 0 holds output chunks c = lane < G, the
   // only ones that can touch a header byte (hlen <= 94 < 16 * 16 <= 16 * G);
@@ -396,8 +396,8 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
           v = keep_bytes(v, int(dlen) - cb);
         }
         if (l4_on && uint32_t(cb) < tcp_end) {
-          l4_acc += uint32_t(cb + 16) <= tcp_end ? hsum(v)
-                                                  : masked_hsum(v, 0, int(tcp_end) - cb);
+          l4_acc = uint32_t(cb + 16) <= tcp_end ? chunk_dot2(v, l4_acc)
+                                                 : masked_dot2(v, 0, int(tcp_end) - cb, l4_acc);
         }
         store_chunk(dst + cb, v);
         continue;
@@ -426,7 +426,7 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
       }
 
       if (l4_on && cb + 16 > 34 && uint32_t(cb) < tcp_end) {
-        l4_acc += masked_hsum(v, max(34 - cb, 0), min(int(tcp_end) - cb, 16));
+        l4_acc = masked_dot2(v, max(34 - cb, 0), min(int(tcp_end) - cb, 16), l4_acc);
       }
       if (c < 4) {
         keep = v;   // line 0 (chunks 0..3) is stored whole after the sums
@@ -455,7 +455,7 @@ build_segment(const SegFrame& F, uint32_t k, uint32_t j, uint32_t mss, uint8_t* 
                                     : FW[4];
   const uint32_t ip = fold64(uint64_t(FW[3] >> 16) + len_id + FW[5] +
                              (FW[6] & 0xffff0000u) + FW[7] + (FW[8] & 0xffffu));
-  const uint32_t l4 = sub_sum<G>(fold64(l4_acc));
+  const uint32_t l4 = sub_sum<G>(fold32(l4_acc));
   // lanes 0..3 write the first 64 bytes in one instruction: nontemporal
   // stores are not merged in L2, and separate stores of chunks 1 and 3 wrote
   // that line to HBM three times
