@@ -487,16 +487,20 @@ __device__ __forceinline__ uint32_t
 range_sum32(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
 {
   static_assert(UM >= 1 && UM <= U, "rows");
+  static_assert(G >= 4, "lo (< 64) lies in the first row");
   uint32_t acc = 0;
 #pragma unroll
   for (int u = 0; u < UM; ++u) {
     const int b = 16 * (lane + u * G);
     const u32x4 v = fc.v[u];
     const bool full = b >= lo && b + 16 <= hi;
-    const uint32_t w = chunk_dot2(v, 0u);
-    acc += full ? w : 0u;
+    const uint32_t with = chunk_dot2(v, acc); // (chained through acc: one live temporary)
+    acc = full ? with : acc;
     if (!full && b < hi && b + 16 > lo) {
-      acc = masked_dot2(v, max(lo - b, 0), min(hi - b, 16), acc);
+      // rows past the first start past lo (lo < 16 * G: the frame's header),
+      // so only their upper bound cuts a chunk
+      acc = u == 0 ? masked_dot2(v, max(lo - b, 0), min(hi - b, 16), acc)
+                   : masked_dot2(v, 0, min(hi - b, 16), acc);
     }
   }
   if constexpr (UM == U) {
@@ -507,6 +511,47 @@ range_sum32(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
     }
   }
   return acc;
+}
+
+
+// The same with 64-bit LE dword sums and per-row masks: kept for the
+// geometries with 16 rows per lane (8 x 16), where range_sum32's extra
+// temporaries cost a VGPR spill at their 128-register budget.
+template<int G, int U, bool NT, int UM = U>
+__device__ __forceinline__ uint64_t
+range_sum64(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
+{
+  static_assert(UM >= 1 && UM <= U, "rows");
+  uint64_t acc = 0;
+#pragma unroll
+  for (int u = 0; u < UM; ++u) {
+    const int b = 16 * (lane + u * G);
+    const int l = max(lo - b, 0), h = min(hi - b, 16);
+    if (l < h) {
+      acc += (l == 0 && h == 16) ? hsum(fc.v[u]) : masked_hsum(fc.v[u], l, h);
+    }
+  }
+  if constexpr (UM == U) {
+    constexpr int held = 16 * G * U;
+    if (hi > held) {
+      const int from = max(lo, held);
+      acc += lane_sum<G, U, NT>(fc.a0 + uintptr_t(from), uint32_t(hi - from), lane);
+    }
+  }
+  return acc;
+}
+
+// A lane's share of the TCP range [lo, hi), folded to 32 bits: range_sum32,
+// or range_sum64 for the 16-row geometries.
+template<int G, int U, bool NT>
+__device__ __forceinline__ uint32_t
+tcp_range_part(const FrameChunks<G, U>& fc, int lane, int lo, int hi)
+{
+  if constexpr (U > 8) {
+    return fold64(range_sum64<G, U, NT>(fc, lane, lo, hi));
+  } else {
+    return fold32(range_sum32<G, U, NT>(fc, lane, lo, hi));
+  }
 }
 
 } // namespace frame

@@ -119,8 +119,8 @@ frame_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
     const bool do_l4 = h.tcp && !h.trunc && (!GENERATE || h.tcplen >= 18u);
     // (32-bit v_dot2 accumulation, masks on the boundary chunks only: 4
     // branches +1.5 % against 64-bit adds, profiles/ab_frame_ip_header_r06.txt)
-    const uint32_t l4_part = sub_sum<FG>(fold32(
-      do_l4 ? range_sum32<FG, FU, NT>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen)) : 0u));
+    const uint32_t l4_part = sub_sum<FG>(
+      do_l4 ? tcp_range_part<FG, FU, NT>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen)) : 0u);
     // generation: both field values, on every lane (the sums and the header
     // are subgroup-uniform)
     uint32_t ipv = 0, l4v = 0;
@@ -374,8 +374,8 @@ zc_server_kernel(ZcMailbox* mb, ZcArgs args)
       const int h0 = fc.h0;
       const bool do_l4 = h.tcp && !h.trunc;
       const uint32_t ip_part = h.ipv4 ? ipsum : 0u;
-      const uint32_t l4_part = sub_sum<FG>(fold32(
-        do_l4 ? range_sum32<FG, FU, false>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen)) : 0u));
+      const uint32_t l4_part = sub_sum<FG>(
+        do_l4 ? tcp_range_part<FG, FU, false>(fc, lane, h0 + 34, h0 + 34 + int(h.tcplen)) : 0u);
       if (lane == 0) {
         const bool ip_ok = h.ipv4 && finish(ip_part, false, MODE_INET, 0, 0, 0, 20) == 0xffffu;
         const bool l4_ok = do_l4 && finish(l4_part, ((fa + 34) & 1) != 0, MODE_TCP, 0, h.src,
