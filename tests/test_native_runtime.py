@@ -21,17 +21,45 @@ EXE = os.path.join(ROOT, "tests", "native", "_build", "runtime_check")
 BATCHES = ("F1500", "F1500-tcp", "F9000", "F9000-tcp", "ZIPF", "ZIPF-tcp")
 
 
+def _threads(pid):
+    """Each thread's state and kernel wait channel (/proc), taken from a
+    stalled checker before it is killed: a thread parked in the amdgpu
+    driver names a GPU wait, one in a futex a host-side lock."""
+    out = []
+    try:
+        for tid in sorted(os.listdir(f"/proc/{pid}/task"), key=int):
+            base = f"/proc/{pid}/task/{tid}"
+            try:
+                with open(f"{base}/comm") as f:
+                    comm = f.read().strip()
+                with open(f"{base}/stat") as f:
+                    state = f.read().rsplit(")", 1)[1].split()[0]
+                with open(f"{base}/wchan") as f:
+                    wchan = f.read().strip() or "-"
+            except OSError:
+                continue
+            out.append(f"{tid} {comm} {state} {wchan}")
+    except OSError as e:
+        out.append(f"/proc/{pid}: {e}")
+    return "\n".join(out)
+
+
 def _run(*args, timeout=300):
     if not os.path.exists(EXE):
         pytest.fail(f"{EXE} is missing: `make native` (or __graft_entry__.build())")
+    p = subprocess.Popen([EXE, *args], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True)
     try:
-        p = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=timeout)
-    except subprocess.TimeoutExpired as e:      # the stall's stderr names its phase
-        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
-        return -9, None, f"runtime_check {' '.join(args)}: no exit in {timeout} s\n{err}"
-    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:           # the stall's stderr names its phase
+        threads = _threads(p.pid)
+        p.kill()
+        out, err = p.communicate()
+        return -9, None, (f"runtime_check {' '.join(args)}: no exit in {timeout} s\n"
+                          f"threads (tid comm state wchan):\n{threads}\n{err}")
+    lines = [x for x in out.splitlines() if x.startswith("{")]
     res = json.loads(lines[-1]) if lines else None
-    return p.returncode, res, p.stderr
+    return p.returncode, res, err
 
 
 def test_zipf_lengths_match_the_spec(golden):
